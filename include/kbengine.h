@@ -1,0 +1,181 @@
+/*
+ * kbengine.h -- C ABI of the MI355X kafkabalancer move-search engine.
+ *
+ * This is the drop-in boundary for the reference's step pipeline
+ * (balancer.go:34-65).  The reference seam is the step signature
+ *     func(*PartitionList, RebalanceConfig) (*PartitionList, error)
+ * dispatched by Balance() (balancer.go:49-65).  A host (the cgo shim shown in
+ * INTEGRATION.md, the C++ host library in kafkabalancer_amd/csrc/host, or the
+ * Python mirror) marshals a PartitionList into kb_cluster once, then asks the
+ * engine for one Balance() step at a time (kb_engine_balance) or for a whole
+ * -max-reassign plan that stays resident on the GPU (kb_engine_plan).
+ *
+ * All entry points are plain C: pointers + sizes, no HIP or torch types.
+ * Return values: >= 0 success (status), < 0 a KB_ERR_* code; the text of the
+ * last error is available from kb_engine_last_error().
+ */
+#ifndef KBENGINE_H
+#define KBENGINE_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KB_ABI_VERSION 1
+
+/* step indices == position in the reference's steps table (balancer.go:34-44) */
+enum kb_step {
+    KB_STEP_VALIDATE_WEIGHTS = 0,     /* steps.go:7-23 */
+    KB_STEP_VALIDATE_REPLICAS = 1,    /* steps.go:27-36 */
+    KB_STEP_FILL_DEFAULTS = 2,        /* steps.go:39-66 */
+    KB_STEP_REMOVE_EXTRA = 3,         /* steps.go:70-89 */
+    KB_STEP_ADD_MISSING = 4,          /* steps.go:93-113 */
+    KB_STEP_MOVE_DISALLOWED = 5,      /* steps.go:117-143 */
+    KB_STEP_REASSIGN_LEADERS = 6,     /* steps.go:301-307 -> distributeLeaders :234-282 */
+    KB_STEP_MOVE_LEADERS = 7,         /* steps.go:292-298 -> move(leaders=true) */
+    KB_STEP_MOVE_NON_LEADERS = 8      /* steps.go:286-288 -> move(leaders=false) */
+};
+
+/* kb_change.status / return value of kb_engine_balance */
+enum { KB_NOCHANGE = 0, KB_CHANGE = 1 };
+
+/* kinds of change (what replacepl/addpl did, utils.go:166-202) */
+enum { KB_KIND_NONE = 0, KB_KIND_REPLACE = 1, KB_KIND_REMOVE = 2, KB_KIND_ADD = 3, KB_KIND_SWAP = 4 };
+
+/* how a change reaches the partition list */
+enum {
+    KB_SEM_APPLIED = 0,   /* every change is applied to the state (default) */
+    KB_SEM_GO = 1         /* emulate Go slice aliasing: a remove shifts in place and keeps
+                             the slice length (duplicates the last replica), an add is not
+                             visible to the next call (utils.go:178,199-202) */
+};
+
+/* error codes */
+enum {
+    KB_OK = 0,
+    KB_ERR_INVALID = -1,        /* bad arguments */
+    KB_ERR_HIP = -2,            /* HIP runtime error / no device */
+    KB_ERR_UNSUPPORTED = -3,    /* outside the engine's sizing limits */
+    KB_ERR_STEP = -4,           /* a step returned an error (Balance() error); see last_error */
+    KB_ERR_CAPACITY = -5,       /* a per-broker list or the contender buffer overflowed */
+    KB_ERR_PANIC = -6           /* input on which the reference Go code panics */
+};
+
+/* Cluster state, the marshalled PartitionList (kafkabalancer.go:40-58).
+ * Arrays are host memory; the engine copies them to the device once. */
+typedef struct {
+    int64_t n_partitions;
+    const int64_t *replica_ids;     /* concatenated Replicas of all partitions */
+    const int64_t *replica_off;     /* [n_partitions + 1] offsets into replica_ids */
+    const double *weight;           /* [n] Weight (0 = absent) */
+    const int64_t *num_replicas;    /* [n] NumReplicas (0 = absent) */
+    const int64_t *num_consumers;   /* [n] NumConsumers (may be NULL => all 0) */
+    int64_t n_sets;                 /* distinct Brokers lists */
+    const int64_t *set_ids;         /* concatenated Brokers lists */
+    const int64_t *set_off;         /* [n_sets + 1] */
+    const int64_t *set_idx;         /* [n] index of the partition's Brokers list, -1 = nil */
+    /* optional, used only to format error messages like the reference */
+    const char *topic_blob;         /* concatenated topic names (may be NULL) */
+    const int64_t *topic_off;       /* [n + 1] */
+    const int64_t *partition_id;    /* [n] PartitionID (may be NULL) */
+} kb_cluster;
+
+/* RebalanceConfig (balancer.go:12-20) plus engine options */
+typedef struct {
+    int32_t allow_leader;           /* AllowLeaderRebalancing */
+    int32_t rebalance_leaders;      /* RebalanceLeaders */
+    int64_t min_replicas;           /* MinReplicasForRebalancing */
+    double min_unbalance;           /* MinUnbalance */
+    const int64_t *brokers;         /* Brokers (explicit -broker-ids) */
+    int64_t n_brokers;
+    int32_t brokers_nil;            /* 1 => Brokers == nil ("auto") */
+    int32_t semantics;              /* KB_SEM_* */
+    int32_t device;                 /* HIP device ordinal */
+    int32_t list_slack;             /* extra entries per broker list (0 = default 1024) */
+    int64_t shard_begin;            /* partitions [shard_begin, shard_end) scanned by this */
+    int64_t shard_end;              /*   engine; 0,0 = all (multi-GPU sharding) */
+} kb_config;
+
+/* One step's result: the change Balance() would return (balancer.go:49-65). */
+typedef struct {
+    int32_t status;                 /* KB_NOCHANGE / KB_CHANGE / < 0 error */
+    int32_t step;                   /* kb_step that produced it (or failed) */
+    int32_t kind;                   /* KB_KIND_* */
+    int32_t slot;                   /* replica slot that changed */
+    int64_t partition;              /* index into the cluster's partition list */
+    int64_t from_broker;            /* broker id replaced/removed (-1 for add) */
+    int64_t to_broker;              /* broker id placed/added (-1 for remove) */
+    double unbalance_before;        /* su: getUnbalanceBL before the step (move steps) */
+    double unbalance_after;         /* cu: scored unbalance of the chosen move */
+    int32_t exact;                  /* 1 if unbalance_after is the exact sequential fold */
+    int32_t err_code;               /* engine-internal error detail */
+    int64_t err_broker;             /* broker id named in the error message */
+} kb_change;
+
+typedef struct {
+    int64_t steps;                  /* steps executed */
+    int64_t candidates;             /* (partition, slot, target) moves scored (SURVEY 8d metric 1) */
+    int64_t contenders;             /* near-tie candidates verified with exact folds */
+    int64_t exact_folds;            /* exact getUnbalanceBL evaluations */
+    int64_t scan_bytes;             /* algorithmic bytes read by the scan kernel, last step */
+    double device_ms;               /* device time of the last kb_engine_plan (HIP events) */
+    int64_t n_brokers;              /* dense broker universe size */
+    int64_t n_sets;
+    int32_t integral;               /* 1 => loads are exact under incremental updates */
+    int32_t max_replicas;           /* replica slots per partition on the device */
+} kb_stats;
+
+typedef struct kb_engine kb_engine;
+
+/* ABI version of the loaded library (== KB_ABI_VERSION) */
+int kb_abi_version(void);
+
+/* Validates + fills defaults like ValidateWeights/ValidateReplicas/FillDefaults
+ * (steps.go:7-66) and uploads the SoA state.  A validation error does not fail
+ * creation: it is returned by the first kb_engine_balance(), like Balance(). */
+int kb_engine_create(const kb_cluster *cluster, const kb_config *cfg, kb_engine **out);
+
+/* One Balance() call: runs the fused step pipeline on the device, applies the
+ * change to the device state (per cfg->semantics), returns KB_CHANGE /
+ * KB_NOCHANGE or < 0.  Equivalent of balancer.go:49-65 + the aliasing write. */
+int kb_engine_balance(kb_engine *e, kb_change *out);
+
+/* Device-resident plan: up to max_steps Balance() calls without host
+ * round trips (run()'s loop with -complete-partition=false,
+ * kafkabalancer.go:181-221).  Stops after the first no-change or error.
+ * Writes the changes to out[0..*n_out).  Returns the last status. */
+int kb_engine_plan(kb_engine *e, int64_t max_steps, kb_change *out, int64_t *n_out);
+
+/* Current replicas of partition i (after applied changes); returns the count. */
+int64_t kb_engine_replicas(kb_engine *e, int64_t i, int64_t *buf, int64_t cap);
+
+/* Exact broker loads (getBrokerLoad, utils.go:92-105) for the dense universe;
+ * ids[k], loads[k] for k < return value. */
+int64_t kb_engine_loads(kb_engine *e, int64_t *ids, double *loads, int64_t cap);
+
+/* getUnbalanceBL (utils.go:119-147) of the current state over bl_move order */
+double kb_engine_unbalance(kb_engine *e);
+
+int kb_engine_stats(kb_engine *e, kb_stats *out);
+
+/* Reference-format message of the last error ("<Step>: partition Partition(t,p,[..]) ..."). */
+int kb_engine_last_error(kb_engine *e, char *buf, size_t n);
+
+void kb_engine_destroy(kb_engine *e);
+
+/* ---- multi-GPU step phases (one engine per rank, partitions sharded) ----
+ * A step is:  begin (local scan) -> exchange of fixed-size summaries between
+ * ranks (all-gather, done by the caller over RCCL) -> finish (identical
+ * resolution on every rank).  `summary` and `gathered` are DEVICE pointers. */
+int64_t kb_engine_summary_bytes(kb_engine *e);
+int kb_engine_step_begin(kb_engine *e, void *summary_dev);
+int kb_engine_step_finish(kb_engine *e, const void *gathered_dev, int32_t n_ranks, kb_change *out);
+/* hipStream_t on which all engine work is enqueued (NULL = engine-owned stream) */
+int kb_engine_set_stream(kb_engine *e, void *hip_stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,1081 @@
+// kernels.hip -- CDNA4 (gfx950) kernels of the kafkabalancer move-search engine.
+//
+// One Balance() step (balancer.go:49-65) is five launches on one stream:
+//   k_prep      1 WG   sort brokers by (load, id) (getBL, utils.go:107-117), exact
+//                      sequential folds of su (getUnbalanceBL, utils.go:119-147),
+//                      per-broker score terms, error bound eps
+//   k_setlists  nsets waves: per allowed-broker set, the first/last brokers of
+//                      the set in bl order (move targets, steps.go:257-266; Add and
+//                      Disallowed picks, steps.go:102,130-134)
+//   k_scan      P/1024 WGs  HBM stream over the SoA partition arrays: the Remove /
+//                      Add / Disallowed / distributeLeaders first-index predicates and
+//                      the O(1)-delta score of every leader / non-leader move
+//                      (steps.go:232-288), block minima, grid minima by atomicMin
+//   k_census    P/1024 WGs  re-visits only the workgroups whose minimum is within
+//                      8*eps of the grid minimum and emits every near-tie candidate
+//   k_resolve   1 WG   exact verification of near ties (sequential folds in bl order,
+//                      strict-< first minimum in (partition, slot, target) order,
+//                      steps.go:276), the step decision in the reference's step order,
+//                      and the on-device apply (replacepl/addpl, utils.go:166-202) with
+//                      an exact partition-ordered refold of touched broker loads
+//                      (getBrokerLoad, utils.go:92-105).
+//
+// Exactness: every value the reference's decision depends on is either computed
+// with the reference's own operation order (IEEE binary64, no FMA: the file is
+// built with -ffp-contract=off; true division), or bounded by eps and resolved
+// exactly when the bound does not decide (DESIGN.md "Exactness").
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <cfloat>
+#include "engine_dev.h"
+#include "kernels_api.h"
+
+namespace kbe {
+
+// --------------------------------------------------------------- helpers
+
+__device__ __forceinline__ unsigned long long d2u(double d) { return (unsigned long long)__double_as_longlong(d); }
+__device__ __forceinline__ double u2d(unsigned long long u) { return __longlong_as_double((long long)u); }
+
+// order-preserving encoding of a double into u64 (for atomicMin)
+__device__ __forceinline__ unsigned long long enc(double d) {
+    unsigned long long u = d2u(d);
+    return (u >> 63) ? ~u : (u | 0x8000000000000000ull);
+}
+__device__ __forceinline__ double dec(unsigned long long e) {
+    unsigned long long u = (e >> 63) ? (e & 0x7FFFFFFFFFFFFFFFull) : ~e;
+    return u2d(u);
+}
+
+// reference term (utils.go:136-143): r = L/avg - 1; r>0 ? r*r : r*r/2 (exact ops)
+__device__ __forceinline__ double term_x(double L, double avg) {
+    double r = L / avg - 1.0;
+    if (r > 0) return r * r;
+    return r * r / 2;
+}
+// approximate term used for scoring (error covered by eps)
+__device__ __forceinline__ double term_a(double L, double inv_avg) {
+    double r = __fma_rn(L, inv_avg, -1.0);
+    double q = r * r;
+    return r > 0 ? q : 0.5 * q;
+}
+
+__device__ __forceinline__ bool setbit(const uint64_t* sb, int b) {
+    return (sb[b >> 6] >> (b & 63)) & 1ull;
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_min(T v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) { T x = __shfl_xor(v, o); v = x < v ? x : v; }
+    return v;
+}
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+// getUnbalanceBL (utils.go:119-147) of the bl_move order with bl[s] -= w and
+// bl[t] += w (steps.go:250,272): two sequential folds, exact reference order.
+__device__ double exact_unbalance(const int32_t* __restrict__ blm, int nblm,
+                                  const double* __restrict__ load, int s, int t, double w) {
+    double Ls = s >= 0 ? load[s] - w : 0.0;
+    double Lt = t >= 0 ? load[t] + w : 0.0;
+    double S = 0.0;
+    for (int k = 0; k < nblm; k++) {
+        int b = blm[k];
+        double L = b == s ? Ls : (b == t ? Lt : load[b]);
+        S += L;
+    }
+    double avg = S / (double)nblm;
+    double U = 0.0;
+    for (int k = 0; k < nblm; k++) {
+        int b = blm[k];
+        double L = b == s ? Ls : (b == t ? Lt : load[b]);
+        double r = L / avg - 1.0;
+        if (r > 0) U += r * r;
+        else U += r * r / 2;
+    }
+    return U;
+}
+
+// --------------------------------------------------------------- k_prep
+
+
+__global__ __launch_bounds__(PREP_THREADS) void k_prep(PrepArgs a) {
+    extern __shared__ __align__(16) unsigned char smem[];
+    const int NP2 = a.NP2;
+    unsigned long long* keys = (unsigned long long*)smem;        // NP2
+    double* Tm = (double*)(keys + NP2);                           // NP2
+    uint32_t* idx = (uint32_t*)(Tm + NP2);                        // NP2
+    __shared__ double s_red[PREP_THREADS / 64];
+    __shared__ int s_wcnt[PREP_THREADS / 64];
+    __shared__ double s_avg, s_S, s_U0;
+    __shared__ int s_nblm;
+    DevCtl* ctl = a.ctl;
+    const int tid = threadIdx.x;
+    if (ctl->halted) return;
+    if (tid == 0) {
+        ctl->gmin[0] = ctl->gmin[1] = NONE64;
+        for (int f = 0; f < NF; f++) ctl->first[f] = NONE32;
+        ctl->ncand[0] = ctl->ncand[1] = 0;
+        ctl->ncont = 0;
+        ctl->cont_overflow = 0;
+    }
+    for (int i = tid; i < NP2; i += PREP_THREADS) {
+        if (i < a.B) { keys[i] = d2u(a.load[i]); idx[i] = (uint32_t)i; }
+        else { keys[i] = NONE64; idx[i] = NONE32; }
+    }
+    __syncthreads();
+    // bitonic sort by (load bits, dense id); loads are finite and >= 0, so the
+    // IEEE bit pattern orders like the value (byBrokerLoad.Less, utils.go:23-28)
+    for (int k = 2; k <= NP2; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = tid; i < NP2; i += PREP_THREADS) {
+                int ixj = i ^ j;
+                if (ixj > i) {
+                    unsigned long long ki = keys[i], kj = keys[ixj];
+                    uint32_t ii = idx[i], ij = idx[ixj];
+                    bool less = (kj < ki) || (kj == ki && ij < ii);
+                    bool up = (i & k) == 0;
+                    if (up == less) { keys[i] = kj; keys[ixj] = ki; idx[i] = ij; idx[ixj] = ii; }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    // compaction of the bl_move subsequence (NP2 <= 4096 => 4 elements / thread)
+    int base = tid * 4;
+    int flag[4]; unsigned long long kv[4]; uint32_t iv[4];
+    int c = 0;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        int i = base + q;
+        flag[q] = 0;
+        kv[q] = 0; iv[q] = NONE32;
+        if (i < a.B) {
+            uint32_t b = idx[i];
+            kv[q] = keys[i]; iv[q] = b;
+            a.order[i] = (int32_t)b;
+            flag[q] = (a.cnt[b] > 0 || a.incfg[b]) ? 1 : 0;
+            c += flag[q];
+        }
+    }
+    // block exclusive scan of c
+    const int lane = tid & 63, wid = tid >> 6;
+    int incl = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) { int y = __shfl_up(incl, o); if (lane >= o) incl += y; }
+    if (lane == 63) s_wcnt[wid] = incl;
+    __syncthreads();
+    int woff = 0, total = 0;
+    for (int w = 0; w < PREP_THREADS / 64; w++) { if (w < wid) woff += s_wcnt[w]; total += s_wcnt[w]; }
+    int pos = woff + incl - c;
+    __syncthreads();   // all reads of keys[] done before the in-place compaction
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        int i = base + q;
+        if (i < a.B) {
+            uint32_t b = iv[q];
+            if (flag[q]) { keys[pos] = kv[q]; a.blm[pos] = (int32_t)b; a.posm[b] = pos; pos++; }
+            else a.posm[b] = -1;
+        }
+    }
+    if (tid == 0) s_nblm = total;
+    __syncthreads();
+    const int nblm = s_nblm;
+    const double* Lm = (const double*)keys;
+    // S: sequential fold in bl order (utils.go:123-128)
+    if (tid == 0) {
+        double S = 0.0;
+        for (int k = 0; k < nblm; k++) S += Lm[k];
+        s_S = S;
+        s_avg = S / (double)nblm;
+    }
+    __syncthreads();
+    const double avg = s_avg;
+    for (int k = tid; k < nblm; k += PREP_THREADS) Tm[k] = term_x(Lm[k], avg);
+    __syncthreads();
+    // su: sequential fold of the terms (utils.go:134-143)
+    if (tid == 0) {
+        double U = 0.0;
+        for (int k = 0; k < nblm; k++) U += Tm[k];
+        s_U0 = U;
+    }
+    // error-bound ingredients: V = sum |r|(1+|r|), Rmax = max |r|
+    const double inv_avg = 1.0 / avg;
+    double v = 0.0, rm = 0.0;
+    for (int k = tid; k < nblm; k += PREP_THREADS) {
+        double r = fabs(Lm[k] * inv_avg - 1.0);
+        v += r * (1.0 + r);
+        rm = r > rm ? r : rm;
+    }
+    v = wave_sum(v);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) { double x = __shfl_xor(rm, o); rm = x > rm ? x : rm; }
+    if (lane == 0) s_red[wid] = v;
+    __syncthreads();
+    double V = 0.0;
+    for (int w = 0; w < PREP_THREADS / 64; w++) V += s_red[w];
+    __syncthreads();
+    if (lane == 0) s_red[wid] = rm;
+    __syncthreads();
+    double Rm = 0.0;
+    for (int w = 0; w < PREP_THREADS / 64; w++) Rm = s_red[w] > Rm ? s_red[w] : Rm;
+    for (int b = tid; b < a.B; b += PREP_THREADS) {
+        double L = a.load[b];
+        a.LT[b] = make_double2(L, a.posm[b] >= 0 ? term_a(L, inv_avg) : 0.0);
+    }
+    if (tid == 0) {
+        const double u = DBL_EPSILON / 2;
+        double R = Rm + a.rmax_w * inv_avg;
+        double eps = 64.0 * u * ((double)(nblm + 8) * (s_U0 + 2.0 * V) + 4.0 * (1.0 + R) * (1.0 + R));
+        if (!(eps > 1e-300)) eps = 1e-300;
+        ctl->S = s_S; ctl->avg = avg; ctl->inv_avg = inv_avg; ctl->U0 = s_U0;
+        ctl->V = V; ctl->eps = eps; ctl->nblm = nblm;
+        ctl->heavy = nblm > 0 ? a.blm[nblm - 1] : -1;
+        ctl->light = nblm > 0 ? a.blm[0] : -1;
+    }
+}
+
+// ------------------------------------------------------------ k_setlists
+
+
+__global__ __launch_bounds__(256) void k_setlists(SetArgs a) {
+    if (a.ctl->halted) return;
+    const int lane = threadIdx.x & 63;
+    const int set = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (set >= a.nsets) return;
+    const uint64_t* sb = a.setbits + (size_t)set * a.W64;
+    int32_t* L = a.lists + (size_t)set * 3 * a.K;
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    for (int kind = 0; kind < 3; kind++) {
+        int found = 0;
+        for (int base = 0; base < a.B && found < a.K; base += 64) {
+            int k = base + lane;
+            bool mem = false;
+            int b = -1;
+            if (k < a.B) {
+                b = a.order[kind == 0 ? k : a.B - 1 - k];
+                mem = setbit(sb, b);
+                if (kind == 0) mem = mem && (a.cnt[b] > 0 || a.incfg[b]);
+                else if (kind == 1) mem = mem && a.cnt[b] > 0;
+            }
+            unsigned long long m = __ballot(mem);
+            if (mem) {
+                int r = found + __popcll(m & lt);
+                if (r < a.K) L[kind * a.K + r] = b;
+            }
+            found += __popcll(m);
+        }
+        for (int r = found + lane; r < a.K; r += 64) L[kind * a.K + r] = -1;
+    }
+    int n = 0;
+    for (int base = 0; base < a.B; base += 64) {
+        int b = base + lane;
+        bool mem = b < a.B && setbit(sb, b) && (a.cnt[b] > 0 || a.incfg[b]);
+        n += __popcll(__ballot(mem));
+    }
+    if (lane == 0) a.nelig[set] = n;
+}
+
+// --------------------------------------------------------------- k_scan
+
+
+template <int RC>
+struct PartRegs {
+    double w[PER_LANE];
+    uint32_t m[PER_LANE];
+    uint32_t r[RC][PER_LANE];
+};
+
+template <int RC>
+__device__ __forceinline__ void load_parts(const ScanArgs& a, long long base, PartRegs<RC>& P) {
+    const double2 w01 = *(const double2*)(a.w + base);
+    const double2 w23 = *(const double2*)(a.w + base + 2);
+    P.w[0] = w01.x; P.w[1] = w01.y; P.w[2] = w23.x; P.w[3] = w23.y;
+    const uint4 m4 = *(const uint4*)(a.meta + base);
+    P.m[0] = m4.x; P.m[1] = m4.y; P.m[2] = m4.z; P.m[3] = m4.w;
+#pragma unroll
+    for (int k = 0; k < RC; k++) {
+        const uint2 r2 = *(const uint2*)(a.rep + (long long)k * a.Ppad + base);
+        P.r[k][0] = r2.x & 0xFFFFu; P.r[k][1] = r2.x >> 16;
+        P.r[k][2] = r2.y & 0xFFFFu; P.r[k][3] = r2.y >> 16;
+    }
+}
+
+// first target in bl_move order that is allowed and not a replica (steps.go:257-266)
+template <int RC>
+__device__ __forceinline__ int first_target(const int32_t* al, int K, const uint32_t (&reps)[RC], int nrep, int skip) {
+    int found = 0;
+    for (int i = 0; i < K; i++) {
+        int b = al[i];
+        if (b < 0) return -1;
+        bool isrep = false;
+#pragma unroll
+        for (int k = 0; k < RC; k++) isrep |= (k < nrep) && ((int)reps[k] == b);
+        if (!isrep) { if (found == skip) return b; found++; }
+    }
+    return -1;
+}
+
+template <int RC>
+__global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
+    DevCtl* ctl = a.ctl;
+    if (ctl->halted) return;
+    const double inv_avg = ctl->inv_avg;
+    const int heavy = ctl->heavy;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const long long base = a.shard_begin + (long long)blockIdx.x * TILE + (long long)tid * PER_LANE;
+
+    PartRegs<RC> P;
+    load_parts<RC>(a, base, P);
+
+    double dminL = HUGE_VAL, dminN = HUGE_VAL;
+    uint32_t fst[NF];
+#pragma unroll
+    for (int f = 0; f < NF; f++) fst[f] = NONE32;
+    unsigned long long cL = 0, cN = 0;
+
+#pragma unroll
+    for (int j = 0; j < PER_LANE; j++) {
+        const long long p = base + j;
+        if (p >= a.shard_end) continue;
+        const uint32_t m = P.m[j];
+        const int nrep = (int)meta_nrep(m), want = (int)meta_want(m);
+        const int elig = (int)meta_elig(m), set = (int)meta_set(m);
+        uint32_t reps[RC];
+#pragma unroll
+        for (int k = 0; k < RC; k++) reps[k] = P.r[k][j];
+        const uint32_t pi = (uint32_t)p;
+        if (a.sem_go) {
+            bool dup = false;
+#pragma unroll
+            for (int x = 0; x < RC; x++)
+#pragma unroll
+                for (int y = x + 1; y < RC; y++) dup |= (y < nrep) && reps[x] == reps[y];
+            if (dup) fst[F_DUP] = min(fst[F_DUP], pi);
+        }
+        if (want < nrep) fst[F_REMOVE] = min(fst[F_REMOVE], pi);
+        if (want > nrep) fst[F_ADD] = min(fst[F_ADD], pi);
+        if (nrep == 0) {
+            fst[F_EMPTY] = min(fst[F_EMPTY], pi);
+            if (elig) fst[F_EMPTY_ELIG] = min(fst[F_EMPTY_ELIG], pi);
+        }
+        const uint64_t* sb = a.setbits + (size_t)set * a.W64;
+        bool dis = false;
+        int nin = 0;
+#pragma unroll
+        for (int k = 0; k < RC; k++) {
+            if (k < nrep) {
+                bool in = setbit(sb, (int)reps[k]);
+                dis |= !in;
+                nin += in ? 1 : 0;
+            }
+        }
+        if (dis) fst[F_DIS] = min(fst[F_DIS], pi);
+        if (a.rebalance && elig && nrep > 0 && (int)reps[0] == heavy) fst[F_LEAD] = min(fst[F_LEAD], pi);
+        if (elig && nrep > 0) {
+            const int32_t* al = a.lists + (size_t)set * 3 * a.K;
+            const int t = first_target<RC>(al, a.K, reps, nrep, 0);
+            if (t >= 0) {
+                const unsigned long long ne = (unsigned long long)(a.nelig[set] - nin);
+                const double wv = P.w[j];
+                const double2 lt = a.LT[t];
+                const double dt = term_a(lt.x + wv, inv_avg) - lt.y;
+                if (a.allow_leader) {
+                    const double2 ls = a.LT[reps[0]];
+                    const double d = (term_a(ls.x - wv, inv_avg) - ls.y) + dt;
+                    dminL = d < dminL ? d : dminL;
+                    cL += ne;
+                }
+#pragma unroll
+                for (int k = 1; k < RC; k++) {
+                    if (k < nrep) {
+                        const double2 ls = a.LT[reps[k]];
+                        const double d = (term_a(ls.x - wv, inv_avg) - ls.y) + dt;
+                        dminN = d < dminN ? d : dminN;
+                    }
+                }
+                cN += ne * (unsigned long long)(nrep - 1);
+            }
+        }
+    }
+    // workgroup reduction: wave shuffles, then LDS across the 4 waves
+    __shared__ double s_d[2][SCAN_THREADS / 64];
+    __shared__ uint32_t s_f[NF][SCAN_THREADS / 64];
+    __shared__ unsigned long long s_c[2][SCAN_THREADS / 64];
+    dminL = wave_min(dminL);
+    dminN = wave_min(dminN);
+    cL = wave_sum(cL);
+    cN = wave_sum(cN);
+#pragma unroll
+    for (int f = 0; f < NF; f++) fst[f] = wave_min(fst[f]);
+    if (lane == 0) {
+        s_d[0][wid] = dminL; s_d[1][wid] = dminN;
+        s_c[0][wid] = cL; s_c[1][wid] = cN;
+#pragma unroll
+        for (int f = 0; f < NF; f++) s_f[f][wid] = fst[f];
+    }
+    __syncthreads();
+    if (tid == 0) {
+        for (int x = 1; x < SCAN_THREADS / 64; x++) {
+            dminL = s_d[0][x] < dminL ? s_d[0][x] : dminL;
+            dminN = s_d[1][x] < dminN ? s_d[1][x] : dminN;
+            cL += s_c[0][x]; cN += s_c[1][x];
+#pragma unroll
+            for (int f = 0; f < NF; f++) fst[f] = min(fst[f], s_f[f][x]);
+        }
+        a.blockrec[blockIdx.x] = make_double2(dminL, dminN);
+        if (dminL < HUGE_VAL) atomicMin(&ctl->gmin[0], enc(dminL));
+        if (dminN < HUGE_VAL) atomicMin(&ctl->gmin[1], enc(dminN));
+#pragma unroll
+        for (int f = 0; f < NF; f++) if (fst[f] != NONE32) atomicMin(&ctl->first[f], fst[f]);
+        if (cL) atomicAdd(&ctl->ncand[0], cL);
+        if (cN) atomicAdd(&ctl->ncand[1], cN);
+    }
+}
+
+// ------------------------------------------------------------- k_census
+
+__device__ __forceinline__ void emit(const ScanArgs& a, int kind, int s, int t, double w,
+                                     unsigned long long iter) {
+    uint32_t i = atomicAdd(&a.ctl->ncont, 1u);
+    if (i < a.cont_cap) {
+        Contender c;
+        c.s = s; c.t = t; c.w = w; c.iter = iter; c.kind = kind; c.pad = 0;
+        a.cont[i] = c;
+    } else {
+        a.ctl->cont_overflow = 1;
+    }
+}
+
+// walk every allowed, non-replica target in bl_move order for one (partition, slot)
+// and emit the ones within 4*eps of the minimum; stop once 8*eps is exceeded
+// (the approximate delta is monotone in the target load up to 2*eps).
+template <int RC>
+__device__ void walk_targets(const ScanArgs& a, int kind, long long p, int slot, int src,
+                             const uint32_t (&reps)[RC], int nrep, const uint64_t* sb, double wv,
+                             double ds, double g, double eps, int nblm, double inv_avg) {
+    for (int k = 0; k < nblm; k++) {
+        const int b = a.blm[k];
+        if (!setbit(sb, b)) continue;
+        bool isrep = false;
+#pragma unroll
+        for (int q = 0; q < RC; q++) isrep |= (q < nrep) && ((int)reps[q] == b);
+        if (isrep) continue;
+        const double2 lt = a.LT[b];
+        const double d = ds + (term_a(lt.x + wv, inv_avg) - lt.y);
+        if (d <= g + 4.0 * eps)
+            emit(a, kind, src, b, wv, ((unsigned long long)p << 21) | ((unsigned long long)slot << 16) | (unsigned long long)k);
+        if (d > g + 8.0 * eps) break;
+    }
+}
+
+template <int RC>
+__global__ __launch_bounds__(SCAN_THREADS) void k_census(ScanArgs a) {
+    DevCtl* ctl = a.ctl;
+    if (ctl->halted) return;
+    const double eps = ctl->eps;
+    const unsigned long long eL = ctl->gmin[0], eN = ctl->gmin[1];
+    const double gL = eL == NONE64 ? HUGE_VAL : dec(eL);
+    const double gN = eN == NONE64 ? HUGE_VAL : dec(eN);
+    const double2 br = a.blockrec[blockIdx.x];
+    const bool doL = a.allow_leader && eL != NONE64 && br.x <= gL + 8.0 * eps;
+    const bool doN = eN != NONE64 && br.y <= gN + 8.0 * eps;
+    if (!doL && !doN) return;
+    const double inv_avg = ctl->inv_avg;
+    const int nblm = ctl->nblm;
+    const long long base = a.shard_begin + (long long)blockIdx.x * TILE + (long long)threadIdx.x * PER_LANE;
+    PartRegs<RC> P;
+    load_parts<RC>(a, base, P);
+#pragma unroll
+    for (int j = 0; j < PER_LANE; j++) {
+        const long long p = base + j;
+        if (p >= a.shard_end) continue;
+        const uint32_t m = P.m[j];
+        const int nrep = (int)meta_nrep(m), elig = (int)meta_elig(m), set = (int)meta_set(m);
+        if (!elig || nrep == 0) continue;
+        uint32_t reps[RC];
+#pragma unroll
+        for (int k = 0; k < RC; k++) reps[k] = P.r[k][j];
+        const int32_t* al = a.lists + (size_t)set * 3 * a.K;
+        const int t = first_target<RC>(al, a.K, reps, nrep, 0);
+        if (t < 0) continue;
+        const uint64_t* sb = a.setbits + (size_t)set * a.W64;
+        const double wv = P.w[j];
+        const double2 lt = a.LT[t];
+        const double dt = term_a(lt.x + wv, inv_avg) - lt.y;
+        if (doL) {
+            const double2 ls = a.LT[reps[0]];
+            const double ds = term_a(ls.x - wv, inv_avg) - ls.y;
+            if (ds + dt <= gL + 8.0 * eps)
+                walk_targets<RC>(a, 0, p, 0, (int)reps[0], reps, nrep, sb, wv, ds, gL, eps, nblm, inv_avg);
+        }
+        if (doN) {
+#pragma unroll
+            for (int k = 1; k < RC; k++) {
+                if (k < nrep) {
+                    const double2 ls = a.LT[reps[k]];
+                    const double ds = term_a(ls.x - wv, inv_avg) - ls.y;
+                    if (ds + dt <= gN + 8.0 * eps)
+                        walk_targets<RC>(a, 1, p, k, (int)reps[k], reps, nrep, sb, wv, ds, gN, eps, nblm, inv_avg);
+                }
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------ k_resolve
+
+
+struct Decision {
+    int32_t status, step, kind, slot;
+    long long part;
+    int32_t from, to;
+    double su, cu;
+    int32_t exact, err, err_broker, pad;
+};
+
+__device__ __forceinline__ double contribution(const ResolveArgs& a, uint32_t q, int b) {
+    const uint32_t m = a.meta[q];
+    const int lead = a.rep[q] == (uint16_t)b;   // slot 0 of partition q
+    const double w = a.w[q];
+    if (lead) return w * (double)((int)meta_nrep(m) + a.nc[q]);
+    return w;
+}
+
+// remove partition q from broker b's list (block-wide, all threads call)
+__device__ void list_remove(const ResolveArgs& a, int b, uint32_t q, int* s_i) {
+    const uint32_t st = a.lstart[b], n = a.llen[b];
+    if (threadIdx.x == 0) *s_i = -1;
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < n; i += RESOLVE_THREADS)
+        if (a.lent[st + i] == q) *s_i = (int)i;
+    __syncthreads();
+    const int at = *s_i;
+    if (at < 0) return;
+    for (uint32_t c = (uint32_t)at; c + 1 < n; c += RESOLVE_THREADS) {
+        uint32_t j = c + threadIdx.x;
+        uint32_t v = 0;
+        bool act = j + 1 < n;
+        if (act) v = a.lent[st + j + 1];
+        __syncthreads();
+        if (act) a.lent[st + j] = v;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) a.llen[b] = n - 1;
+    __syncthreads();
+}
+
+// insert partition q into broker b's sorted list
+__device__ bool list_insert(const ResolveArgs& a, int b, uint32_t q, int* s_i) {
+    const uint32_t st = a.lstart[b], n = a.llen[b];
+    if (n >= a.lcap[b]) return false;
+    if (threadIdx.x == 0) *s_i = 0;
+    __syncthreads();
+    int c = 0;
+    for (uint32_t i = threadIdx.x; i < n; i += RESOLVE_THREADS) c += a.lent[st + i] < q ? 1 : 0;
+    c = wave_sum(c);
+    if ((threadIdx.x & 63) == 0 && c) atomicAdd(s_i, c);
+    __syncthreads();
+    const uint32_t at = (uint32_t)*s_i;
+    // shift [at, n) right by one, processing chunks from the end
+    long long hi = (long long)n;
+    while (hi > (long long)at) {
+        long long lo = hi - RESOLVE_THREADS;
+        if (lo < (long long)at) lo = at;
+        long long j = lo + threadIdx.x;
+        bool act = j < hi;
+        uint32_t v = 0;
+        if (act) v = a.lent[st + j];
+        __syncthreads();
+        if (act) a.lent[st + j + 1] = v;
+        __syncthreads();
+        hi = lo;
+    }
+    if (threadIdx.x == 0) { a.lent[st + at] = q; a.llen[b] = n + 1; }
+    __syncthreads();
+    return true;
+}
+
+__global__ __launch_bounds__(RESOLVE_THREADS) void k_resolve(ResolveArgs a) {
+    DevCtl* ctl = a.ctl;
+    if (ctl->halted) return;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    constexpr int NW = RESOLVE_THREADS / 64;
+    __shared__ Decision D;
+    __shared__ int s_done, s_i;
+    __shared__ unsigned long long s_u[NW];
+    __shared__ double s_dv[NW];
+    __shared__ int s_flag[NW];
+    __shared__ int s_idx;
+    __shared__ double s_fold[8][1024];           // refold staging (non-integral mode)
+    const double su = ctl->U0;
+    const double eps = ctl->eps;
+    const int nblm = ctl->nblm;
+
+    if (tid == 0) {
+        D.status = 0; D.step = -1; D.kind = 0; D.slot = -1; D.part = -1;
+        D.from = -1; D.to = -1; D.su = su; D.cu = su; D.exact = 1; D.err = E_NONE; D.err_broker = -1;
+        s_done = 0;
+        const uint32_t* F = ctl->first;
+        auto rd = [&](uint32_t p, int k) -> int { return (int)a.rep[(long long)k * a.Ppad + p]; };
+        if (a.sem_go && F[F_DUP] != NONE32) {
+            D.status = -1; D.step = 1; D.err = E_DUP; D.part = F[F_DUP]; s_done = 1;
+        } else if (F[F_REMOVE] != NONE32) {                      // steps.go:70-89
+            uint32_t p = F[F_REMOVE];
+            uint32_t m = a.meta[p];
+            int nrep = (int)meta_nrep(m), set = (int)meta_set(m);
+            const uint64_t* sb = a.setbits + (size_t)set * a.W64;
+            int best = -1, bslot = -1;
+            for (int k = 0; k < nrep; k++) {
+                int b = rd(p, k);
+                if (!setbit(sb, b)) continue;
+                if (best < 0 || a.load[b] < a.load[best] || (a.load[b] == a.load[best] && b < best)) { best = b; bslot = k; }
+            }
+            D.step = 3; D.part = p;
+            if (best < 0) { D.status = -1; D.err = E_REMOVE; }
+            else {
+                // replacepl removes the FIRST slot holding that broker (utils.go:167-178)
+                D.status = 1; D.kind = 2; D.slot = bslot; D.from = best; D.to = -1;
+            }
+            s_done = 1;
+        } else if (F[F_ADD] != NONE32) {                         // steps.go:93-113
+            uint32_t p = F[F_ADD];
+            uint32_t m = a.meta[p];
+            int nrep = (int)meta_nrep(m), set = (int)meta_set(m);
+            const int32_t* dl = a.lists + ((size_t)set * 3 + 2) * a.K;
+            int t = -1;
+            for (int i = 0; i < a.K && t < 0; i++) {
+                int b = dl[i];
+                if (b < 0) break;
+                bool isrep = false;
+                for (int k = 0; k < nrep; k++) isrep |= rd(p, k) == b;
+                if (!isrep) t = b;
+            }
+            D.step = 4; D.part = p;
+            if (t < 0) { D.status = -1; D.err = E_ADD; }
+            else { D.status = 1; D.kind = 3; D.slot = nrep; D.from = -1; D.to = t; }
+            s_done = 1;
+        } else if (F[F_DIS] != NONE32) {                         // steps.go:117-143
+            uint32_t p = F[F_DIS];
+            uint32_t m = a.meta[p];
+            int nrep = (int)meta_nrep(m), set = (int)meta_set(m);
+            const uint64_t* sb = a.setbits + (size_t)set * a.W64;
+            int vslot = -1;
+            for (int k = 0; k < nrep && vslot < 0; k++) if (!setbit(sb, rd(p, k))) vslot = k;
+            const int32_t* dl = a.lists + ((size_t)set * 3 + 1) * a.K;
+            int t = -1;
+            for (int i = 0; i < a.K && t < 0; i++) {
+                int b = dl[i];
+                if (b < 0) break;
+                bool isrep = false;
+                for (int k = 0; k < nrep; k++) isrep |= rd(p, k) == b;
+                if (!isrep) t = b;
+            }
+            D.step = 5; D.part = p; D.slot = vslot; D.from = rd(p, vslot);
+            if (t < 0) { D.status = -1; D.err = E_DIS; D.err_broker = D.from; }
+            else { D.status = 1; D.kind = 1; D.to = t; }
+            s_done = 1;
+        } else if (a.rebalance && !(su < a.min_unbalance)) {     // steps.go:299-347
+            if (F[F_EMPTY] != NONE32 || nblm == 0) {
+                D.status = -1; D.step = 6; D.err = E_PANIC; D.part = F[F_EMPTY]; s_done = 1;
+            } else if (F[F_LEAD] != NONE32) {
+                uint32_t p = F[F_LEAD];
+                uint32_t m = a.meta[p];
+                int nrep = (int)meta_nrep(m);
+                int light = ctl->light;
+                int ex = -1;
+                for (int k = 0; k < nrep && ex < 0; k++) if (rd(p, k) == light) ex = k;
+                D.status = 1; D.step = 6; D.part = p; D.slot = 0; D.from = rd(p, 0); D.to = light;
+                D.kind = (ex > 0) ? 4 : 1;      // swap when bl[0] is already a replica
+                if (ex == 0) D.kind = 4;        // replacing the leader with itself: no-op swap
+                s_done = 1;
+            }
+        }
+    }
+    __syncthreads();
+
+    // move(): leader step (if allowed), then non-leader step (steps.go:284-298)
+    for (int kind = a.allow_leader ? 0 : 1; kind < 2 && !s_done; kind++) {
+        const int step = kind == 0 ? 7 : 8;
+        if (tid == 0 && ctl->first[F_EMPTY_ELIG] != NONE32) {
+            D.status = -1; D.step = step; D.err = E_PANIC; D.part = ctl->first[F_EMPTY_ELIG]; s_done = 1;
+        }
+        if (tid == 0 && ctl->cont_overflow) {
+            D.status = -1; D.step = step; D.err = E_CONT_OVERFLOW; s_done = 1;
+        }
+        __syncthreads();
+        if (s_done) break;
+        const uint32_t nc = min(ctl->ncont, a.cont_cap);
+        // (1) earliest contender of this kind and whether all share its key
+        unsigned long long mi = NONE64;
+        int midx = -1;
+        for (uint32_t i = tid; i < nc; i += RESOLVE_THREADS) {
+            const Contender c = a.cont[i];
+            if (c.kind == kind && c.iter < mi) { mi = c.iter; midx = (int)i; }
+        }
+        unsigned long long wm = wave_min(mi);
+        if (lane == 0) s_u[wid] = wm;
+        __syncthreads();
+        if (tid == 0) {
+            unsigned long long x = NONE64;
+            for (int q = 0; q < NW; q++) x = s_u[q] < x ? s_u[q] : x;
+            s_u[0] = x;
+            s_idx = -1;
+        }
+        __syncthreads();
+        if (mi == s_u[0] && mi != NONE64) s_idx = midx;
+        __syncthreads();
+        const int i0 = s_idx;
+        bool have = i0 >= 0;
+        int same = 1;
+        Contender c0;
+        c0.s = c0.t = -1; c0.w = 0; c0.iter = NONE64; c0.kind = kind; c0.pad = 0;
+        if (have) {
+            c0 = a.cont[i0];
+            for (uint32_t i = tid; i < nc; i += RESOLVE_THREADS) {
+                const Contender c = a.cont[i];
+                if (c.kind == kind && !(c.s == c0.s && c.t == c0.t && d2u(c.w) == d2u(c0.w))) same = 0;
+            }
+        }
+        int allsame = __syncthreads_and(same);
+        double Ustar = su;
+        unsigned long long witer = NONE64;
+        int wi = -1, exact = 1;
+        const double thr = su - a.min_unbalance;          // steps.go:292
+        if (have && allsame) {
+            // one key: every contender scores the same exact U; first in iteration order wins
+            const double2 ls = make_double2(a.load[c0.s], 0.0);
+            const double inv_avg = ctl->inv_avg;
+            // approximate U of the key, same formula as the scan
+            double ts = term_a(a.load[c0.s], inv_avg), tt = term_a(a.load[c0.t], inv_avg);
+            double d = (term_a(ls.x - c0.w, inv_avg) - ts) + (term_a(a.load[c0.t] + c0.w, inv_avg) - tt);
+            double Ua = su + d;
+            witer = c0.iter; wi = i0;
+            const double lim = thr < su ? thr : su;
+            if (Ua + 2.0 * eps < lim) { Ustar = Ua; exact = 0; }
+            else if (Ua - 2.0 * eps >= (thr > su ? thr : su)) { Ustar = Ua; exact = 0; }
+            else {
+                if (tid == 0) s_dv[0] = exact_unbalance(a.blm, nblm, a.load, c0.s, c0.t, c0.w);
+                __syncthreads();
+                Ustar = s_dv[0];
+                if (tid == 0) atomicAdd(&ctl->total_folds, 1ull);
+            }
+        } else if (have) {
+            // several keys: exact sequential fold for every contender, lexicographic min
+            double bu = HUGE_VAL;
+            unsigned long long bi = NONE64;
+            int bx = -1;
+            unsigned long long nf = 0;
+            for (uint32_t i = tid; i < nc; i += RESOLVE_THREADS) {
+                const Contender c = a.cont[i];
+                if (c.kind != kind) continue;
+                double u = exact_unbalance(a.blm, nblm, a.load, c.s, c.t, c.w);
+                nf++;
+                if (u < bu || (u == bu && c.iter < bi)) { bu = u; bi = c.iter; bx = (int)i; }
+            }
+            nf = wave_sum(nf);
+            if (lane == 0 && nf) atomicAdd(&ctl->total_folds, nf);
+            // block lexicographic argmin over (u, iter)
+            for (int o = 32; o > 0; o >>= 1) {
+                double ou = __shfl_xor(bu, o);
+                unsigned long long oi = __shfl_xor(bi, o);
+                int ox = __shfl_xor(bx, o);
+                if (ou < bu || (ou == bu && oi < bi)) { bu = ou; bi = oi; bx = ox; }
+            }
+            if (lane == 0) { s_dv[wid] = bu; s_u[wid] = bi; s_flag[wid] = bx; }
+            __syncthreads();
+            if (tid == 0) {
+                for (int q = 1; q < NW; q++)
+                    if (s_dv[q] < s_dv[0] || (s_dv[q] == s_dv[0] && s_u[q] < s_u[0])) {
+                        s_dv[0] = s_dv[q]; s_u[0] = s_u[q]; s_flag[0] = s_flag[q];
+                    }
+            }
+            __syncthreads();
+            Ustar = s_dv[0]; witer = s_u[0]; wi = s_flag[0];
+        }
+        __syncthreads();
+        if (tid == 0) {
+            // cu starts at su and only a strictly smaller u replaces it (steps.go:227-229,276)
+            const bool improved = have && Ustar < su;
+            const double cu = improved ? Ustar : su;
+            if (cu < thr) {
+                if (!improved) {
+                    // replacepl on the zero Partition: the reference panics
+                    D.status = -1; D.step = step; D.err = E_PANIC; s_done = 1;
+                } else {
+                    const Contender c = a.cont[wi];
+                    D.status = 1; D.step = step; D.kind = 1;
+                    D.part = (long long)(witer >> 21); D.slot = (int)((witer >> 16) & 31);
+                    D.from = c.s; D.to = c.t; D.su = su; D.cu = cu; D.exact = exact;
+                    s_done = 1;
+                }
+            }
+        }
+        __syncthreads();
+    }
+
+    // ---------------------------------------------------------- apply
+    __shared__ int s_aff[2 * MAXR + 2];
+    __shared__ double s_oldc[2 * MAXR + 2];
+    __shared__ int s_naff;
+    if (tid == 0) {
+        s_naff = 0;
+        if (D.status == 1) {
+            const long long p = D.part;
+            const uint32_t m = a.meta[p];
+            int nrep = (int)meta_nrep(m);
+            int r[MAXR + 1];
+            for (int k = 0; k < nrep; k++) r[k] = (int)a.rep[(long long)k * a.Ppad + p];
+            const double wv = a.w[p];
+            const int ncp = a.nc[p];
+            // old contributions of every broker of p
+            for (int k = 0; k < nrep; k++) {
+                s_aff[s_naff] = r[k];
+                s_oldc[s_naff] = k == 0 ? wv * (double)(nrep + ncp) : wv;
+                s_naff++;
+            }
+            int nn = nrep;
+            bool state_changed = true;
+            if (D.kind == 1) {                       // replace at slot (utils.go:186-190)
+                r[D.slot] = D.to;
+            } else if (D.kind == 4) {                // swap with the existing replica (utils.go:179-185)
+                int ex = -1;
+                for (int k = 0; k < nrep; k++) if (r[k] == D.to) ex = k;
+                int old = r[D.slot];
+                r[D.slot] = D.to;
+                r[ex] = old;
+                D.slot = D.slot;
+            } else if (D.kind == 2) {                // remove (utils.go:176-178)
+                for (int k = D.slot; k + 1 < nrep; k++) r[k] = r[k + 1];
+                if (a.sem_go) state_changed = false; // pl keeps its length: duplicates
+                else nn = nrep - 1;
+            } else if (D.kind == 3) {                // add (utils.go:199-202)
+                if (a.sem_go) state_changed = false; // append is not visible through pl
+                else { r[nrep] = D.to; nn = nrep + 1; }
+            }
+            if (a.sem_go && (D.kind == 2 || D.kind == 3)) {
+                // Go aliasing: the remove shifted the shared backing array in place
+                if (D.kind == 2) for (int k = 0; k < nrep; k++) a.rep[(long long)k * a.Ppad + p] = (uint16_t)r[k];
+                s_naff = 0;
+            } else if (state_changed) {
+                for (int k = 0; k < nn; k++) a.rep[(long long)k * a.Ppad + p] = (uint16_t)r[k];
+                a.meta[p] = make_meta((uint32_t)nn, meta_want(m), meta_elig(m), meta_set(m));
+                if (D.kind == 1) { a.cnt[D.from]--; a.cnt[D.to]++; }
+                if (D.kind == 2) { a.cnt[D.from]--; }
+                if (D.kind == 3) { a.cnt[D.to]++; }
+                // new contributions; integral mode updates loads incrementally (exact)
+                int base_aff = s_naff;
+                for (int k = 0; k < nn; k++) {
+                    int b = r[k];
+                    double c = k == 0 ? wv * (double)(nn + ncp) : wv;
+                    int f = -1;
+                    for (int x = 0; x < base_aff; x++) if (s_aff[x] == b) f = x;
+                    if (f >= 0) {
+                        if (s_oldc[f] == c) { s_aff[f] = -1 - s_aff[f]; }  // unchanged contribution
+                        else { if (a.integral) a.load[b] = (a.load[b] - s_oldc[f]) + c; }
+                    } else {
+                        if (a.integral) a.load[b] = a.load[b] + c;
+                        s_aff[s_naff] = b; s_oldc[s_naff] = 0.0; s_naff++;
+                    }
+                }
+                for (int x = 0; x < base_aff; x++) {
+                    int b = s_aff[x];
+                    if (b < 0) continue;
+                    bool still = false;
+                    for (int k = 0; k < nn; k++) still |= r[k] == b;
+                    if (!still && a.integral) a.load[b] = a.load[b] - s_oldc[x];
+                }
+                // compact affected set (brokers whose contribution changed)
+                int n2 = 0;
+                for (int x = 0; x < s_naff; x++) if (s_aff[x] >= 0) s_aff[n2++] = s_aff[x];
+                s_naff = n2;
+            } else {
+                s_naff = 0;
+            }
+        }
+    }
+    __syncthreads();
+    // non-integral: maintain per-broker partition lists and refold touched loads exactly
+    if (D.status == 1 && !a.integral && s_naff > 0) {
+        const uint32_t p = (uint32_t)D.part;
+        bool ok = true;
+        if (D.kind == 1) {
+            list_remove(a, D.from, p, &s_i);
+            ok = list_insert(a, D.to, p, &s_i);
+        } else if (D.kind == 2 && !a.sem_go) {
+            list_remove(a, D.from, p, &s_i);
+        } else if (D.kind == 3 && !a.sem_go) {
+            ok = list_insert(a, D.to, p, &s_i);
+        }
+        if (!ok) {
+            if (tid == 0) { ctl->list_overflow = 1; D.status = -1; D.err = E_LIST_OVERFLOW; }
+        } else {
+            const int naff = s_naff;
+            for (int x0 = 0; x0 < naff; x0 += 8) {
+                // stage up to 8 brokers' contributions chunk by chunk; lane 0 of wave x folds
+                int nb = naff - x0 < 8 ? naff - x0 : 8;
+                uint32_t maxn = 0;
+                for (int x = 0; x < nb; x++) { uint32_t n = a.llen[s_aff[x0 + x]]; maxn = n > maxn ? n : maxn; }
+                double acc = 0.0;
+                for (uint32_t c = 0; c < maxn; c += 1024) {
+                    for (int x = 0; x < nb; x++) {
+                        const int b = s_aff[x0 + x];
+                        const uint32_t n = a.llen[b], st = a.lstart[b];
+                        uint32_t i = c + tid;
+                        if (i < n) s_fold[x][tid] = contribution(a, a.lent[st + i], b);
+                    }
+                    __syncthreads();
+                    if (lane == 0 && wid < nb) {
+                        const int b = s_aff[x0 + wid];
+                        const uint32_t n = a.llen[b];
+                        uint32_t lim = n - c < 1024 ? n - c : 1024;
+                        if (c < n) for (uint32_t i = 0; i < lim; i++) acc += s_fold[wid][i];
+                    }
+                    __syncthreads();
+                }
+                if (lane == 0 && wid < nb) a.load[s_aff[x0 + wid]] = acc;
+                __syncthreads();
+            }
+        }
+    }
+    __syncthreads();
+    if (tid == 0) {
+        ChangeDev ch;
+        ch.status = D.status; ch.step = D.step; ch.kind = D.kind; ch.slot = D.slot;
+        ch.part = D.part; ch.from = D.from; ch.to = D.to; ch.su = D.su; ch.cu = D.cu;
+        ch.exact = D.exact; ch.err_code = D.err; ch.err_broker = D.err_broker; ch.pad = 0;
+        if (ctl->logpos < ctl->logcap) a.log[ctl->logpos] = ch;
+        ctl->logpos++;
+        ctl->steps++;
+        // reference candidate count of the steps that actually ran this iteration
+        unsigned long long add = 0;
+        if (D.step < 0 || D.step >= 7) {
+            if (a.allow_leader) add += ctl->ncand[0];
+            if (!(D.step == 7)) add += ctl->ncand[1];
+        }
+        ctl->total_cand += add;
+        ctl->total_cont += min(ctl->ncont, a.cont_cap);
+        if (D.status != 1) ctl->halted = 1;
+    }
+}
+
+// --------------------------------------------------- multi-GPU summaries
+
+
+// pack this rank's scan result + local near-tie contenders
+__global__ __launch_bounds__(256) void k_summary(SumArgs a) {
+    DevCtl* ctl = a.ctl;
+    Summary* s = a.out;
+    const uint32_t nc = min(ctl->ncont, a.cont_cap);
+    const uint32_t n = nc < (uint32_t)SUMMARY_CONT ? nc : (uint32_t)SUMMARY_CONT;
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) s->cont[i] = a.cont[i];
+    if (threadIdx.x == 0) {
+        s->gmin[0] = ctl->gmin[0]; s->gmin[1] = ctl->gmin[1];
+        for (int f = 0; f < NF; f++) s->first[f] = ctl->first[f];
+        s->ncand[0] = ctl->ncand[0]; s->ncand[1] = ctl->ncand[1];
+        s->ncont = n;
+        s->overflow = (ctl->cont_overflow || nc > (uint32_t)SUMMARY_CONT) ? 1u : 0u;
+        if (ctl->halted) s->overflow |= 2u;
+    }
+}
+
+
+// combine every rank's summary identically on every rank
+__global__ __launch_bounds__(256) void k_merge(MergeArgs a) {
+    DevCtl* ctl = a.ctl;
+    if (ctl->halted) return;
+    __shared__ unsigned long long g[2];
+    __shared__ uint32_t total;
+    if (threadIdx.x == 0) {
+        g[0] = g[1] = NONE64;
+        uint32_t f[NF];
+        for (int q = 0; q < NF; q++) f[q] = NONE32;
+        unsigned long long c0 = 0, c1 = 0;
+        uint32_t ov = 0;
+        for (int r = 0; r < a.nranks; r++) {
+            const Summary* s = a.all + r;
+            g[0] = s->gmin[0] < g[0] ? s->gmin[0] : g[0];
+            g[1] = s->gmin[1] < g[1] ? s->gmin[1] : g[1];
+            for (int q = 0; q < NF; q++) f[q] = min(f[q], s->first[q]);
+            c0 += s->ncand[0]; c1 += s->ncand[1];
+            ov |= s->overflow & 1u;
+        }
+        ctl->gmin[0] = g[0]; ctl->gmin[1] = g[1];
+        for (int q = 0; q < NF; q++) ctl->first[q] = f[q];
+        ctl->ncand[0] = c0; ctl->ncand[1] = c1;
+        ctl->cont_overflow = ov;
+        total = 0;
+    }
+    __syncthreads();
+    const double eps = ctl->eps, inv_avg = ctl->inv_avg;
+    for (int r = 0; r < a.nranks; r++) {
+        const Summary* s = a.all + r;
+        for (uint32_t i = threadIdx.x; i < s->ncont; i += blockDim.x) {
+            const Contender c = s->cont[i];
+            // each rank emitted relative to its own minimum; keep those within the
+            // global bound (every rank holds the same loads, so d is identical)
+            const double gm = dec(g[c.kind]);
+            const double2 ls = a.LT[c.s], lt = a.LT[c.t];
+            const double d = (term_a(ls.x - c.w, inv_avg) - ls.y) + (term_a(lt.x + c.w, inv_avg) - lt.y);
+            if (!(d <= gm + 4.0 * eps)) continue;
+            uint32_t k = atomicAdd(&total, 1u);
+            if (k < a.cont_cap) a.cont[k] = c;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) ctl->ncont = total;
+}
+
+// ------------------------------------------------------- launch helpers
+
+template <int RC>
+static void launch_scan_rc(const ScanArgs& a, int tiles, hipStream_t st) {
+    hipLaunchKernelGGL(k_scan<RC>, dim3(tiles), dim3(SCAN_THREADS), 0, st, a);
+}
+template <int RC>
+static void launch_census_rc(const ScanArgs& a, int tiles, hipStream_t st) {
+    hipLaunchKernelGGL(k_census<RC>, dim3(tiles), dim3(SCAN_THREADS), 0, st, a);
+}
+
+#define KB_RC_SWITCH(RCV, FN, ...)                  \
+    switch (RCV) {                                   \
+        case 1: FN<1>(__VA_ARGS__); break;           \
+        case 2: FN<2>(__VA_ARGS__); break;           \
+        case 3: FN<3>(__VA_ARGS__); break;           \
+        case 4: FN<4>(__VA_ARGS__); break;           \
+        case 6: FN<6>(__VA_ARGS__); break;           \
+        case 8: FN<8>(__VA_ARGS__); break;           \
+        case 12: FN<12>(__VA_ARGS__); break;         \
+        default: FN<16>(__VA_ARGS__); break;         \
+    }
+
+void launch_prep(const PrepArgs& a, hipStream_t st) {
+    size_t lds = (size_t)a.NP2 * (8 + 8 + 4);
+    hipLaunchKernelGGL(k_prep, dim3(1), dim3(PREP_THREADS), lds, st, a);
+}
+void launch_setlists(const SetArgs& a, hipStream_t st) {
+    int blocks = (a.nsets + 3) / 4;
+    hipLaunchKernelGGL(k_setlists, dim3(blocks), dim3(256), 0, st, a);
+}
+void launch_scan(const ScanArgs& a, int rc, int tiles, hipStream_t st) {
+    KB_RC_SWITCH(rc, launch_scan_rc, a, tiles, st);
+}
+void launch_census(const ScanArgs& a, int rc, int tiles, hipStream_t st) {
+    KB_RC_SWITCH(rc, launch_census_rc, a, tiles, st);
+}
+void launch_resolve(const ResolveArgs& a, hipStream_t st) {
+    hipLaunchKernelGGL(k_resolve, dim3(1), dim3(RESOLVE_THREADS), 0, st, a);
+}
+void launch_summary(const SumArgs& a, hipStream_t st) {
+    hipLaunchKernelGGL(k_summary, dim3(1), dim3(256), 0, st, a);
+}
+void launch_merge(const MergeArgs& a, hipStream_t st) {
+    hipLaunchKernelGGL(k_merge, dim3(1), dim3(256), 0, st, a);
+}
+
+}  // namespace kbe

@@ -1,0 +1,103 @@
+// kernels_api.h -- argument blocks and launchers of the kernels in kernels.hip.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include "engine_dev.h"
+
+namespace kbe {
+
+struct PrepArgs {
+    DevCtl* ctl;
+    const double* load;
+    const int32_t* cnt;
+    const uint8_t* incfg;
+    int B, NP2;
+    int32_t* order;        // [B] universe sorted by (load, id)
+    int32_t* blm;          // [B] bl_move order (present or in cfg.Brokers)
+    int32_t* posm;         // [B] position in bl_move or -1
+    double2* LT;           // [B] {load, approx term}
+    double rmax_w;         // max weight (for the eps bound)
+};
+
+struct SetArgs {
+    const DevCtl* ctl;
+    int nsets, B, W64, K;
+    const uint64_t* setbits;
+    const int32_t* order;
+    const int32_t* cnt;
+    const uint8_t* incfg;
+    int32_t* lists;        // [nsets][3][K]: asc bl_move, desc present, desc universe
+    int32_t* nelig;        // [nsets] |set ∩ bl_move|
+};
+
+struct ScanArgs {
+    DevCtl* ctl;
+    const double* w;
+    const uint16_t* rep;      // [RC][Ppad] slot-major dense broker ids
+    const uint32_t* meta;     // [Ppad]
+    long long Ppad, shard_begin, shard_end;
+    int K, W64;
+    const uint64_t* setbits;
+    const int32_t* lists;
+    const int32_t* nelig;
+    const double2* LT;
+    const int32_t* blm;
+    const int32_t* posm;
+    int allow_leader, rebalance, sem_go;
+    double2* blockrec;        // [tiles] per-tile min score delta {leader, non-leader}
+    Contender* cont;
+    uint32_t cont_cap;
+};
+
+struct ResolveArgs {
+    DevCtl* ctl;
+    double* w;
+    uint16_t* rep;
+    uint32_t* meta;
+    const int32_t* nc;        // NumConsumers
+    long long Ppad;
+    int RC, K, W64, B;
+    const uint64_t* setbits;
+    const int32_t* lists;
+    const int32_t* blm;
+    const int32_t* posm;
+    double* load;
+    int32_t* cnt;
+    const Contender* cont;
+    uint32_t cont_cap;
+    int allow_leader, rebalance, sem_go, integral;
+    long long minrep;
+    double min_unbalance;
+    // per-broker partition lists (non-integral mode): CSR with slack
+    uint32_t* lstart;
+    uint32_t* llen;
+    uint32_t* lcap;
+    uint32_t* lent;
+    ChangeDev* log;
+};
+
+struct SumArgs {
+    DevCtl* ctl;
+    const Contender* cont;
+    uint32_t cont_cap;
+    Summary* out;
+};
+
+struct MergeArgs {
+    DevCtl* ctl;
+    const Summary* all;
+    int nranks;
+    Contender* cont;
+    uint32_t cont_cap;
+    const double2* LT;
+};
+
+void launch_prep(const PrepArgs& a, hipStream_t st);
+void launch_setlists(const SetArgs& a, hipStream_t st);
+void launch_scan(const ScanArgs& a, int rc, int tiles, hipStream_t st);
+void launch_census(const ScanArgs& a, int rc, int tiles, hipStream_t st);
+void launch_resolve(const ResolveArgs& a, hipStream_t st);
+void launch_summary(const SumArgs& a, hipStream_t st);
+void launch_merge(const MergeArgs& a, hipStream_t st);
+
+}  // namespace kbe

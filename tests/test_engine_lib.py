@@ -1,0 +1,45 @@
+"""CPU tests of the native artefacts: the C-ABI library loads and exports every
+symbol include/kbengine.h declares (no compute call without a GPU)."""
+import ctypes
+import os
+import re
+
+from kafkabalancer_amd import engine as E
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_symbols():
+    with open(os.path.join(ROOT, "include", "kbengine.h")) as f:
+        src = f.read()
+    return sorted(set(re.findall(r"\b(kb_[a-z_]+)\s*\(", src)))
+
+
+def test_library_exports_header():
+    syms = header_symbols()
+    assert "kb_engine_create" in syms and "kb_engine_plan" in syms
+    lib = ctypes.CDLL(E.LIB_PATH)
+    missing = [s for s in syms if not hasattr(lib, s)]
+    assert not missing, missing
+    assert sorted(E.EXPORTS) == syms
+
+
+def test_abi_version():
+    assert E.lib().kb_abi_version() == 1
+
+
+def test_library_is_gfx950_code_object():
+    with open(E.LIB_PATH, "rb") as f:
+        blob = f.read()
+    assert b"gfx950" in blob
+
+
+def test_product_does_not_reference_oracle():
+    """The product path never imports, links or calls the oracle."""
+    pkg = os.path.join(ROOT, "kafkabalancer_amd")
+    for dp, _, fns in os.walk(pkg):
+        for fn in fns:
+            if fn.endswith((".py", ".cpp", ".hip", ".h", ".hpp", "Makefile")):
+                with open(os.path.join(dp, fn), errors="ignore") as f:
+                    txt = f.read()
+                assert "oracle" not in txt.lower().replace("oracle_free", ""), os.path.join(dp, fn)

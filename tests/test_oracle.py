@@ -1,0 +1,191 @@
+"""CPU tests: the oracle is pinned by the reference's own test vectors.
+
+- the 16 TestBalancing cases (reference balancer_test.go:36-186), as data in
+  tests/golden/balancer_cases.json
+- the c1 plans predicted by SURVEY.md 8c
+- cross-check of the C oracle against the independent Python restatement
+  (oracle/pyref.py) on random tie-heavy multi-step plans
+- Go encoding/json float formatting against Python's shortest repr
+"""
+import copy
+import json
+import random
+import struct
+
+import pytest
+
+from oracle import oracle as O
+from oracle import pyref
+
+from helpers import default_cfg, golden
+from test_gpu_parity_data import random_plist
+
+
+def test_reference_balancer_cases():
+    g = golden("balancer_cases.json")
+    assert len(g["cases"]) == 16
+    for c in g["cases"]:
+        cfg = default_cfg(**g["configs"][c["cfg"]])
+        r = O.balance(O.OraclePL({"version": 1, "partitions": c["pl"]}), cfg, O.SEM_GO)
+        if "err" in c:
+            assert r["status"] == -1 and c["err"] in r["err"], (c["line"], r)
+        elif c["ppl"] is None:
+            assert r["status"] == 0, (c["line"], r)
+        else:
+            e = c["ppl"][0]
+            p = r["partition"]
+            assert r["status"] == 1, c["line"]
+            for k in ("topic", "partition", "replicas", "weight", "num_replicas", "brokers"):
+                assert p[k] == e[k], (c["line"], k, p[k], e[k])
+            assert p["num_consumers"] == e.get("num_consumers", 0)
+
+
+def test_pyref_reference_cases():
+    g = golden("balancer_cases.json")
+    for c in g["cases"]:
+        cfg = default_cfg(**g["configs"][c["cfg"]])
+        pl = pyref.normalize({"partitions": c["pl"]})
+        try:
+            r = pyref.balance(pl, cfg)
+        except pyref.StepError as ex:
+            assert "err" in c and c["err"] in str(ex), (c["line"], ex)
+            continue
+        if c.get("ppl") is None:
+            assert r is None and "err" not in c, c["line"]
+        else:
+            e = c["ppl"][0]
+            assert pl[r[1]]["replicas"] == e["replicas"], c["line"]
+
+
+def test_c1_predicted_plans():
+    """SURVEY.md 8c predictions for test/test.json."""
+    pl = golden("test.json")
+    code, out, _ = O.run_plan(O.OraclePL(pl), O.default_cfg())
+    assert code == 0
+    assert out == (b'{"version":1,"partitions":[{"topic":"foo2","partition":1,"replicas":[4,2],'
+                   b'"weight":1,"num_replicas":2,"brokers":[1,2,3,4]}]}\n')
+    code, out, _ = O.run_plan(O.OraclePL(pl), O.default_cfg(), max_reassign=1000)
+    assert code == 0 and out.count(b'"topic"') == 2
+    # -allow-leader: a 2-cycle on foo2/0 from step 5 on, and the
+    # default -complete-partition then never terminates
+    cfg = dict(O.default_cfg(), allow_leader=True)
+    o = O.OraclePL(pl)
+    seq = [O.balance(o, cfg)["pidx"] for _ in range(9)]
+    assert len(set(seq[:5])) == 5 and set(seq[5:]) == {3}
+    code, _, _ = O.run_plan(O.OraclePL(pl), cfg, max_reassign=3, complete_partition=True)
+    assert code == 0      # completion stops at the next (different) partition
+    code, _, _ = O.run_plan(O.OraclePL(pl), cfg, max_reassign=6, complete_partition=True)
+    assert code == 99     # the 6th move is foo2/0, which then flips forever
+
+
+def _pyref_plan(plist, cfg, steps):
+    pl = pyref.normalize(plist)
+    out = []
+    try:
+        for _ in range(steps):
+            r = pyref.balance(pl, cfg)
+            if r is None:
+                break
+            out.append(r)
+    except pyref.StepError as ex:
+        return out, str(ex), pl
+    return out, None, pl
+
+
+@pytest.mark.parametrize("seed", range(60))
+def test_oracle_vs_pyref(seed):
+    rng = random.Random(seed)
+    pl = random_plist(rng, rng.choice([4, 12, 40]), rng.choice([2, 3, 5, 8]),
+                      rng.choice(["uniform", "int", "zipf"]), rng.choice(["none", "some", "all"]),
+                      rng.random() < 0.4, rng.random() < 0.3)
+    cfg = default_cfg(allow_leader=rng.random() < 0.5, rebalance_leaders=rng.random() < 0.3,
+                      min_replicas=rng.choice([1, 2, 3]), min_unbalance=rng.choice([0.0, 0.01]))
+    if rng.random() < 0.3:
+        cfg["brokers"] = list(range(1, 10))
+    steps = 15
+    pch, perr, ppl = _pyref_plan(copy.deepcopy(pl), cfg, steps)
+    o = O.OraclePL(pl)
+    och = []
+    oerr = None
+    for _ in range(steps):
+        r = O.balance(o, cfg, O.SEM_APPLIED)
+        if r["status"] == 0:
+            break
+        if r["status"] < 0:
+            oerr = r["err"]
+            break
+        och.append((r["step"], r["pidx"], r["kind"] if r["kind"] != "swap" else "swap", r["from_"], r["to"]))
+    assert [(a[0], a[1], a[3], a[4]) for a in pch] == [(a[0], a[1], a[3], a[4]) for a in och]
+    if perr is None:
+        assert oerr is None
+        assert [p["replicas"] for p in ppl] == o.state()
+    else:
+        assert oerr is not None
+        if "panic" not in perr:
+            assert perr == oerr
+
+
+def test_golden_plans_reproduce():
+    """The committed oracle plans (gen_golden.py) still come out of the oracle."""
+    g = golden("plans_small.json")
+    assert len(g["cases"]) >= 20
+    for case in g["cases"]:
+        o = O.OraclePL(case["plist"])
+        sem = O.SEM_GO if case["sem"] == "go" else O.SEM_APPLIED
+        got, err = [], None
+        for _ in range(case["steps"]):
+            r = O.balance(o, case["cfg"], sem)
+            if r["status"] == 0:
+                break
+            if r["status"] < 0:
+                err = r["err"]
+                break
+            got.append([r["step"], r["pidx"], r["kind"], r["from_"], r["to"], r["slot"]])
+        assert got == case["changes"], case["name"]
+        assert err == case["err"], case["name"]
+        assert o.state() == case["final"], case["name"]
+
+
+def go_float(x):
+    """Go encoding/json float64 text, from Python's shortest round-trip digits."""
+    import decimal
+    if x == 0:
+        return "0"
+    sign = "-" if x < 0 else ""
+    a = abs(x)
+    t = decimal.Decimal(repr(a)).normalize().as_tuple()
+    digits = "".join(map(str, t.digits))
+    point = len(digits) + t.exponent          # value = 0.digits * 10^point
+    if a < 1e-6 or a >= 1e21:
+        e = point - 1
+        mant = digits[0] + ("." + digits[1:] if len(digits) > 1 else "")
+        return sign + mant + (("e-%d" % -e) if e < 0 else ("e+%02d" % e))
+    if point <= 0:
+        return sign + "0." + "0" * (-point) + digits
+    if point >= len(digits):
+        return sign + digits + "0" * (point - len(digits))
+    return sign + digits[:point] + "." + digits[point:]
+
+
+def test_go_float_format():
+    rng = random.Random(7)
+    vals = [1.0, 0.5, 0.1, 1e-7, 2.5e-7, 1e-6, 123456.789, 1e20, 1e21, 3e22, 1 / 3, 2.0 ** -30,
+            0.000123, 1e300, 5e-324, 7.0, 100.0]
+    vals += [rng.uniform(1, 1e6) ** -1.1 for _ in range(300)]
+    vals += [rng.uniform(0, 1e7) for _ in range(200)]
+    for v in vals:
+        assert O.format_float(v) == go_float(v), v
+        assert float(O.format_float(v)) == v
+
+
+def test_json_writer_matches_go_layout():
+    pl = {"version": 1, "partitions": [
+        {"topic": "a<b>&c", "partition": 3, "replicas": [2, 1], "weight": 2.5e-7, "num_consumers": 2},
+        {"topic": "x", "partition": 0, "replicas": [1, 2]}]}
+    code, out, _ = O.run_plan(O.OraclePL(pl), O.default_cfg(), full_output=True, max_reassign=0)
+    assert code == 0
+    want = ('{"version":1,"partitions":[{"topic":"a\\u003cb\\u003e\\u0026c","partition":3,'
+            '"replicas":[2,1],"weight":2.5e-7,"num_consumers":2},'
+            '{"topic":"x","partition":0,"replicas":[1,2]}]}\n').encode()
+    assert out == want
+    json.loads(out)
