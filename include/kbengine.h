@@ -96,6 +96,10 @@ typedef struct {
     int32_t list_slack;             /* extra entries per broker list (0 = default 1024) */
     int64_t shard_begin;            /* partitions [shard_begin, shard_end) scanned by this */
     int64_t shard_end;              /*   engine; 0,0 = all (multi-GPU sharding) */
+    int32_t exact_unbalance;        /* 1 => unbalance_after is always the exact sequential
+                                       fold (costs one O(B) fold per step); 0 => exact only
+                                       when a near tie needed it, else within eps */
+    int32_t time_kernels;           /* 1 => HIP events around every launch (kb_engine_timings) */
 } kb_config;
 
 /* One step's result: the change Balance() would return (balancer.go:49-65). */
@@ -159,6 +163,11 @@ int64_t kb_engine_loads(kb_engine *e, int64_t *ids, double *loads, int64_t cap);
 double kb_engine_unbalance(kb_engine *e);
 
 int kb_engine_stats(kb_engine *e, kb_stats *out);
+
+/* Per-kernel device time of the last kb_engine_plan when cfg->time_kernels was
+ * set: ms[k] = summed duration of kernel k over the plan, launches[k] = count,
+ * for k in {0 prep, 1 setlists, 2 scan, 3 census, 4 resolve}.  Returns 5. */
+int kb_engine_timings(kb_engine *e, double *ms, int64_t *launches, int n);
 
 /* Reference-format message of the last error ("<Step>: partition Partition(t,p,[..]) ..."). */
 int kb_engine_last_error(kb_engine *e, char *buf, size_t n);

@@ -81,6 +81,13 @@ struct kb_engine {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     double last_ms = 0;
     int64_t scan_bytes = 0;
+    int exact_unb = 0;
+    // per-kernel timing (cfg->time_kernels): one event ring per batch of steps
+    int time_kernels = 0;
+    std::vector<hipEvent_t> tev;      // 6 events per step
+    int tev_used = 0;
+    double kms[5] = {0, 0, 0, 0, 0};
+    int64_t klaunch[5] = {0, 0, 0, 0, 0};
     std::string last_err;
 };
 
@@ -134,6 +141,8 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
     e->minrep = cfg->min_replicas;
     e->min_unb = cfg->min_unbalance;
     e->dev = cfg->device;
+    e->exact_unb = cfg->exact_unbalance ? 1 : 0;
+    e->time_kernels = cfg->time_kernels ? 1 : 0;
     if (c->topic_blob && c->topic_off) {
         e->topics.resize(n);
         for (int64_t i = 0; i < n; i++)
@@ -440,7 +449,36 @@ static void fill_resolve_args(kb_engine* e, ResolveArgs& r) {
     r.load = e->load; r.cnt = e->cnt; r.cont = e->cont; r.cont_cap = e->cont_cap;
     r.allow_leader = e->allow_leader; r.rebalance = e->rebalance; r.sem_go = e->sem == KB_SEM_GO;
     r.integral = e->integral ? 1 : 0; r.minrep = e->minrep; r.min_unbalance = e->min_unb;
+    r.exact_unb = e->exact_unb;
     r.lstart = e->lstart; r.llen = e->llen; r.lcap = e->lcap; r.lent = e->lent; r.log = e->log;
+}
+
+static const int kStepBatch = 64;
+
+static void mark(kb_engine* e, int k) {
+    if (!e->time_kernels) return;
+    if (e->tev.empty()) {
+        e->tev.resize((size_t)kStepBatch * 6 + 12);
+        for (auto& v : e->tev) hipEventCreate(&v);
+    }
+    if (e->tev_used < (int)e->tev.size()) hipEventRecord(e->tev[e->tev_used++], e->st);
+    (void)k;
+}
+
+// accumulate the durations of the marks recorded since the last harvest
+static void harvest(kb_engine* e) {
+    if (!e->time_kernels || e->tev_used == 0) return;
+    hipEventSynchronize(e->tev[e->tev_used - 1]);
+    for (int s = 0; s + 5 < e->tev_used; s += 6) {
+        for (int k = 0; k < 5; k++) {
+            float ms = 0;
+            if (hipEventElapsedTime(&ms, e->tev[s + k], e->tev[s + k + 1]) == hipSuccess) {
+                e->kms[k] += ms;
+                e->klaunch[k]++;
+            }
+        }
+    }
+    e->tev_used = 0;
 }
 
 // prep + setlists + scan (the local half of a step)
@@ -449,7 +487,9 @@ static void enqueue_front(kb_engine* e) {
     pa.ctl = e->ctl; pa.load = e->load; pa.cnt = e->cnt; pa.incfg = e->incfg;
     pa.B = (int)e->B; pa.NP2 = e->NP2; pa.order = e->order; pa.blm = e->blm; pa.posm = e->posm;
     pa.LT = e->LT; pa.rmax_w = e->wmax;
+    mark(e, 0);
     launch_prep(pa, e->st);
+    mark(e, 1);
     SetArgs sa;
     sa.ctl = e->ctl; sa.nsets = (int)e->nsets; sa.B = (int)e->B; sa.W64 = e->W64; sa.K = e->K;
     sa.setbits = e->setbits; sa.order = e->order; sa.cnt = e->cnt; sa.incfg = e->incfg;
@@ -458,8 +498,13 @@ static void enqueue_front(kb_engine* e) {
     if (e->tiles > 0) {
         ScanArgs s;
         fill_scan_args(e, s);
+        mark(e, 2);
         launch_scan(s, e->rc_dev, (int)e->tiles, e->st);
+        mark(e, 3);
         launch_census(s, e->rc_dev, (int)e->tiles, e->st);
+    } else {
+        mark(e, 2);
+        mark(e, 3);
     }
 }
 
@@ -467,7 +512,9 @@ static void enqueue_step(kb_engine* e) {
     enqueue_front(e);
     ResolveArgs r;
     fill_resolve_args(e, r);
+    mark(e, 4);
     launch_resolve(r, e->st);
+    mark(e, 5);
 }
 
 static int reset_ctl(kb_engine* e, int logcap) {
@@ -541,6 +588,7 @@ extern "C" int kb_engine_balance(kb_engine* e, kb_change* out) {
     HIPCHK(hipEventRecord(e->ev1, e->st));
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(e->st));
+    harvest(e);
     float ms = 0;
     hipEventElapsedTime(&ms, e->ev0, e->ev1);
     e->last_ms = ms;
@@ -560,9 +608,11 @@ extern "C" int kb_engine_plan(kb_engine* e, int64_t max_steps, kb_change* out, i
         HIPCHK(dalloc(&e->log, e->logcap));
     }
     if (reset_ctl(e, e->logcap) != KB_OK) return KB_ERR_HIP;
+    for (int k = 0; k < 5; k++) { e->kms[k] = 0; e->klaunch[k] = 0; }
+    e->tev_used = 0;
     HIPCHK(hipEventRecord(e->ev0, e->st));
     int64_t done = 0;
-    const int64_t batch = 64;
+    const int64_t batch = kStepBatch;
     while (done < max_steps) {
         int64_t nb = std::min<int64_t>(batch, max_steps - done);
         for (int64_t s = 0; s < nb; s++) enqueue_step(e);
@@ -570,6 +620,7 @@ extern "C" int kb_engine_plan(kb_engine* e, int64_t max_steps, kb_change* out, i
         HIPCHK(hipGetLastError());
         HIPCHK(hipMemcpyAsync(e->h_ctl, e->ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, e->st));
         HIPCHK(hipStreamSynchronize(e->st));
+        harvest(e);
         if (e->h_ctl->halted) break;
     }
     HIPCHK(hipEventRecord(e->ev1, e->st));
@@ -648,6 +699,15 @@ extern "C" int kb_engine_stats(kb_engine* e, kb_stats* o) {
     return KB_OK;
 }
 
+extern "C" int kb_engine_timings(kb_engine* e, double* ms, int64_t* launches, int n) {
+    if (!e) return KB_ERR_INVALID;
+    for (int k = 0; k < 5 && k < n; k++) {
+        if (ms) ms[k] = e->kms[k];
+        if (launches) launches[k] = e->klaunch[k];
+    }
+    return 5;
+}
+
 extern "C" int kb_engine_last_error(kb_engine* e, char* buf, size_t n) {
     if (!e || !buf || n == 0) return KB_ERR_INVALID;
     snprintf(buf, n, "%s", e->last_err.c_str());
@@ -663,6 +723,7 @@ extern "C" void kb_engine_destroy(kb_engine* e) {
     if (e->h_ctl) hipHostFree(e->h_ctl);
     if (e->ev0) hipEventDestroy(e->ev0);
     if (e->ev1) hipEventDestroy(e->ev1);
+    for (auto v : e->tev) hipEventDestroy(v);
     if (e->own_st && e->st) hipStreamDestroy(e->st);
     delete e;
 }

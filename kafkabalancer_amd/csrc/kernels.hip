@@ -757,8 +757,8 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void k_resolve(ResolveArgs a) {
             double Ua = su + d;
             witer = c0.iter; wi = i0;
             const double lim = thr < su ? thr : su;
-            if (Ua + 2.0 * eps < lim) { Ustar = Ua; exact = 0; }
-            else if (Ua - 2.0 * eps >= (thr > su ? thr : su)) { Ustar = Ua; exact = 0; }
+            const bool certain = (Ua + 2.0 * eps < lim) || (Ua - 2.0 * eps >= (thr > su ? thr : su));
+            if (certain && !a.exact_unb) { Ustar = Ua; exact = 0; }
             else {
                 if (tid == 0) s_dv[0] = exact_unbalance(a.blm, nblm, a.load, c0.s, c0.t, c0.w);
                 __syncthreads();

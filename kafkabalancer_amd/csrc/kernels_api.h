@@ -65,7 +65,7 @@ struct ResolveArgs {
     int32_t* cnt;
     const Contender* cont;
     uint32_t cont_cap;
-    int allow_leader, rebalance, sem_go, integral;
+    int allow_leader, rebalance, sem_go, integral, exact_unb;
     long long minrep;
     double min_unbalance;
     // per-broker partition lists (non-integral mode): CSR with slack

@@ -23,6 +23,7 @@ KIND_NAMES = {0: "none", 1: "replace", 2: "remove", 3: "add", 4: "swap"}
 
 EXPORTS = ["kb_abi_version", "kb_engine_create", "kb_engine_balance", "kb_engine_plan",
            "kb_engine_replicas", "kb_engine_loads", "kb_engine_unbalance", "kb_engine_stats",
+           "kb_engine_timings",
            "kb_engine_last_error", "kb_engine_destroy", "kb_engine_summary_bytes",
            "kb_engine_step_begin", "kb_engine_step_finish", "kb_engine_set_stream"]
 
@@ -42,7 +43,8 @@ class kb_config(C.Structure):
                 ("min_replicas", C.c_int64), ("min_unbalance", C.c_double),
                 ("brokers", P64), ("n_brokers", C.c_int64), ("brokers_nil", C.c_int32),
                 ("semantics", C.c_int32), ("device", C.c_int32), ("list_slack", C.c_int32),
-                ("shard_begin", C.c_int64), ("shard_end", C.c_int64)]
+                ("shard_begin", C.c_int64), ("shard_end", C.c_int64),
+                ("exact_unbalance", C.c_int32), ("time_kernels", C.c_int32)]
 
 
 class kb_change(C.Structure):
@@ -85,6 +87,8 @@ def lib():
         L.kb_engine_unbalance.restype = C.c_double
         L.kb_engine_stats.argtypes = [vp, C.POINTER(kb_stats)]
         L.kb_engine_stats.restype = C.c_int
+        L.kb_engine_timings.argtypes = [vp, PD, P64, C.c_int]
+        L.kb_engine_timings.restype = C.c_int
         L.kb_engine_last_error.argtypes = [vp, C.c_char_p, C.c_size_t]
         L.kb_engine_last_error.restype = C.c_int
         L.kb_engine_destroy.argtypes = [vp]
@@ -195,7 +199,8 @@ def _change_dict(ch):
 class Engine:
     """One device-resident engine over a cluster (kb_engine_*)."""
 
-    def __init__(self, cluster, cfg, semantics=KB_SEM_APPLIED, device=0, shard=None, list_slack=0):
+    def __init__(self, cluster, cfg, semantics=KB_SEM_APPLIED, device=0, shard=None, list_slack=0,
+                 exact_unbalance=False, time_kernels=False):
         L = lib()
         if not isinstance(cluster, ClusterSoA):
             cluster = ClusterSoA.from_plist(cluster)
@@ -219,6 +224,8 @@ class Engine:
         kc.semantics = semantics
         kc.device = device
         kc.list_slack = list_slack
+        kc.exact_unbalance = int(bool(exact_unbalance))
+        kc.time_kernels = int(bool(time_kernels))
         if shard is not None:
             kc.shard_begin, kc.shard_end = shard
         h = C.c_void_p()
@@ -282,6 +289,15 @@ class Engine:
         s = kb_stats()
         lib().kb_engine_stats(self.h, C.byref(s))
         return {f: getattr(s, f) for f, _ in s._fields_}
+
+    KERNELS = ("prep", "setlists", "scan", "census", "resolve")
+
+    def timings(self):
+        """{kernel: (total_ms, launches)} of the last plan (time_kernels=True)."""
+        ms = np.zeros(5)
+        n = np.zeros(5, np.int64)
+        lib().kb_engine_timings(self.h, ms.ctypes.data_as(PD), n.ctypes.data_as(P64), 5)
+        return {k: (float(ms[i]), int(n[i])) for i, k in enumerate(self.KERNELS)}
 
     # multi-GPU step phases
     def summary_bytes(self):
