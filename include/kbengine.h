@@ -166,7 +166,7 @@ int kb_engine_stats(kb_engine *e, kb_stats *out);
 
 /* Per-kernel device time of the last kb_engine_plan when cfg->time_kernels was
  * set: ms[k] = summed duration of kernel k over the plan, launches[k] = count,
- * for k in {0 prep, 1 setlists, 2 scan, 3 census, 4 resolve}.  Returns 5. */
+ * for k in {0 prep, 1 setlists, 2 scan, 3 reduce, 4 census, 5 resolve}.  Returns 6. */
 int kb_engine_timings(kb_engine *e, double *ms, int64_t *launches, int n);
 
 /* Reference-format message of the last error ("<Step>: partition Partition(t,p,[..]) ..."). */

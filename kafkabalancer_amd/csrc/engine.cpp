@@ -70,7 +70,7 @@ struct kb_engine {
     int32_t* blm = nullptr;
     int32_t* posm = nullptr;
     double2* LT = nullptr;
-    double2* blockrec = nullptr;
+    BlockRec* blockrec = nullptr;
     Contender* cont = nullptr;
     uint32_t cont_cap = 1u << 20;
     uint32_t *lstart = nullptr, *llen = nullptr, *lcap = nullptr, *lent = nullptr;
@@ -86,8 +86,8 @@ struct kb_engine {
     int time_kernels = 0;
     std::vector<hipEvent_t> tev;      // 6 events per step
     int tev_used = 0;
-    double kms[5] = {0, 0, 0, 0, 0};
-    int64_t klaunch[5] = {0, 0, 0, 0, 0};
+    double kms[6] = {0, 0, 0, 0, 0, 0};
+    int64_t klaunch[6] = {0, 0, 0, 0, 0, 0};
     std::string last_err;
 };
 
@@ -320,7 +320,8 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
     // shard
     e->shard_begin = cfg->shard_begin;
     e->shard_end = (cfg->shard_begin == 0 && cfg->shard_end == 0) ? n : cfg->shard_end;
-    if (e->shard_begin < 0 || e->shard_end > n || e->shard_begin > e->shard_end || (e->shard_begin % TILE) != 0) {
+    if (e->shard_begin < 0 || e->shard_end > n || e->shard_begin > e->shard_end ||
+        ((e->shard_begin % TILE) != 0 && e->shard_begin != e->shard_end)) {
         e->last_err = "shard_begin must be a multiple of 1024 and 0 <= begin <= end <= n";
         delete e;
         return KB_ERR_INVALID;
@@ -458,7 +459,7 @@ static const int kStepBatch = 64;
 static void mark(kb_engine* e, int k) {
     if (!e->time_kernels) return;
     if (e->tev.empty()) {
-        e->tev.resize((size_t)kStepBatch * 6 + 12);
+        e->tev.resize((size_t)kStepBatch * 7 + 14);
         for (auto& v : e->tev) hipEventCreate(&v);
     }
     if (e->tev_used < (int)e->tev.size()) hipEventRecord(e->tev[e->tev_used++], e->st);
@@ -469,8 +470,8 @@ static void mark(kb_engine* e, int k) {
 static void harvest(kb_engine* e) {
     if (!e->time_kernels || e->tev_used == 0) return;
     hipEventSynchronize(e->tev[e->tev_used - 1]);
-    for (int s = 0; s + 5 < e->tev_used; s += 6) {
-        for (int k = 0; k < 5; k++) {
+    for (int s = 0; s + 6 < e->tev_used; s += 7) {
+        for (int k = 0; k < 6; k++) {
             float ms = 0;
             if (hipEventElapsedTime(&ms, e->tev[s + k], e->tev[s + k + 1]) == hipSuccess) {
                 e->kms[k] += ms;
@@ -501,10 +502,15 @@ static void enqueue_front(kb_engine* e) {
         mark(e, 2);
         launch_scan(s, e->rc_dev, (int)e->tiles, e->st);
         mark(e, 3);
+        ReduceArgs ra;
+        ra.ctl = e->ctl; ra.blockrec = e->blockrec; ra.tiles = (int)e->tiles;
+        launch_reduce(ra, e->st);
+        mark(e, 4);
         launch_census(s, e->rc_dev, (int)e->tiles, e->st);
     } else {
         mark(e, 2);
         mark(e, 3);
+        mark(e, 4);
     }
 }
 
@@ -512,9 +518,9 @@ static void enqueue_step(kb_engine* e) {
     enqueue_front(e);
     ResolveArgs r;
     fill_resolve_args(e, r);
-    mark(e, 4);
-    launch_resolve(r, e->st);
     mark(e, 5);
+    launch_resolve(r, e->st);
+    mark(e, 6);
 }
 
 static int reset_ctl(kb_engine* e, int logcap) {
@@ -608,7 +614,7 @@ extern "C" int kb_engine_plan(kb_engine* e, int64_t max_steps, kb_change* out, i
         HIPCHK(dalloc(&e->log, e->logcap));
     }
     if (reset_ctl(e, e->logcap) != KB_OK) return KB_ERR_HIP;
-    for (int k = 0; k < 5; k++) { e->kms[k] = 0; e->klaunch[k] = 0; }
+    for (int k = 0; k < 6; k++) { e->kms[k] = 0; e->klaunch[k] = 0; }
     e->tev_used = 0;
     HIPCHK(hipEventRecord(e->ev0, e->st));
     int64_t done = 0;
@@ -701,11 +707,11 @@ extern "C" int kb_engine_stats(kb_engine* e, kb_stats* o) {
 
 extern "C" int kb_engine_timings(kb_engine* e, double* ms, int64_t* launches, int n) {
     if (!e) return KB_ERR_INVALID;
-    for (int k = 0; k < 5 && k < n; k++) {
+    for (int k = 0; k < 6 && k < n; k++) {
         if (ms) ms[k] = e->kms[k];
         if (launches) launches[k] = e->klaunch[k];
     }
-    return 5;
+    return 6;
 }
 
 extern "C" int kb_engine_last_error(kb_engine* e, char* buf, size_t n) {

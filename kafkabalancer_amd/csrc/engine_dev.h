@@ -46,6 +46,13 @@ struct Contender {                  // a near-tie candidate move (32 B)
     int32_t pad;
 };
 
+// per-tile scan record (64 B): no global atomics in the scan, k_reduce combines
+struct BlockRec {
+    double dmin[2];                 // min score delta {leader, non-leader}
+    unsigned long long cand[2];     // reference candidate counts
+    uint32_t first[NF];             // first-index predicates
+};
+
 struct ChangeDev {
     int32_t status, step, kind, slot;
     int64_t part;

@@ -101,6 +101,52 @@ __device__ double exact_unbalance(const int32_t* __restrict__ blm, int nblm,
     return U;
 }
 
+// Sequential fold of n doubles held in LDS, in order (the reference's fold).
+// Loads are batched 16 at a time so the dependent add chain, not LDS latency,
+// sets the pace.
+__device__ __forceinline__ double fold_lds(const double* x, int n, double acc = 0.0) {
+    int k = 0;
+    for (; k + 16 <= n; k += 16) {
+        double v[16];
+#pragma unroll
+        for (int i = 0; i < 16; i++) v[i] = x[k + i];
+#pragma unroll
+        for (int i = 0; i < 16; i++) acc += v[i];
+    }
+    for (; k < n; k++) acc += x[k];
+    return acc;
+}
+
+// exact_unbalance with the bl_move loads staged in LDS (Lm) and the two
+// modified entries at bl positions ps / pt (steps.go:250,272; utils.go:119-147)
+__device__ double exact_unbalance_lds(const double* Lm, int n, int ps, int pt, double Ls, double Lt) {
+    double S = 0.0;
+    int k = 0;
+    for (; k + 16 <= n; k += 16) {
+        double v[16];
+#pragma unroll
+        for (int i = 0; i < 16; i++) v[i] = Lm[k + i];
+#pragma unroll
+        for (int i = 0; i < 16; i++) S += (k + i == ps) ? Ls : ((k + i == pt) ? Lt : v[i]);
+    }
+    for (; k < n; k++) S += (k == ps) ? Ls : ((k == pt) ? Lt : Lm[k]);
+    const double avg = S / (double)n;
+    double U = 0.0;
+    k = 0;
+    for (; k + 16 <= n; k += 16) {
+        double t[16];
+#pragma unroll
+        for (int i = 0; i < 16; i++) {
+            const double L = (k + i == ps) ? Ls : ((k + i == pt) ? Lt : Lm[k + i]);
+            t[i] = term_x(L, avg);
+        }
+#pragma unroll
+        for (int i = 0; i < 16; i++) U += t[i];
+    }
+    for (; k < n; k++) U += term_x((k == ps) ? Ls : ((k == pt) ? Lt : Lm[k]), avg);
+    return U;
+}
+
 // --------------------------------------------------------------- k_prep
 
 
@@ -189,8 +235,7 @@ __global__ __launch_bounds__(PREP_THREADS) void k_prep(PrepArgs a) {
     const double* Lm = (const double*)keys;
     // S: sequential fold in bl order (utils.go:123-128)
     if (tid == 0) {
-        double S = 0.0;
-        for (int k = 0; k < nblm; k++) S += Lm[k];
+        const double S = fold_lds(Lm, nblm);
         s_S = S;
         s_avg = S / (double)nblm;
     }
@@ -199,11 +244,7 @@ __global__ __launch_bounds__(PREP_THREADS) void k_prep(PrepArgs a) {
     for (int k = tid; k < nblm; k += PREP_THREADS) Tm[k] = term_x(Lm[k], avg);
     __syncthreads();
     // su: sequential fold of the terms (utils.go:134-143)
-    if (tid == 0) {
-        double U = 0.0;
-        for (int k = 0; k < nblm; k++) U += Tm[k];
-        s_U0 = U;
-    }
+    if (tid == 0) s_U0 = fold_lds(Tm, nblm);
     // error-bound ingredients: V = sum |r|(1+|r|), Rmax = max |r|
     const double inv_avg = 1.0 / avg;
     double v = 0.0, rm = 0.0;
@@ -428,13 +469,58 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
 #pragma unroll
             for (int f = 0; f < NF; f++) fst[f] = min(fst[f], s_f[f][x]);
         }
-        a.blockrec[blockIdx.x] = make_double2(dminL, dminN);
-        if (dminL < HUGE_VAL) atomicMin(&ctl->gmin[0], enc(dminL));
-        if (dminN < HUGE_VAL) atomicMin(&ctl->gmin[1], enc(dminN));
+        BlockRec r;
+        r.dmin[0] = dminL; r.dmin[1] = dminN;
+        r.cand[0] = cL; r.cand[1] = cN;
 #pragma unroll
-        for (int f = 0; f < NF; f++) if (fst[f] != NONE32) atomicMin(&ctl->first[f], fst[f]);
-        if (cL) atomicAdd(&ctl->ncand[0], cL);
-        if (cN) atomicAdd(&ctl->ncand[1], cN);
+        for (int f = 0; f < NF; f++) r.first[f] = fst[f];
+        a.blockrec[blockIdx.x] = r;
+    }
+}
+
+// ------------------------------------------------------------- k_reduce
+// one workgroup combines the per-tile records (replaces ~10 same-address
+// atomics per tile, which serialise at ~90 ops/us per word)
+__global__ __launch_bounds__(1024) void k_reduce(ReduceArgs a) {
+    DevCtl* ctl = a.ctl;
+    if (ctl->halted) return;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    double d0 = HUGE_VAL, d1 = HUGE_VAL;
+    unsigned long long c0 = 0, c1 = 0;
+    uint32_t f[NF];
+#pragma unroll
+    for (int q = 0; q < NF; q++) f[q] = NONE32;
+    for (int i = tid; i < a.tiles; i += 1024) {
+        const BlockRec r = a.blockrec[i];
+        d0 = r.dmin[0] < d0 ? r.dmin[0] : d0;
+        d1 = r.dmin[1] < d1 ? r.dmin[1] : d1;
+        c0 += r.cand[0]; c1 += r.cand[1];
+#pragma unroll
+        for (int q = 0; q < NF; q++) f[q] = min(f[q], r.first[q]);
+    }
+    d0 = wave_min(d0); d1 = wave_min(d1); c0 = wave_sum(c0); c1 = wave_sum(c1);
+#pragma unroll
+    for (int q = 0; q < NF; q++) f[q] = wave_min(f[q]);
+    __shared__ double s_d[2][16];
+    __shared__ unsigned long long s_c[2][16];
+    __shared__ uint32_t s_f[NF][16];
+    if (lane == 0) {
+        s_d[0][wid] = d0; s_d[1][wid] = d1; s_c[0][wid] = c0; s_c[1][wid] = c1;
+#pragma unroll
+        for (int q = 0; q < NF; q++) s_f[q][wid] = f[q];
+    }
+    __syncthreads();
+    if (tid == 0) {
+        for (int x = 1; x < 16; x++) {
+            d0 = s_d[0][x] < d0 ? s_d[0][x] : d0;
+            d1 = s_d[1][x] < d1 ? s_d[1][x] : d1;
+            c0 += s_c[0][x]; c1 += s_c[1][x];
+            for (int q = 0; q < NF; q++) f[q] = min(f[q], s_f[q][x]);
+        }
+        ctl->gmin[0] = d0 < HUGE_VAL ? enc(d0) : NONE64;
+        ctl->gmin[1] = d1 < HUGE_VAL ? enc(d1) : NONE64;
+        ctl->ncand[0] = c0; ctl->ncand[1] = c1;
+        for (int q = 0; q < NF; q++) ctl->first[q] = f[q];
     }
 }
 
@@ -457,9 +543,25 @@ __device__ __forceinline__ void emit(const ScanArgs& a, int kind, int s, int t, 
 // (the approximate delta is monotone in the target load up to 2*eps).
 template <int RC>
 __device__ void walk_targets(const ScanArgs& a, int kind, long long p, int slot, int src,
-                             const uint32_t (&reps)[RC], int nrep, const uint64_t* sb, double wv,
-                             double ds, double g, double eps, int nblm, double inv_avg) {
-    for (int k = 0; k < nblm; k++) {
+                             const uint32_t (&reps)[RC], int nrep, const uint64_t* sb, const int32_t* al,
+                             double wv, double ds, double g, double eps, int nblm, double inv_avg) {
+    const unsigned long long ib = ((unsigned long long)p << 21) | ((unsigned long long)slot << 16);
+    // the set's first K eligible brokers in bl_move order come precomputed
+    int start = 0;
+    for (int i = 0; i < a.K; i++) {
+        const int b = al[i];
+        if (b < 0) return;                       // set exhausted
+        start = a.posm[b] + 1;
+        bool isrep = false;
+#pragma unroll
+        for (int q = 0; q < RC; q++) isrep |= (q < nrep) && ((int)reps[q] == b);
+        if (isrep) continue;
+        const double2 lt = a.LT[b];
+        const double d = ds + (term_a(lt.x + wv, inv_avg) - lt.y);
+        if (d <= g + 4.0 * eps) emit(a, kind, src, b, wv, ib | (unsigned long long)(start - 1));
+        if (d > g + 8.0 * eps) return;
+    }
+    for (int k = start; k < nblm; k++) {         // rare: more than K near-tied targets
         const int b = a.blm[k];
         if (!setbit(sb, b)) continue;
         bool isrep = false;
@@ -468,9 +570,8 @@ __device__ void walk_targets(const ScanArgs& a, int kind, long long p, int slot,
         if (isrep) continue;
         const double2 lt = a.LT[b];
         const double d = ds + (term_a(lt.x + wv, inv_avg) - lt.y);
-        if (d <= g + 4.0 * eps)
-            emit(a, kind, src, b, wv, ((unsigned long long)p << 21) | ((unsigned long long)slot << 16) | (unsigned long long)k);
-        if (d > g + 8.0 * eps) break;
+        if (d <= g + 4.0 * eps) emit(a, kind, src, b, wv, ib | (unsigned long long)k);
+        if (d > g + 8.0 * eps) return;
     }
 }
 
@@ -482,9 +583,9 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_census(ScanArgs a) {
     const unsigned long long eL = ctl->gmin[0], eN = ctl->gmin[1];
     const double gL = eL == NONE64 ? HUGE_VAL : dec(eL);
     const double gN = eN == NONE64 ? HUGE_VAL : dec(eN);
-    const double2 br = a.blockrec[blockIdx.x];
-    const bool doL = a.allow_leader && eL != NONE64 && br.x <= gL + 8.0 * eps;
-    const bool doN = eN != NONE64 && br.y <= gN + 8.0 * eps;
+    const BlockRec& br = a.blockrec[blockIdx.x];
+    const bool doL = a.allow_leader && eL != NONE64 && br.dmin[0] <= gL + 8.0 * eps;
+    const bool doN = eN != NONE64 && br.dmin[1] <= gN + 8.0 * eps;
     if (!doL && !doN) return;
     const double inv_avg = ctl->inv_avg;
     const int nblm = ctl->nblm;
@@ -512,7 +613,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_census(ScanArgs a) {
             const double2 ls = a.LT[reps[0]];
             const double ds = term_a(ls.x - wv, inv_avg) - ls.y;
             if (ds + dt <= gL + 8.0 * eps)
-                walk_targets<RC>(a, 0, p, 0, (int)reps[0], reps, nrep, sb, wv, ds, gL, eps, nblm, inv_avg);
+                walk_targets<RC>(a, 0, p, 0, (int)reps[0], reps, nrep, sb, al, wv, ds, gL, eps, nblm, inv_avg);
         }
         if (doN) {
 #pragma unroll
@@ -521,7 +622,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_census(ScanArgs a) {
                     const double2 ls = a.LT[reps[k]];
                     const double ds = term_a(ls.x - wv, inv_avg) - ls.y;
                     if (ds + dt <= gN + 8.0 * eps)
-                        walk_targets<RC>(a, 1, p, k, (int)reps[k], reps, nrep, sb, wv, ds, gN, eps, nblm, inv_avg);
+                        walk_targets<RC>(a, 1, p, k, (int)reps[k], reps, nrep, sb, al, wv, ds, gN, eps, nblm, inv_avg);
                 }
             }
         }
@@ -613,9 +714,11 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void k_resolve(ResolveArgs a) {
     __shared__ int s_flag[NW];
     __shared__ int s_idx;
     __shared__ double s_fold[8][1024];           // refold staging (non-integral mode)
+    __shared__ double s_Lm[MAXB];                // loads in bl_move order (exact folds)
     const double su = ctl->U0;
     const double eps = ctl->eps;
     const int nblm = ctl->nblm;
+    for (int k = tid; k < nblm; k += RESOLVE_THREADS) s_Lm[k] = a.load[a.blm[k]];
 
     if (tid == 0) {
         D.status = 0; D.step = -1; D.kind = 0; D.slot = -1; D.part = -1;
@@ -760,7 +863,7 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void k_resolve(ResolveArgs a) {
             const bool certain = (Ua + 2.0 * eps < lim) || (Ua - 2.0 * eps >= (thr > su ? thr : su));
             if (certain && !a.exact_unb) { Ustar = Ua; exact = 0; }
             else {
-                if (tid == 0) s_dv[0] = exact_unbalance(a.blm, nblm, a.load, c0.s, c0.t, c0.w);
+                if (tid == 0) s_dv[0] = exact_unbalance_lds(s_Lm, nblm, a.posm[c0.s], a.posm[c0.t], a.load[c0.s] - c0.w, a.load[c0.t] + c0.w);
                 __syncthreads();
                 Ustar = s_dv[0];
                 if (tid == 0) atomicAdd(&ctl->total_folds, 1ull);
@@ -774,7 +877,7 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void k_resolve(ResolveArgs a) {
             for (uint32_t i = tid; i < nc; i += RESOLVE_THREADS) {
                 const Contender c = a.cont[i];
                 if (c.kind != kind) continue;
-                double u = exact_unbalance(a.blm, nblm, a.load, c.s, c.t, c.w);
+                double u = exact_unbalance_lds(s_Lm, nblm, a.posm[c.s], a.posm[c.t], a.load[c.s] - c.w, a.load[c.t] + c.w);
                 nf++;
                 if (u < bu || (u == bu && c.iter < bi)) { bu = u; bi = c.iter; bx = (int)i; }
             }
@@ -934,7 +1037,7 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void k_resolve(ResolveArgs a) {
                         const int b = s_aff[x0 + wid];
                         const uint32_t n = a.llen[b];
                         uint32_t lim = n - c < 1024 ? n - c : 1024;
-                        if (c < n) for (uint32_t i = 0; i < lim; i++) acc += s_fold[wid][i];
+                        if (c < n) acc = fold_lds(&s_fold[wid][0], (int)lim, acc);
                     }
                     __syncthreads();
                 }
@@ -1067,6 +1170,9 @@ void launch_scan(const ScanArgs& a, int rc, int tiles, hipStream_t st) {
 }
 void launch_census(const ScanArgs& a, int rc, int tiles, hipStream_t st) {
     KB_RC_SWITCH(rc, launch_census_rc, a, tiles, st);
+}
+void launch_reduce(const ReduceArgs& a, hipStream_t st) {
+    hipLaunchKernelGGL(k_reduce, dim3(1), dim3(1024), 0, st, a);
 }
 void launch_resolve(const ResolveArgs& a, hipStream_t st) {
     hipLaunchKernelGGL(k_resolve, dim3(1), dim3(RESOLVE_THREADS), 0, st, a);

@@ -44,9 +44,15 @@ struct ScanArgs {
     const int32_t* blm;
     const int32_t* posm;
     int allow_leader, rebalance, sem_go;
-    double2* blockrec;        // [tiles] per-tile min score delta {leader, non-leader}
+    BlockRec* blockrec;       // [tiles] per-tile record (k_reduce combines)
     Contender* cont;
     uint32_t cont_cap;
+};
+
+struct ReduceArgs {
+    DevCtl* ctl;
+    const BlockRec* blockrec;
+    int tiles;
 };
 
 struct ResolveArgs {
@@ -96,6 +102,7 @@ void launch_prep(const PrepArgs& a, hipStream_t st);
 void launch_setlists(const SetArgs& a, hipStream_t st);
 void launch_scan(const ScanArgs& a, int rc, int tiles, hipStream_t st);
 void launch_census(const ScanArgs& a, int rc, int tiles, hipStream_t st);
+void launch_reduce(const ReduceArgs& a, hipStream_t st);
 void launch_resolve(const ResolveArgs& a, hipStream_t st);
 void launch_summary(const SumArgs& a, hipStream_t st);
 void launch_merge(const MergeArgs& a, hipStream_t st);

@@ -290,13 +290,13 @@ class Engine:
         lib().kb_engine_stats(self.h, C.byref(s))
         return {f: getattr(s, f) for f, _ in s._fields_}
 
-    KERNELS = ("prep", "setlists", "scan", "census", "resolve")
+    KERNELS = ("prep", "setlists", "scan", "reduce", "census", "resolve")
 
     def timings(self):
         """{kernel: (total_ms, launches)} of the last plan (time_kernels=True)."""
-        ms = np.zeros(5)
-        n = np.zeros(5, np.int64)
-        lib().kb_engine_timings(self.h, ms.ctypes.data_as(PD), n.ctypes.data_as(P64), 5)
+        ms = np.zeros(6)
+        n = np.zeros(6, np.int64)
+        lib().kb_engine_timings(self.h, ms.ctypes.data_as(PD), n.ctypes.data_as(P64), 6)
         return {k: (float(ms[i]), int(n[i])) for i, k in enumerate(self.KERNELS)}
 
     # multi-GPU step phases

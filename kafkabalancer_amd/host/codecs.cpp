@@ -1,0 +1,566 @@
+// codecs.cpp -- reference codecs (codecs.go:15-93) with Go encoding/json and
+// regexp behaviour:
+//   * JSON in: json.Decoder.Decode into PartitionList (case-insensitive field
+//     match, unknown fields ignored, ints must be integer literals, first type
+//     error wins, syntax errors first), then the version==1 check (codecs.go:24-26)
+//   * text in: `kafka-topics.sh --describe` lines matched by
+//     ^\tTopic: ([^\t]*)\tPartition: ([0-9]*)\tLeader: ([0-9]*)\tReplicas: ([0-9,]*)\tIsr: ([0-9,]*)
+//     with Atoi errors ignored (codecs.go:28-56), bufio.Scanner 64 KiB lines
+//   * JSON out: Go encoding/json bytes (HTML-escaped strings, omitempty,
+//     shortest float formatting), trailing newline (json.Encoder)
+#include "codecs.hpp"
+
+#include <charconv>
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <set>
+#include <utility>
+
+namespace kbh {
+
+std::string Partition::str() const {
+    std::string s = "Partition(" + topic + "," + std::to_string((long long)partition) + ",[";
+    for (size_t i = 0; i < replicas.len; i++) {
+        if (i) s += " ";
+        s += std::to_string((long long)replicas.at(i));
+    }
+    return s + "])";
+}
+
+// ------------------------------------------------------------ floats
+
+static void shortest(double x, std::string& digits, int& e10) {
+    // shortest round-trip digits d1.d2d3... x 10^e10
+    char buf[64];
+    auto r = std::to_chars(buf, buf + sizeof buf, std::fabs(x), std::chars_format::scientific);
+    std::string t(buf, r.ptr);
+    size_t epos = t.find('e');
+    std::string m = t.substr(0, epos);
+    e10 = std::atoi(t.c_str() + epos + 1);
+    digits.clear();
+    for (char c : m) if (c != '.') digits += c;
+    while (digits.size() > 1 && digits.back() == '0') digits.pop_back();
+}
+
+std::string GoFloat(double x) {
+    if (x == 0) return std::signbit(x) ? "-0" : "0";
+    std::string d;
+    int e10;
+    shortest(x, d, e10);
+    std::string o = x < 0 ? "-" : "";
+    double a = std::fabs(x);
+    if (a < 1e-6 || a >= 1e21) {
+        o += d[0];
+        if (d.size() > 1) o += "." + d.substr(1);
+        o += "e";
+        if (e10 < 0) o += "-" + std::to_string(-e10);          // e-07 -> e-7 cleanup
+        else { o += "+"; if (e10 < 10) o += "0"; o += std::to_string(e10); }
+        return o;
+    }
+    int point = e10 + 1;
+    if (point <= 0) o += "0." + std::string((size_t)-point, '0') + d;
+    else if (point >= (int)d.size()) o += d + std::string((size_t)(point - (int)d.size()), '0');
+    else o += d.substr(0, (size_t)point) + "." + d.substr((size_t)point);
+    return o;
+}
+
+std::string GoFloatG(double x) {
+    if (x == 0) return std::signbit(x) ? "-0" : "0";
+    if (std::isinf(x)) return x > 0 ? "+Inf" : "-Inf";
+    if (std::isnan(x)) return "NaN";
+    std::string d;
+    int e10;
+    shortest(x, d, e10);
+    std::string o = x < 0 ? "-" : "";
+    int exp = e10;
+    if (exp < -4 || exp >= 21) {
+        o += d[0];
+        if (d.size() > 1) o += "." + d.substr(1);
+        char eb[16];
+        snprintf(eb, sizeof eb, "e%c%02d", exp < 0 ? '-' : '+', exp < 0 ? -exp : exp);
+        return o + eb;
+    }
+    int point = e10 + 1;
+    if (point <= 0) o += "0." + std::string((size_t)-point, '0') + d;
+    else if (point >= (int)d.size()) o += d + std::string((size_t)(point - (int)d.size()), '0');
+    else o += d.substr(0, (size_t)point) + "." + d.substr((size_t)point);
+    return o;
+}
+
+// ------------------------------------------------------- JSON parsing
+
+namespace {
+
+struct JVal {
+    enum Kind { OBJ, ARR, STR, NUM, BOOL, NUL } k = NUL;
+    std::string s;                                   // string value / number literal
+    bool b = false;
+    std::vector<std::pair<std::string, JVal>> obj;
+    std::vector<JVal> arr;
+};
+
+std::string quote_char(unsigned char c) {
+    if (c == '\'') return "'\\''";
+    if (c == '"') return "'\"'";
+    if (c >= 0x20 && c < 0x7f) return std::string("'") + (char)c + "'";
+    char b[16];
+    switch (c) {
+        case '\n': return "'\\n'";
+        case '\r': return "'\\r'";
+        case '\t': return "'\\t'";
+        default: snprintf(b, sizeof b, "'\\x%02x'", c); return b;
+    }
+}
+
+struct Parser {
+    const std::string& in;
+    size_t i = 0;
+    std::string err;
+    explicit Parser(const std::string& s) : in(s) {}
+
+    void ws() { while (i < in.size() && (in[i] == ' ' || in[i] == '\t' || in[i] == '\n' || in[i] == '\r')) i++; }
+    bool fail(const std::string& m) { if (err.empty()) err = m; return false; }
+    bool eof_mid() { return fail("unexpected EOF"); }
+
+    bool value(JVal& v, const char* ctx) {
+        ws();
+        if (i >= in.size()) return eof_mid();
+        char c = in[i];
+        if (c == '{') return object(v);
+        if (c == '[') return array(v);
+        if (c == '"') { v.k = JVal::STR; return str(v.s); }
+        if (c == '-' || (c >= '0' && c <= '9')) return number(v);
+        if (c == 't') return literal(v, "true", JVal::BOOL, true);
+        if (c == 'f') return literal(v, "false", JVal::BOOL, false);
+        if (c == 'n') return literal(v, "null", JVal::NUL, false);
+        return fail("invalid character " + quote_char((unsigned char)c) + " " + ctx);
+    }
+    bool literal(JVal& v, const char* lit, JVal::Kind k, bool b) {
+        size_t n = strlen(lit);
+        for (size_t j = 0; j < n; j++) {
+            if (i + j >= in.size()) return eof_mid();
+            if (in[i + j] != lit[j])
+                return fail("invalid character " + quote_char((unsigned char)in[i + j]) + " in literal " +
+                            lit + " (expecting " + quote_char((unsigned char)lit[j]) + ")");
+        }
+        i += n;
+        v.k = k;
+        v.b = b;
+        return true;
+    }
+    bool number(JVal& v) {
+        size_t st = i;
+        if (in[i] == '-') i++;
+        if (i >= in.size()) return eof_mid();
+        if (in[i] == '0') i++;
+        else if (in[i] >= '1' && in[i] <= '9') { while (i < in.size() && isdigit((unsigned char)in[i])) i++; }
+        else return fail("invalid character " + quote_char((unsigned char)in[i]) + " in numeric literal");
+        if (i < in.size() && in[i] == '.') {
+            i++;
+            if (i >= in.size()) return eof_mid();
+            if (!isdigit((unsigned char)in[i])) return fail("invalid character " + quote_char((unsigned char)in[i]) + " after decimal point in numeric literal");
+            while (i < in.size() && isdigit((unsigned char)in[i])) i++;
+        }
+        if (i < in.size() && (in[i] == 'e' || in[i] == 'E')) {
+            i++;
+            if (i < in.size() && (in[i] == '+' || in[i] == '-')) i++;
+            if (i >= in.size()) return eof_mid();
+            if (!isdigit((unsigned char)in[i])) return fail("invalid character " + quote_char((unsigned char)in[i]) + " in exponent of numeric literal");
+            while (i < in.size() && isdigit((unsigned char)in[i])) i++;
+        }
+        v.k = JVal::NUM;
+        v.s = in.substr(st, i - st);
+        return true;
+    }
+    static void put_utf8(std::string& o, uint32_t cp) {
+        if (cp < 0x80) o += (char)cp;
+        else if (cp < 0x800) { o += (char)(0xC0 | (cp >> 6)); o += (char)(0x80 | (cp & 63)); }
+        else if (cp < 0x10000) { o += (char)(0xE0 | (cp >> 12)); o += (char)(0x80 | ((cp >> 6) & 63)); o += (char)(0x80 | (cp & 63)); }
+        else { o += (char)(0xF0 | (cp >> 18)); o += (char)(0x80 | ((cp >> 12) & 63)); o += (char)(0x80 | ((cp >> 6) & 63)); o += (char)(0x80 | (cp & 63)); }
+    }
+    bool hex4(uint32_t& v) {
+        v = 0;
+        for (int j = 0; j < 4; j++) {
+            if (i >= in.size()) return eof_mid();
+            char c = in[i++];
+            v <<= 4;
+            if (c >= '0' && c <= '9') v |= (uint32_t)(c - '0');
+            else if (c >= 'a' && c <= 'f') v |= (uint32_t)(c - 'a' + 10);
+            else if (c >= 'A' && c <= 'F') v |= (uint32_t)(c - 'A' + 10);
+            else return fail("invalid character " + quote_char((unsigned char)c) + " in \\u hexadecimal character escape");
+        }
+        return true;
+    }
+    bool str(std::string& o) {
+        i++;  // opening quote
+        o.clear();
+        for (;;) {
+            if (i >= in.size()) return eof_mid();
+            unsigned char c = (unsigned char)in[i];
+            if (c == '"') { i++; return true; }
+            if (c < 0x20) return fail("invalid character " + quote_char(c) + " in string literal");
+            if (c == '\\') {
+                i++;
+                if (i >= in.size()) return eof_mid();
+                char e = in[i++];
+                switch (e) {
+                    case '"': o += '"'; break;
+                    case '\\': o += '\\'; break;
+                    case '/': o += '/'; break;
+                    case 'b': o += '\b'; break;
+                    case 'f': o += '\f'; break;
+                    case 'n': o += '\n'; break;
+                    case 'r': o += '\r'; break;
+                    case 't': o += '\t'; break;
+                    case 'u': {
+                        uint32_t cp;
+                        if (!hex4(cp)) return false;
+                        if (cp >= 0xD800 && cp < 0xDC00 && i + 1 < in.size() && in[i] == '\\' && in[i + 1] == 'u') {
+                            size_t save = i;
+                            i += 2;
+                            uint32_t lo;
+                            if (!hex4(lo)) return false;
+                            if (lo >= 0xDC00 && lo < 0xE000) cp = 0x10000 + ((cp - 0xD800) << 10) + (lo - 0xDC00);
+                            else { i = save; cp = 0xFFFD; }
+                        } else if (cp >= 0xD800 && cp < 0xE000) {
+                            cp = 0xFFFD;
+                        }
+                        put_utf8(o, cp);
+                        break;
+                    }
+                    default:
+                        return fail("invalid character " + quote_char((unsigned char)e) + " in string escape code");
+                }
+                continue;
+            }
+            o += (char)c;
+            i++;
+        }
+    }
+    bool object(JVal& v) {
+        v.k = JVal::OBJ;
+        i++;
+        ws();
+        if (i >= in.size()) return eof_mid();
+        if (in[i] == '}') { i++; return true; }
+        for (;;) {
+            ws();
+            if (i >= in.size()) return eof_mid();
+            if (in[i] != '"') return fail("invalid character " + quote_char((unsigned char)in[i]) + " looking for beginning of object key string");
+            std::string key;
+            if (!str(key)) return false;
+            ws();
+            if (i >= in.size()) return eof_mid();
+            if (in[i] != ':') return fail("invalid character " + quote_char((unsigned char)in[i]) + " after object key");
+            i++;
+            JVal val;
+            if (!value(val, "looking for beginning of value")) return false;
+            v.obj.emplace_back(std::move(key), std::move(val));
+            ws();
+            if (i >= in.size()) return eof_mid();
+            if (in[i] == ',') { i++; continue; }
+            if (in[i] == '}') { i++; return true; }
+            return fail("invalid character " + quote_char((unsigned char)in[i]) + " after object key:value pair");
+        }
+    }
+    bool array(JVal& v) {
+        v.k = JVal::ARR;
+        i++;
+        ws();
+        if (i >= in.size()) return eof_mid();
+        if (in[i] == ']') { i++; return true; }
+        for (;;) {
+            JVal el;
+            if (!value(el, "looking for beginning of value")) return false;
+            v.arr.push_back(std::move(el));
+            ws();
+            if (i >= in.size()) return eof_mid();
+            if (in[i] == ',') { i++; continue; }
+            if (in[i] == ']') { i++; return true; }
+            return fail("invalid character " + quote_char((unsigned char)in[i]) + " after array element");
+        }
+    }
+};
+
+const char* kind_name(const JVal& v) {
+    switch (v.k) {
+        case JVal::OBJ: return "object";
+        case JVal::ARR: return "array";
+        case JVal::STR: return "string";
+        case JVal::NUM: return "number";
+        case JVal::BOOL: return "bool";
+        default: return "null";
+    }
+}
+
+bool fold_eq(const std::string& a, const char* b) {
+    size_t n = strlen(b);
+    if (a.size() != n) return false;
+    for (size_t i = 0; i < n; i++) if (tolower((unsigned char)a[i]) != tolower((unsigned char)b[i])) return false;
+    return true;
+}
+
+struct Decoder {
+    std::string err;   // first UnmarshalTypeError
+    void type_err(const JVal& v, const std::string& field, const std::string& type) {
+        if (!err.empty()) return;
+        std::string what = kind_name(v);
+        if (v.k == JVal::NUM) what += " " + v.s;
+        err = "json: cannot unmarshal " + what + " into Go struct field " + field + " of type " + type;
+    }
+    void to_int(const JVal& v, int64_t& out, const std::string& field, const std::string& type) {
+        if (v.k == JVal::NUL) return;
+        if (v.k != JVal::NUM) return type_err(v, field, type);
+        const char* s = v.s.c_str();
+        errno = 0;
+        char* end = nullptr;
+        long long x = strtoll(s, &end, 10);
+        if (errno || *end) return type_err(v, field, type);
+        out = x;
+    }
+    void to_float(const JVal& v, double& out, const std::string& field) {
+        if (v.k == JVal::NUL) return;
+        if (v.k != JVal::NUM) return type_err(v, field, "float64");
+        errno = 0;
+        double x = strtod(v.s.c_str(), nullptr);
+        if (errno == ERANGE && std::isinf(x)) return type_err(v, field, "float64");
+        out = x;
+    }
+    void to_ints(const JVal& v, Slice& out, const std::string& field, const std::string& elem) {
+        if (v.k == JVal::NUL) { out = Slice(); return; }
+        if (v.k != JVal::ARR) return type_err(v, field, "[]" + elem);
+        std::vector<int64_t> xs;
+        for (const JVal& e : v.arr) {
+            int64_t x = 0;
+            to_int(e, x, field, elem);
+            xs.push_back(x);
+        }
+        out = Slice::of(xs);
+    }
+    void partition(const JVal& v, Partition& p) {
+        if (v.k == JVal::NUL) return;
+        if (v.k != JVal::OBJ) return type_err(v, "PartitionList.partitions", "main.Partition");
+        for (const auto& kv : v.obj) {
+            const std::string& k = kv.first;
+            const JVal& x = kv.second;
+            if (fold_eq(k, "topic")) {
+                if (x.k == JVal::NUL) continue;
+                if (x.k != JVal::STR) type_err(x, "Partition.partitions.topic", "main.TopicName");
+                else p.topic = x.s;
+            } else if (fold_eq(k, "partition")) {
+                to_int(x, p.partition, "Partition.partitions.partition", "main.PartitionID");
+            } else if (fold_eq(k, "replicas")) {
+                to_ints(x, p.replicas, "Partition.partitions.replicas", "main.BrokerID");
+            } else if (fold_eq(k, "weight")) {
+                to_float(x, p.weight, "Partition.partitions.weight");
+            } else if (fold_eq(k, "num_replicas")) {
+                to_int(x, p.num_replicas, "Partition.partitions.num_replicas", "int");
+            } else if (fold_eq(k, "brokers")) {
+                to_ints(x, p.brokers, "Partition.partitions.brokers", "main.BrokerID");
+            } else if (fold_eq(k, "num_consumers")) {
+                to_int(x, p.num_consumers, "Partition.partitions.num_consumers", "int");
+            }
+        }
+    }
+    void plist(const JVal& v, PartitionList& pl) {
+        if (v.k == JVal::NUL) return;
+        if (v.k != JVal::OBJ) {
+            if (err.empty()) err = std::string("json: cannot unmarshal ") + kind_name(v) + " into Go value of type main.PartitionList";
+            return;
+        }
+        for (const auto& kv : v.obj) {
+            if (fold_eq(kv.first, "version")) {
+                to_int(kv.second, pl.version, "PartitionList.version", "int");
+            } else if (fold_eq(kv.first, "partitions")) {
+                const JVal& a = kv.second;
+                if (a.k == JVal::NUL) { pl.partitions.clear(); pl.nil_partitions = true; continue; }
+                if (a.k != JVal::ARR) { type_err(a, "PartitionList.partitions", "[]main.Partition"); continue; }
+                pl.partitions.clear();
+                pl.nil_partitions = false;
+                for (const JVal& e : a.arr) {
+                    Partition p;
+                    partition(e, p);
+                    pl.partitions.push_back(std::move(p));
+                }
+            }
+        }
+    }
+};
+
+// Atoi with the reference's ignored error: value on success, 0 otherwise
+int64_t atoi_go(const std::string& s) {
+    if (s.empty()) return 0;
+    errno = 0;
+    char* end = nullptr;
+    long long x = strtoll(s.c_str(), &end, 10);
+    if (errno || *end) return 0;
+    return x;
+}
+
+bool take(const std::string& l, size_t& i, const char* lit) {
+    size_t n = strlen(lit);
+    if (l.compare(i, n, lit) != 0) return false;
+    i += n;
+    return true;
+}
+std::string span(const std::string& l, size_t& i, const char* set) {
+    size_t st = i;
+    while (i < l.size() && strchr(set, l[i]) && l[i]) i++;
+    return l.substr(st, i - st);
+}
+
+}  // namespace
+
+std::string GetPartitionListFromReader(const std::string& in, bool json,
+                                       const std::vector<std::string>& topics, PartitionList* out) {
+    PartitionList pl;
+    if (json) {
+        Parser ps(in);
+        ps.ws();
+        if (ps.i >= in.size()) return "failed parsing json: EOF";
+        JVal v;
+        if (!ps.value(v, "looking for beginning of value")) return "failed parsing json: " + ps.err;
+        Decoder d;
+        d.plist(v, pl);
+        if (!d.err.empty()) return "failed parsing json: " + d.err;
+        if (pl.version != 1)
+            return "wrong partition list version: expected 1, got " + std::to_string((long long)pl.version);
+    } else {
+        size_t pos = 0;
+        while (pos <= in.size()) {
+            size_t nl = in.find('\n', pos);
+            if (nl == std::string::npos) {
+                if (pos == in.size()) break;
+                nl = in.size();
+            }
+            std::string line = in.substr(pos, nl - pos);
+            pos = nl + 1;
+            if (!line.empty() && line.back() == '\r') line.pop_back();
+            if (line.size() > 65536) return "failed reading file: bufio.Scanner: token too long";
+            size_t i = 0;
+            if (!take(line, i, "\tTopic: ")) continue;
+            size_t t0 = i;
+            while (i < line.size() && line[i] != '\t') i++;
+            std::string topic = line.substr(t0, i - t0);
+            if (!take(line, i, "\tPartition: ")) continue;
+            std::string part = span(line, i, "0123456789");
+            if (!take(line, i, "\tLeader: ")) continue;
+            span(line, i, "0123456789");
+            if (!take(line, i, "\tReplicas: ")) continue;
+            std::string reps = span(line, i, "0123456789,");
+            if (!take(line, i, "\tIsr: ")) continue;
+            if (!topics.empty()) {
+                bool found = false;
+                for (const auto& t : topics) found |= t == topic;
+                if (!found) continue;
+            }
+            Partition p;
+            p.topic = topic;
+            p.partition = atoi_go(part);
+            std::vector<int64_t> rs;
+            size_t a = 0;
+            for (;;) {
+                size_t c = reps.find(',', a);
+                rs.push_back(atoi_go(reps.substr(a, c == std::string::npos ? std::string::npos : c - a)));
+                if (c == std::string::npos) break;
+                a = c + 1;
+            }
+            p.replicas = Slice::of(rs);
+            pl.partitions.push_back(std::move(p));
+            pl.nil_partitions = false;
+        }
+    }
+    if (pl.partitions.empty()) return "empty partition list";
+    *out = std::move(pl);
+    return "";
+}
+
+// ------------------------------------------------------- JSON output
+
+static void json_string(std::string& o, const std::string& s) {
+    static const char* hx = "0123456789abcdef";
+    o += '"';
+    size_t i = 0;
+    while (i < s.size()) {
+        unsigned char c = (unsigned char)s[i];
+        if (c < 0x80) {
+            if (c == '"' || c == '\\') { o += '\\'; o += (char)c; }
+            else if (c == '\n') o += "\\n";
+            else if (c == '\r') o += "\\r";
+            else if (c == '\t') o += "\\t";
+            else if (c == '\b') o += "\\b";
+            else if (c == '\f') o += "\\f";
+            else if (c < 0x20 || c == '<' || c == '>' || c == '&') {
+                o += "\\u00"; o += hx[c >> 4]; o += hx[c & 15];
+            } else o += (char)c;
+            i++;
+            continue;
+        }
+        // validate one UTF-8 sequence; invalid bytes become � (Go encodeState.string)
+        int n = (c >= 0xF0 && c < 0xF5) ? 4 : (c >= 0xE0) ? 3 : (c >= 0xC2 && c < 0xE0) ? 2 : 0;
+        bool ok = n > 0 && i + (size_t)n <= s.size();
+        uint32_t cp = n == 2 ? (c & 0x1F) : n == 3 ? (c & 0x0F) : (c & 0x07);
+        for (int k = 1; ok && k < n; k++) {
+            unsigned char cc = (unsigned char)s[i + (size_t)k];
+            if ((cc & 0xC0) != 0x80) ok = false;
+            cp = (cp << 6) | (cc & 0x3F);
+        }
+        if (ok && ((n == 3 && (cp < 0x800 || (cp >= 0xD800 && cp < 0xE000))) || (n == 4 && (cp < 0x10000 || cp > 0x10FFFF)))) ok = false;
+        if (!ok) { o += "\\ufffd"; i++; continue; }
+        if (cp == 0x2028 || cp == 0x2029) { o += cp == 0x2028 ? "\\u2028" : "\\u2029"; i += (size_t)n; continue; }
+        o.append(s, i, (size_t)n);
+        i += (size_t)n;
+    }
+    o += '"';
+}
+
+static void json_ints(std::string& o, const Slice& s) {
+    if (s.nil()) { o += "null"; return; }
+    o += '[';
+    for (size_t i = 0; i < s.len; i++) {
+        if (i) o += ',';
+        o += std::to_string((long long)s.at(i));
+    }
+    o += ']';
+}
+
+std::string EncodePartitionList(PartitionList& pl) {
+    pl.version = 1;                                           // codecs.go:86
+    std::string o = "{\"version\":1,\"partitions\":";
+    if (pl.nil_partitions && pl.partitions.empty()) o += "null";
+    else {
+        o += '[';
+        for (size_t i = 0; i < pl.partitions.size(); i++) {
+            const Partition& p = pl.partitions[i];
+            if (i) o += ',';
+            o += "{\"topic\":";
+            json_string(o, p.topic);
+            o += ",\"partition\":" + std::to_string((long long)p.partition) + ",\"replicas\":";
+            json_ints(o, p.replicas);
+            if (p.weight != 0) o += ",\"weight\":" + GoFloat(p.weight);
+            if (p.num_replicas != 0) o += ",\"num_replicas\":" + std::to_string((long long)p.num_replicas);
+            if (!p.brokers.nil() && p.brokers.len > 0) { o += ",\"brokers\":"; json_ints(o, p.brokers); }
+            if (p.num_consumers != 0) o += ",\"num_consumers\":" + std::to_string((long long)p.num_consumers);
+            o += '}';
+        }
+        o += ']';
+    }
+    o += "}\n";
+    return o;
+}
+
+PartitionList FilterPartitionList(const PartitionList& pl) {
+    PartitionList out;
+    out.version = pl.version;
+    std::set<std::pair<std::string, int64_t>> seen;
+    for (const Partition& p : pl.partitions) {
+        if (seen.insert({p.topic, p.partition}).second) {
+            out.partitions.push_back(p);
+            out.nil_partitions = false;
+        }
+    }
+    return out;
+}
+
+}  // namespace kbh

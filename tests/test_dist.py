@@ -1,0 +1,186 @@
+"""Multi-rank plan protocol (kafkabalancer_amd/dist.py).
+
+CPU: world_size-2 gloo run of ShardedPlanner with a CPU engine that follows the
+same summary protocol (each rank scores its shard exactly, the merge takes the
+lexicographic (U, iteration) minimum) -- checks the exchange and that every
+rank applies the identical change, against the single-process oracle plan.
+
+GPU: two device engines on disjoint shards of one cluster on one GPU, their
+summaries concatenated as the all-gather would, against one unsharded engine.
+"""
+import os
+import random
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from kafkabalancer_amd.dist import ShardedPlanner, shard_bounds
+from oracle import pyref
+
+from helpers import default_cfg
+
+
+def _cluster(seed, P=40, B=6):
+    rng = random.Random(seed)
+    parts = []
+    for i in range(P):
+        reps = rng.sample(range(1, B + 1), 3)
+        parts.append({"topic": "t", "partition": i, "replicas": reps,
+                      "weight": float(rng.randint(1, 4))})
+    return {"version": 1, "partitions": parts}
+
+
+class CpuShardEngine:
+    """Exact move() restricted to a shard (steps.go:210-297), summary = (U, iter)."""
+
+    def __init__(self, plist, cfg, begin, end):
+        self.pl = pyref.normalize(plist)
+        pyref.balance([dict(p, replicas=list(p["replicas"])) for p in self.pl], cfg)  # validates
+        self.cfg = cfg
+        self.begin, self.end = begin, end
+        # FillDefaults on the local state
+        for p in self.pl:
+            p["brokers"] = sorted({r for q in self.pl for r in q["replicas"]}) if p["brokers"] is None else p["brokers"]
+            p["num_replicas"] = p["num_replicas"] or len(p["replicas"])
+
+    def summary_bytes(self):
+        return 4 * 8
+
+    def step_begin(self, summary):
+        loads = pyref.broker_load(self.pl)
+        bl = pyref.get_bl(loads)
+        su = pyref.unbalance(bl)
+        best = (float("inf"), float("inf"), -1.0, -1.0)
+        for i in range(self.begin, self.end):
+            p = self.pl[i]
+            if p["num_replicas"] < self.cfg["min_replicas"]:
+                continue
+            for slot in range(1, len(p["replicas"])):
+                r = p["replicas"][slot]
+                ridx = [k for k, x in enumerate(bl) if x[0] == r][0]
+                rl = bl[ridx][1]
+                bl[ridx][1] -= p["weight"]
+                for k, (b, l) in enumerate(bl):
+                    if b not in p["brokers"] or b in p["replicas"]:
+                        continue
+                    bl[k][1] = l + p["weight"]
+                    u = pyref.unbalance(bl)
+                    it = (i * 32 + slot) * 4096 + k
+                    if (u, it) < best[:2]:
+                        best = (u, float(it), float(i), float(b))
+                    bl[k][1] = l
+                bl[ridx][1] = rl
+        self.su = su
+        summary.copy_(torch.from_numpy(np.array(best, np.float64)).view(torch.uint8))
+
+    def step_finish(self, gathered, world):
+        recs = gathered.view(torch.float64).reshape(world, 4).tolist()
+        u, it, i, b = min(recs, key=lambda x: (x[0], x[1]))
+        if not (u < self.su - self.cfg["min_unbalance"]):
+            return None
+        i, b = int(i), int(b)
+        slot = (int(it) // 4096) % 32
+        p = self.pl[i]
+        frm = p["replicas"][slot]
+        p["replicas"][slot] = b
+        return {"pidx": i, "slot": slot, "from_": frm, "to": b}
+
+
+def _worker(rank, world, port, plist, cfg, steps, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    n = len(plist["partitions"])
+    # shard on small tiles for the test (the device engine uses 1024)
+    per = -(-n // world)
+    begin, end = rank * per, min(n, (rank + 1) * per)
+    eng = CpuShardEngine(plist, cfg, begin, end)
+    sp = ShardedPlanner(eng, world, device_tensors=False)
+    out = sp.plan(steps)
+    q.put((rank, [(c["pidx"], c["slot"], c["from_"], c["to"]) for c in out],
+           [p["replicas"] for p in eng.pl]))
+    dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_gloo_two_ranks_match_single_process(seed):
+    plist = _cluster(seed)
+    cfg = default_cfg(min_unbalance=0.0)
+    steps = 8
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, plist, cfg, steps, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict((r, (ch, st)) for r, ch, st in [q.get(timeout=300) for _ in procs])
+    for p in procs:
+        p.join(timeout=60)
+    assert res[0] == res[1]                      # every rank applied the identical plan
+    # the single-process reference plan
+    pl = pyref.normalize(plist)
+    want = []
+    for _ in range(steps):
+        r = pyref.balance(pl, cfg)
+        if r is None:
+            break
+        want.append((r[1], r[3], r[4]))
+    got = [(i, f, t) for i, _, f, t in res[0][0]]
+    assert got == want
+    assert res[0][1] == [p["replicas"] for p in pl]
+
+
+def test_shard_bounds_cover_and_align():
+    for n in [1, 1000, 1024, 5000, 1_000_001]:
+        for world in [1, 2, 3, 8]:
+            spans = [shard_bounds(n, world, r) for r in range(world)]
+            assert spans[0][0] == 0 and spans[-1][1] == n
+            for (a, b), (c, d) in zip(spans, spans[1:]):
+                assert b == c
+            assert all(a % 1024 == 0 or a == b for a, b in spans)   # aligned or empty
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("workload", ["zipf-sets", "uniform"])
+def test_two_engines_one_gpu_match_unsharded(workload):
+    from kafkabalancer_amd import engine as E
+    from kafkabalancer_amd import synth
+    if workload == "zipf-sets":
+        cl = synth.make_cluster(5000, 200, 3, "zipf", nsets=16, set_size=40, seed=3)
+        cfg = default_cfg(allow_leader=True, min_unbalance=0.0)
+    else:
+        cl = synth.make_cluster(5000, 60, 3, "uniform", seed=4)
+        cfg = default_cfg(min_unbalance=0.0)
+    ref = E.Engine(cl, cfg)
+    want, err = ref.plan(30)
+    assert err is None
+    world = 2
+    engs = [E.Engine(cl, cfg, shard=shard_bounds(cl.n, world, r)) for r in range(world)]
+    nb = engs[0].summary_bytes()
+    bufs = [torch.zeros(nb, dtype=torch.uint8, device="cuda") for _ in range(world)]
+    got = []
+    for _ in range(30):
+        for e, b in zip(engs, bufs):
+            e.step_begin(b.data_ptr())
+        torch.cuda.synchronize()
+        gathered = torch.cat(bufs)
+        chs = [e.step_finish(gathered.data_ptr(), world) for e in engs]
+        assert chs[0] == chs[1]
+        if chs[0] is None:
+            break
+        got.append(chs[0])
+    key = lambda c: (c["step"], c["pidx"], c["kind"], c["from_"], c["to"], c["slot"])
+    assert [key(c) for c in got] == [key(c) for c in want]
+    assert engs[0].state() == ref.state() == engs[1].state()
