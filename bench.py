@@ -66,7 +66,11 @@ def main():
     ap.add_argument("--scale", type=float, default=1.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--stamps", action="store_true",
+                    help="diagnostic: load the -DKB_STAMPS build and print per-phase times (not a bench line)")
     args = ap.parse_args()
+    if args.stamps:
+        os.environ["KB_ENGINE_LIB"] = os.path.join(ROOT, "kafkabalancer_amd", "lib", "libkbengine_stamps.so")
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -120,6 +124,14 @@ def main():
                      "avg_launch_us": scan_avg_us},
         "kernels_us_per_step": {k: 1e3 * v[0] / max(v[1], 1) for k, v in tk.items()},
     }
+    if args.stamps:
+        st = eng.stamps()
+        n = max(1, st1["steps"])
+        names = ["prep.load", "prep.sort", "prep.compact", "prep.Sfold", "prep.terms", "prep.Ufold",
+                 "prep.bounds", "prep.LT", "res.stage+pred", "res.move", "res.apply", "res.lists",
+                 "res.refold+log"]
+        print(json.dumps({"stamps_us_per_step": {k: st[i] / 100.0 / n for i, k in enumerate(names)}}))
+        return
     if not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(cl, cfg, args.cpu_seconds)
         out["speedup_vs_cpu"] = out["value"] / out["cpu_baseline"]["value"]

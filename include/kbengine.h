@@ -169,6 +169,10 @@ int kb_engine_stats(kb_engine *e, kb_stats *out);
  * for k in {0 prep, 1 setlists, 2 scan, 3 reduce, 4 census, 5 resolve}.  Returns 6. */
 int kb_engine_timings(kb_engine *e, double *ms, int64_t *launches, int n);
 
+/* Diagnostic: accumulated in-kernel phase stamps (100 MHz ticks) of k_prep
+ * [0..7] and k_resolve [8..12]; non-zero only in a -DKB_STAMPS build. */
+int kb_engine_stamps(kb_engine *e, uint64_t *out, int n);
+
 /* Reference-format message of the last error ("<Step>: partition Partition(t,p,[..]) ..."). */
 int kb_engine_last_error(kb_engine *e, char *buf, size_t n);
 

@@ -65,11 +65,11 @@ struct kb_engine {
     uint8_t* incfg = nullptr;
     uint64_t* setbits = nullptr;
     int32_t* lists = nullptr;
-    int32_t* nelig = nullptr;
+    unsigned char* setrec = nullptr;
     int32_t* order = nullptr;
     int32_t* blm = nullptr;
     int32_t* posm = nullptr;
-    double2* LT = nullptr;
+    double* r = nullptr;
     BlockRec* blockrec = nullptr;
     Contender* cont = nullptr;
     uint32_t cont_cap = 1u << 20;
@@ -242,7 +242,7 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
     e->nsets = (int64_t)sets.size();
     if (e->nsets == 0) { sets.emplace_back(); e->nsets = 1; }
     if ((uint64_t)e->nsets >= MAX_SETS) {
-        e->last_err = "too many distinct broker lists";
+        e->last_err = "engine supports at most 32767 distinct broker lists";
         *out = e;
         return KB_ERR_UNSUPPORTED;
     }
@@ -338,16 +338,26 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
         hw[i] = wt[i];
         uint32_t elig = want[i] >= e->minrep ? 1u : 0u;
         uint32_t wnt = want[i] < 0 ? 0u : (uint32_t)std::min<int64_t>(want[i], 31);
-        hm[i] = make_meta((uint32_t)len[i], wnt, elig, (uint32_t)pset[i]);
         for (int k = 0; k < len[i]; k++) hr[(size_t)k * e->Ppad + i] = dense[c->replica_off[i] - c->replica_off[0] + k];
         hnc[i] = (int32_t)ncon[i];
-    }
-    if (e->pending) {
-        // a step will only report the error; keep state for queries
     }
     std::vector<uint64_t> hsb((size_t)e->nsets * e->W64, 0);
     for (int64_t s = 0; s < e->nsets; s++)
         for (int b : sets[s]) hsb[(size_t)s * e->W64 + (b >> 6)] |= 1ull << (b & 63);
+    for (int64_t i = 0; i < n; i++) {
+        // Disallowed trigger (a replica outside the allowed set) and the in-set count
+        uint32_t dis = 0, nin = 0;
+        const uint64_t* sb = &hsb[(size_t)pset[i] * e->W64];
+        for (int k = 0; k < len[i]; k++) {
+            const int b = dense[c->replica_off[i] - c->replica_off[0] + k];
+            const bool in = (sb[b >> 6] >> (b & 63)) & 1ull;
+            dis |= in ? 0u : 1u;
+            nin += in ? 1u : 0u;
+        }
+        const uint32_t elig = want[i] >= e->minrep ? 1u : 0u;
+        const uint32_t wnt = want[i] < 0 ? 0u : (uint32_t)std::min<int64_t>(want[i], 31);
+        hm[i] = make_meta((uint32_t)len[i], wnt, elig, dis, nin, (uint32_t)pset[i]);
+    }
     std::vector<uint8_t> hin(e->B, 0);
     if (!cfg->brokers_nil)
         for (int64_t k = 0; k < cfg->n_brokers; k++) hin[idmap[cfg->brokers[k]]] = 1;
@@ -387,12 +397,12 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
     HIPCHK(dalloc(&e->cnt, e->B));
     HIPCHK(dalloc(&e->incfg, e->B));
     HIPCHK(dalloc(&e->setbits, (size_t)e->nsets * e->W64));
-    HIPCHK(dalloc(&e->lists, (size_t)e->nsets * 3 * e->K));
-    HIPCHK(dalloc(&e->nelig, e->nsets));
+    HIPCHK(dalloc(&e->lists, (size_t)e->nsets * 2 * e->K));
+    HIPCHK(dalloc(&e->setrec, (size_t)e->nsets * sr_stride(e->K)));
     HIPCHK(dalloc(&e->order, e->B));
     HIPCHK(dalloc(&e->blm, e->B));
     HIPCHK(dalloc(&e->posm, e->B));
-    HIPCHK(dalloc(&e->LT, e->B));
+    HIPCHK(dalloc(&e->r, e->B));
     HIPCHK(dalloc(&e->blockrec, e->tiles));
     HIPCHK(dalloc(&e->cont, e->cont_cap));
     HIPCHK(dalloc(&e->ctl, 1));
@@ -437,8 +447,8 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
 static void fill_scan_args(kb_engine* e, ScanArgs& s) {
     s.ctl = e->ctl; s.w = e->w; s.rep = e->rep; s.meta = e->meta;
     s.Ppad = e->Ppad; s.shard_begin = e->shard_begin; s.shard_end = e->shard_end;
-    s.K = e->K; s.W64 = e->W64; s.setbits = e->setbits; s.lists = e->lists; s.nelig = e->nelig;
-    s.LT = e->LT; s.blm = e->blm; s.posm = e->posm;
+    s.K = e->K; s.W64 = e->W64; s.stride = sr_stride(e->K); s.setbits = e->setbits; s.setrec = e->setrec;
+    s.r = e->r; s.blm = e->blm; s.posm = e->posm;
     s.allow_leader = e->allow_leader; s.rebalance = e->rebalance; s.sem_go = e->sem == KB_SEM_GO;
     s.blockrec = e->blockrec; s.cont = e->cont; s.cont_cap = e->cont_cap;
 }
@@ -446,7 +456,7 @@ static void fill_scan_args(kb_engine* e, ScanArgs& s) {
 static void fill_resolve_args(kb_engine* e, ResolveArgs& r) {
     r.ctl = e->ctl; r.w = e->w; r.rep = e->rep; r.meta = e->meta; r.nc = e->nc; r.Ppad = e->Ppad;
     r.RC = e->rc_dev; r.K = e->K; r.W64 = e->W64; r.B = (int)e->B;
-    r.setbits = e->setbits; r.lists = e->lists; r.blm = e->blm; r.posm = e->posm;
+    r.setbits = e->setbits; r.lists = e->lists; r.blm = e->blm; r.posm = e->posm; r.r = e->r;
     r.load = e->load; r.cnt = e->cnt; r.cont = e->cont; r.cont_cap = e->cont_cap;
     r.allow_leader = e->allow_leader; r.rebalance = e->rebalance; r.sem_go = e->sem == KB_SEM_GO;
     r.integral = e->integral ? 1 : 0; r.minrep = e->minrep; r.min_unbalance = e->min_unb;
@@ -487,14 +497,14 @@ static void enqueue_front(kb_engine* e) {
     PrepArgs pa;
     pa.ctl = e->ctl; pa.load = e->load; pa.cnt = e->cnt; pa.incfg = e->incfg;
     pa.B = (int)e->B; pa.NP2 = e->NP2; pa.order = e->order; pa.blm = e->blm; pa.posm = e->posm;
-    pa.LT = e->LT; pa.rmax_w = e->wmax;
+    pa.r = e->r; pa.rmax_w = e->wmax;
     mark(e, 0);
     launch_prep(pa, e->st);
     mark(e, 1);
     SetArgs sa;
     sa.ctl = e->ctl; sa.nsets = (int)e->nsets; sa.B = (int)e->B; sa.W64 = e->W64; sa.K = e->K;
-    sa.setbits = e->setbits; sa.order = e->order; sa.cnt = e->cnt; sa.incfg = e->incfg;
-    sa.lists = e->lists; sa.nelig = e->nelig;
+    sa.stride = sr_stride(e->K); sa.setbits = e->setbits; sa.order = e->order; sa.posm = e->posm;
+    sa.cnt = e->cnt; sa.r = e->r; sa.setrec = e->setrec; sa.lists = e->lists;
     launch_setlists(sa, e->st);
     if (e->tiles > 0) {
         ScanArgs s;
@@ -714,6 +724,14 @@ extern "C" int kb_engine_timings(kb_engine* e, double* ms, int64_t* launches, in
     return 6;
 }
 
+extern "C" int kb_engine_stamps(kb_engine* e, uint64_t* out, int n) {
+    if (!e || !out) return KB_ERR_INVALID;
+    DevCtl c;
+    HIPCHK(hipMemcpy(&c, e->ctl, sizeof c, hipMemcpyDeviceToHost));
+    for (int k = 0; k < 16 && k < n; k++) out[k] = c.stamps[k];
+    return 16;
+}
+
 extern "C" int kb_engine_last_error(kb_engine* e, char* buf, size_t n) {
     if (!e || !buf || n == 0) return KB_ERR_INVALID;
     snprintf(buf, n, "%s", e->last_err.c_str());
@@ -723,7 +741,7 @@ extern "C" int kb_engine_last_error(kb_engine* e, char* buf, size_t n) {
 extern "C" void kb_engine_destroy(kb_engine* e) {
     if (!e) return;
     void* ptrs[] = {e->w, e->rep, e->meta, e->nc, e->load, e->cnt, e->incfg, e->setbits, e->lists,
-                    e->nelig, e->order, e->blm, e->posm, e->LT, e->blockrec, e->cont, e->ctl,
+                    e->setrec, e->order, e->blm, e->posm, e->r, e->blockrec, e->cont, e->ctl,
                     e->log, e->lstart, e->llen, e->lcap, e->lent};
     for (void* p : ptrs) if (p) hipFree(p);
     if (e->h_ctl) hipHostFree(e->h_ctl);
@@ -763,7 +781,7 @@ extern "C" int kb_engine_step_finish(kb_engine* e, const void* gathered_dev, int
     if (e->pending) return pending_result(e, out);
     MergeArgs m;
     m.ctl = e->ctl; m.all = (const Summary*)gathered_dev; m.nranks = n_ranks; m.cont = e->cont;
-    m.cont_cap = e->cont_cap; m.LT = e->LT;
+    m.cont_cap = e->cont_cap; m.r = e->r;
     launch_merge(m, e->st);
     ResolveArgs r;
     fill_resolve_args(e, r);

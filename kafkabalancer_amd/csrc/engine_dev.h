@@ -1,5 +1,5 @@
 // engine_dev.h -- device-side data layout shared by the HIP kernels and the
-// host half of the engine (engine.hip).  See DESIGN.md "Data layout in HBM".
+// host half of the engine (engine.cpp).  See DESIGN.md "Data layout in HBM".
 #pragma once
 #include <cstdint>
 
@@ -14,9 +14,11 @@ constexpr int RESOLVE_THREADS = 1024;
 constexpr int PREP_THREADS = 1024;
 constexpr uint32_t NONE32 = 0xFFFFFFFFu;
 constexpr unsigned long long NONE64 = ~0ull;
-constexpr int SUMMARY_CONT = 1024;  // contenders carried per rank in a multi-GPU summary
+constexpr int SUMMARY_CONT = 1024;  // distinct near-tie keys carried per rank in a summary
+constexpr int DEDUP_RESOLVE = 2048; // LDS key table of k_resolve / k_summary
+constexpr int DEDUP_CENSUS = 512;   // LDS key table of one k_census workgroup
 
-// first-index predicates reduced by the scan (atomicMin over partition index)
+// first-index predicates reduced by the scan (min over partition index)
 enum {
     F_DUP = 0,         // ValidateReplicas (steps.go:27-36), only for Go-aliasing semantics
     F_REMOVE = 1,      // RemoveExtraReplicas trigger (steps.go:74)
@@ -28,15 +30,29 @@ enum {
     NF = 8
 };
 
-// meta word of a partition: nrep | want | eligible | set
+// meta word of a partition:
+//   [0..4] nrep  [5..9] want (NumReplicas, clamped to 31)  [10] eligible (want >= MinReplicas)
+//   [11] a replica is outside the allowed set (MoveDisallowedReplicas trigger)
+//   [12..16] replicas inside the allowed set  [17..31] allowed-set index
 __host__ __device__ inline uint32_t meta_nrep(uint32_t m) { return m & 31u; }
 __host__ __device__ inline uint32_t meta_want(uint32_t m) { return (m >> 5) & 31u; }
 __host__ __device__ inline uint32_t meta_elig(uint32_t m) { return (m >> 10) & 1u; }
-__host__ __device__ inline uint32_t meta_set(uint32_t m) { return m >> 11; }
-__host__ __device__ inline uint32_t make_meta(uint32_t nrep, uint32_t want, uint32_t elig, uint32_t set) {
-    return (nrep & 31u) | ((want > 31u ? 31u : want) << 5) | ((elig & 1u) << 10) | (set << 11);
+__host__ __device__ inline uint32_t meta_dis(uint32_t m) { return (m >> 11) & 1u; }
+__host__ __device__ inline uint32_t meta_nin(uint32_t m) { return (m >> 12) & 31u; }
+__host__ __device__ inline uint32_t meta_set(uint32_t m) { return m >> 17; }
+__host__ __device__ inline uint32_t make_meta(uint32_t nrep, uint32_t want, uint32_t elig, uint32_t dis,
+                                              uint32_t nin, uint32_t set) {
+    return (nrep & 31u) | ((want > 31u ? 31u : want) << 5) | ((elig & 1u) << 10) | ((dis & 1u) << 11) |
+           ((nin & 31u) << 12) | (set << 17);
 }
-constexpr uint32_t MAX_SETS = 1u << 21;
+constexpr uint32_t MAX_SETS = 1u << 15;
+
+// per-set target record, rebuilt every step by k_setlists:
+//   int32 nelig (|set ∩ bl_move|), int32 nlist, int32 ids[K] (first K eligible
+//   brokers in bl_move order), double r[K] (their relative loads L/avg - 1)
+__host__ __device__ inline int sr_ids_off() { return 8; }
+__host__ __device__ inline int sr_r_off(int K) { return (8 + 4 * K + 15) & ~15; }
+__host__ __device__ inline int sr_stride(int K) { return sr_r_off(K) + 8 * K; }
 
 struct Contender {                  // a near-tie candidate move (32 B)
     int32_t s, t;                   // dense source / target broker
@@ -72,7 +88,25 @@ struct DevCtl {
     uint32_t ncont, cont_overflow;
     int32_t list_overflow, pad0;
     unsigned long long total_cand, total_cont, total_folds;
+    // diagnostic phase stamps (builds with -DKB_STAMPS): accumulated
+    // wall_clock64 ticks (100 MHz) per phase of k_prep [0..7] and k_resolve [8..15]
+    unsigned long long stamps[16];
 };
+
+#ifdef KB_STAMPS
+#define KB_STAMP_BEGIN() unsigned long long _kb_t0 = wall_clock64()
+#define KB_STAMP(ctl, i)                                                        \
+    do {                                                                        \
+        if (threadIdx.x == 0) {                                                 \
+            unsigned long long _t = wall_clock64();                             \
+            (ctl)->stamps[i] += _t - _kb_t0;                                    \
+            _kb_t0 = _t;                                                        \
+        }                                                                       \
+    } while (0)
+#else
+#define KB_STAMP_BEGIN() (void)0
+#define KB_STAMP(ctl, i) (void)0
+#endif
 
 // summary exchanged between ranks each step (multi-GPU)
 struct Summary {

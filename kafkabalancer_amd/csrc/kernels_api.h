@@ -15,19 +15,20 @@ struct PrepArgs {
     int32_t* order;        // [B] universe sorted by (load, id)
     int32_t* blm;          // [B] bl_move order (present or in cfg.Brokers)
     int32_t* posm;         // [B] position in bl_move or -1
-    double2* LT;           // [B] {load, approx term}
+    double* r;             // [B] relative load L/avg - 1 (approximate, scoring only)
     double rmax_w;         // max weight (for the eps bound)
 };
 
 struct SetArgs {
     const DevCtl* ctl;
-    int nsets, B, W64, K;
+    int nsets, B, W64, K, stride;
     const uint64_t* setbits;
     const int32_t* order;
+    const int32_t* posm;
     const int32_t* cnt;
-    const uint8_t* incfg;
-    int32_t* lists;        // [nsets][3][K]: asc bl_move, desc present, desc universe
-    int32_t* nelig;        // [nsets] |set ∩ bl_move|
+    const double* r;
+    unsigned char* setrec;  // [nsets][stride] first K eligible targets + their r + nelig
+    int32_t* lists;         // [nsets][2][K]: desc present (Disallowed), desc universe (Add)
 };
 
 struct ScanArgs {
@@ -36,11 +37,10 @@ struct ScanArgs {
     const uint16_t* rep;      // [RC][Ppad] slot-major dense broker ids
     const uint32_t* meta;     // [Ppad]
     long long Ppad, shard_begin, shard_end;
-    int K, W64;
+    int K, W64, stride;
     const uint64_t* setbits;
-    const int32_t* lists;
-    const int32_t* nelig;
-    const double2* LT;
+    const unsigned char* setrec;
+    const double* r;
     const int32_t* blm;
     const int32_t* posm;
     int allow_leader, rebalance, sem_go;
@@ -67,6 +67,7 @@ struct ResolveArgs {
     const int32_t* lists;
     const int32_t* blm;
     const int32_t* posm;
+    const double* r;
     double* load;
     int32_t* cnt;
     const Contender* cont;
@@ -95,7 +96,7 @@ struct MergeArgs {
     int nranks;
     Contender* cont;
     uint32_t cont_cap;
-    const double2* LT;
+    const double* r;
 };
 
 void launch_prep(const PrepArgs& a, hipStream_t st);

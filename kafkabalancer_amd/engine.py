@@ -10,7 +10,7 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libkbengine.so")
+LIB_PATH = os.environ.get("KB_ENGINE_LIB") or os.path.join(_HERE, "lib", "libkbengine.so")
 
 KB_NOCHANGE, KB_CHANGE = 0, 1
 KB_SEM_APPLIED, KB_SEM_GO = 0, 1
@@ -23,7 +23,7 @@ KIND_NAMES = {0: "none", 1: "replace", 2: "remove", 3: "add", 4: "swap"}
 
 EXPORTS = ["kb_abi_version", "kb_engine_create", "kb_engine_balance", "kb_engine_plan",
            "kb_engine_replicas", "kb_engine_loads", "kb_engine_unbalance", "kb_engine_stats",
-           "kb_engine_timings",
+           "kb_engine_timings", "kb_engine_stamps",
            "kb_engine_last_error", "kb_engine_destroy", "kb_engine_summary_bytes",
            "kb_engine_step_begin", "kb_engine_step_finish", "kb_engine_set_stream"]
 
@@ -89,6 +89,8 @@ def lib():
         L.kb_engine_stats.restype = C.c_int
         L.kb_engine_timings.argtypes = [vp, PD, P64, C.c_int]
         L.kb_engine_timings.restype = C.c_int
+        L.kb_engine_stamps.argtypes = [vp, P64, C.c_int]
+        L.kb_engine_stamps.restype = C.c_int
         L.kb_engine_last_error.argtypes = [vp, C.c_char_p, C.c_size_t]
         L.kb_engine_last_error.restype = C.c_int
         L.kb_engine_destroy.argtypes = [vp]
@@ -298,6 +300,12 @@ class Engine:
         n = np.zeros(6, np.int64)
         lib().kb_engine_timings(self.h, ms.ctypes.data_as(PD), n.ctypes.data_as(P64), 6)
         return {k: (float(ms[i]), int(n[i])) for i, k in enumerate(self.KERNELS)}
+
+    def stamps(self):
+        """Diagnostic build only: accumulated phase ticks (100 MHz) of k_prep / k_resolve."""
+        out = np.zeros(16, np.int64)
+        lib().kb_engine_stamps(self.h, out.ctypes.data_as(P64), 16)
+        return out.tolist()
 
     # multi-GPU step phases
     def summary_bytes(self):
