@@ -127,9 +127,8 @@ def main():
     if args.stamps:
         st = eng.stamps()
         n = max(1, st1["steps"])
-        names = ["prep.load", "prep.sort", "prep.compact", "prep.Sfold", "prep.terms", "prep.Ufold",
-                 "prep.bounds", "prep.LT", "res.stage+pred", "res.move", "res.apply", "res.lists",
-                 "res.refold+log"]
+        names = ["res.reduce", "res.pred", "res.move", "res.apply", "prep.sort+blm", "prep.loads+eps",
+                 "prep.sets"]
         print(json.dumps({"stamps_us_per_step": {k: st[i] / 100.0 / n for i, k in enumerate(names)}}))
         return
     if not args.no_cpu_baseline:

@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define KB_ABI_VERSION 1
+#define KB_ABI_VERSION 2
 
 /* step indices == position in the reference's steps table (balancer.go:34-44) */
 enum kb_step {
@@ -39,7 +39,8 @@ enum kb_step {
 };
 
 /* kb_change.status / return value of kb_engine_balance */
-enum { KB_NOCHANGE = 0, KB_CHANGE = 1 };
+enum { KB_NOCHANGE = 0, KB_CHANGE = 1,
+       KB_RETRY = 2 /* kb_engine_step_finish only: loads were refolded exactly, redo the step */ };
 
 /* kinds of change (what replacepl/addpl did, utils.go:166-202) */
 enum { KB_KIND_NONE = 0, KB_KIND_REPLACE = 1, KB_KIND_REMOVE = 2, KB_KIND_ADD = 3, KB_KIND_SWAP = 4 };
@@ -129,6 +130,9 @@ typedef struct {
     int64_t n_sets;
     int32_t integral;               /* 1 => loads are exact under incremental updates */
     int32_t max_replicas;           /* replica slots per partition on the device */
+    int64_t refreshes;              /* exact refolds of the approximate loads (k_refresh) */
+    int64_t exact_halts;            /* steps that needed exact loads to decide */
+    int64_t scan_workgroups;        /* k_scan workgroups (one record each) */
 } kb_stats;
 
 typedef struct kb_engine kb_engine;
@@ -166,11 +170,11 @@ int kb_engine_stats(kb_engine *e, kb_stats *out);
 
 /* Per-kernel device time of the last kb_engine_plan when cfg->time_kernels was
  * set: ms[k] = summed duration of kernel k over the plan, launches[k] = count,
- * for k in {0 prep, 1 setlists, 2 scan, 3 reduce, 4 census, 5 resolve}.  Returns 6. */
+ * for k in {0 k_step (resolve + apply + prep), 1 k_scan, 2 k_refresh}.  Returns 3. */
 int kb_engine_timings(kb_engine *e, double *ms, int64_t *launches, int n);
 
-/* Diagnostic: accumulated in-kernel phase stamps (100 MHz ticks) of k_prep
- * [0..7] and k_resolve [8..12]; non-zero only in a -DKB_STAMPS build. */
+/* Diagnostic: accumulated in-kernel phase stamps (100 MHz ticks) of k_step
+ * phases [0..6]; non-zero only in a -DKB_STAMPS build. */
 int kb_engine_stamps(kb_engine *e, uint64_t *out, int n);
 
 /* Reference-format message of the last error ("<Step>: partition Partition(t,p,[..]) ..."). */

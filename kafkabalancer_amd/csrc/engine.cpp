@@ -2,12 +2,13 @@
 // in include/kbengine.h.  Marshals the reference's PartitionList
 // (kafkabalancer.go:40-58) into the device SoA layout, performs the one-time
 // ValidateWeights / ValidateReplicas / FillDefaults (steps.go:7-66), and drives
-// the per-step kernels of kernels.hip.
+// the per-step kernels of kernels.hip (k_scan -> k_step per Balance() call).
 //
 // Build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off (host folds must
 // round exactly like Go on amd64: no FMA contraction).
 #include <hip/hip_runtime.h>
 #include <algorithm>
+#include <cfloat>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -37,17 +38,21 @@ static const char* kStepNames[9] = {
     "AddMissingReplicas", "MoveDisallowedReplicas", "ReassignLeaders",
     "MoveLeaders", "MoveNonLeaders"};
 
+enum { TK_STEP = 0, TK_SCAN = 1, TK_REFRESH = 2, TK_N = 3 };
+
 struct kb_engine {
     int dev = 0;
     hipStream_t st = nullptr;
     bool own_st = false;
-    int64_t P = 0, Ppad = 0, B = 0, nsets = 0, tiles = 0;
-    int rcap = 0, rc_dev = 1, K = 3, W64 = 1, NP2 = 64;
+    int64_t P = 0, Ppad = 0, B = 0, nsets = 0, ntiles = 0, nscan = 0;
+    int rcap = 0, rc_dev = 1, K = 3, KR = 6, units = 1, W64 = 1, NP2 = 64;
     int sem = KB_SEM_APPLIED, allow_leader = 0, rebalance = 0;
     int64_t minrep = 2;
     double min_unb = 0.01;
     int64_t shard_begin = 0, shard_end = 0;
     bool integral = false;
+    bool lds_sets = true;
+    size_t scan_lds = 0;
     double wmax = 0;
     std::vector<int64_t> ids;
     std::vector<std::string> topics;
@@ -61,19 +66,24 @@ struct kb_engine {
     uint32_t* meta = nullptr;
     int32_t* nc = nullptr;
     double* load = nullptr;
+    double* lerr = nullptr;
+    uint8_t* dirty = nullptr;
     int32_t* cnt = nullptr;
     uint8_t* incfg = nullptr;
     uint64_t* setbits = nullptr;
     int32_t* lists = nullptr;
-    unsigned char* setrec = nullptr;
+    uint4* setrec = nullptr;
     int32_t* order = nullptr;
+    int32_t* posu = nullptr;
     int32_t* blm = nullptr;
     int32_t* posm = nullptr;
     double* r = nullptr;
-    BlockRec* blockrec = nullptr;
+    int32_t* bset_off = nullptr;
+    int32_t* bset_ids = nullptr;
+    unsigned char* recs = nullptr;
     Contender* cont = nullptr;
     uint32_t cont_cap = 1u << 20;
-    uint32_t *lstart = nullptr, *llen = nullptr, *lcap = nullptr, *lent = nullptr;
+    Lists L{nullptr, nullptr, nullptr, nullptr};
     DevCtl* ctl = nullptr;
     ChangeDev* log = nullptr;
     int logcap = 0;
@@ -82,12 +92,14 @@ struct kb_engine {
     double last_ms = 0;
     int64_t scan_bytes = 0;
     int exact_unb = 0;
-    // per-kernel timing (cfg->time_kernels): one event ring per batch of steps
+    // per-kernel timing (cfg->time_kernels): one event per launch boundary
     int time_kernels = 0;
-    std::vector<hipEvent_t> tev;      // 6 events per step
+    std::vector<hipEvent_t> tev;
+    std::vector<int> tkind;           // kernel kind between tev[i] and tev[i+1]
     int tev_used = 0;
-    double kms[6] = {0, 0, 0, 0, 0, 0};
-    int64_t klaunch[6] = {0, 0, 0, 0, 0, 0};
+    double kms[TK_N] = {0, 0, 0};
+    int64_t klaunch[TK_N] = {0, 0, 0};
+    int64_t refreshes = 0;
     std::string last_err;
 };
 
@@ -267,6 +279,8 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
     e->rcap = rcap;
     for (int v : kRcChoices) if (v >= rcap) { e->rc_dev = v; break; }
     e->K = e->rc_dev + 2;
+    e->units = sr_units(e->rc_dev);
+    e->KR = sr_kr(e->rc_dev);
     e->W64 = (int)((e->B + 63) / 64);
     if (e->W64 < 1) e->W64 = 1;
     e->NP2 = 64;
@@ -316,18 +330,24 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
         }
         e->integral = integ && tot < 4503599627370496.0L;  // 2^52
     }
+    // error bounds of the exact folds against the real sums (non-integral mode)
+    std::vector<double> le(e->B, 0.0);
+    if (!e->integral)
+        for (int64_t b = 0; b < e->B; b++)
+            le[b] = 1.01 * (double)std::max(cn[b], 1) * (DBL_EPSILON / 2) * ld[b];
 
     // shard
     e->shard_begin = cfg->shard_begin;
     e->shard_end = (cfg->shard_begin == 0 && cfg->shard_end == 0) ? n : cfg->shard_end;
     if (e->shard_begin < 0 || e->shard_end > n || e->shard_begin > e->shard_end ||
-        ((e->shard_begin % TILE) != 0 && e->shard_begin != e->shard_end)) {
+        ((e->shard_begin % SHARD_ALIGN) != 0 && e->shard_begin != e->shard_end)) {
         e->last_err = "shard_begin must be a multiple of 1024 and 0 <= begin <= end <= n";
         delete e;
         return KB_ERR_INVALID;
     }
-    e->tiles = (e->shard_end - e->shard_begin + TILE - 1) / TILE;
-    e->Ppad = ((n + TILE - 1) / TILE) * TILE + TILE;
+    e->ntiles = (e->shard_end - e->shard_begin + TILE - 1) / TILE;
+    // padding: the last tile of the shard may read up to TILE past shard_end
+    e->Ppad = ((n + TILE - 1) / TILE) * TILE + 2 * TILE;
 
     // host SoA images
     std::vector<double> hw(e->Ppad, 0.0);
@@ -336,8 +356,6 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
     std::vector<int32_t> hnc(e->Ppad, 0);
     for (int64_t i = 0; i < n; i++) {
         hw[i] = wt[i];
-        uint32_t elig = want[i] >= e->minrep ? 1u : 0u;
-        uint32_t wnt = want[i] < 0 ? 0u : (uint32_t)std::min<int64_t>(want[i], 31);
         for (int k = 0; k < len[i]; k++) hr[(size_t)k * e->Ppad + i] = dense[c->replica_off[i] - c->replica_off[0] + k];
         hnc[i] = (int32_t)ncon[i];
     }
@@ -361,6 +379,20 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
     std::vector<uint8_t> hin(e->B, 0);
     if (!cfg->brokers_nil)
         for (int64_t k = 0; k < cfg->n_brokers; k++) hin[idmap[cfg->brokers[k]]] = 1;
+    // broker -> sets containing it (incremental set-record upkeep)
+    std::vector<int32_t> hbo(e->B + 1, 0), hbi;
+    {
+        std::vector<std::vector<int32_t>> bs(e->B);
+        for (int64_t s = 0; s < e->nsets; s++) {
+            std::vector<int> u = sets[s];
+            std::sort(u.begin(), u.end());
+            u.erase(std::unique(u.begin(), u.end()), u.end());
+            for (int b : u) bs[b].push_back((int32_t)s);
+        }
+        for (int64_t b = 0; b < e->B; b++) hbo[b + 1] = hbo[b] + (int32_t)bs[b].size();
+        hbi.reserve(hbo[e->B]);
+        for (int64_t b = 0; b < e->B; b++) hbi.insert(hbi.end(), bs[b].begin(), bs[b].end());
+    }
 
     // per-broker partition lists (non-integral mode), sorted by partition index
     std::vector<uint32_t> hls, hll, hlc, hle;
@@ -387,6 +419,18 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
 
     // device
     if (hipSetDevice(e->dev) != hipSuccess) { e->last_err = "hipSetDevice failed (no GPU?)"; *out = e; return KB_ERR_HIP; }
+    int ncu = 256;
+    hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, e->dev);
+    if (ncu <= 0) ncu = 256;
+    const size_t rbytes = ((size_t)e->B * 8 + 15) & ~(size_t)15;
+    const size_t setbytes = (size_t)e->nsets * e->units * 16;
+    const size_t dedup = (size_t)DEDUP_SCAN * (4 + 8 + 8);
+    e->lds_sets = setbytes <= (size_t)LDS_SETS_MAX;
+    e->scan_lds = rbytes + (e->lds_sets ? setbytes : 0) + dedup;
+    // one wave of resident workgroups; each loops over its tiles
+    int per_cu = scan_blocks_per_cu(e->rc_dev, e->lds_sets, e->scan_lds);
+    if (per_cu < 1) per_cu = 1;
+    e->nscan = std::min<int64_t>(e->ntiles, (int64_t)per_cu * ncu);
     HIPCHK(hipStreamCreateWithFlags(&e->st, hipStreamNonBlocking));
     e->own_st = true;
     HIPCHK(dalloc(&e->w, e->Ppad));
@@ -394,16 +438,21 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
     HIPCHK(dalloc(&e->rep, (size_t)e->rc_dev * e->Ppad));
     HIPCHK(dalloc(&e->nc, e->Ppad));
     HIPCHK(dalloc(&e->load, e->B));
+    HIPCHK(dalloc(&e->lerr, e->B));
+    HIPCHK(dalloc(&e->dirty, e->B));
     HIPCHK(dalloc(&e->cnt, e->B));
     HIPCHK(dalloc(&e->incfg, e->B));
     HIPCHK(dalloc(&e->setbits, (size_t)e->nsets * e->W64));
     HIPCHK(dalloc(&e->lists, (size_t)e->nsets * 2 * e->K));
-    HIPCHK(dalloc(&e->setrec, (size_t)e->nsets * sr_stride(e->K)));
+    HIPCHK(dalloc(&e->setrec, (size_t)e->nsets * e->units));
     HIPCHK(dalloc(&e->order, e->B));
+    HIPCHK(dalloc(&e->posu, e->B));
     HIPCHK(dalloc(&e->blm, e->B));
     HIPCHK(dalloc(&e->posm, e->B));
     HIPCHK(dalloc(&e->r, e->B));
-    HIPCHK(dalloc(&e->blockrec, e->tiles));
+    HIPCHK(dalloc(&e->bset_off, e->B + 1));
+    HIPCHK(dalloc(&e->bset_ids, hbi.size()));
+    HIPCHK(dalloc(&e->recs, (size_t)std::max<int64_t>(e->nscan, 1) * WGREC_BYTES));
     HIPCHK(dalloc(&e->cont, e->cont_cap));
     HIPCHK(dalloc(&e->ctl, 1));
     e->logcap = 1024;
@@ -414,26 +463,32 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
     HIPCHK(hipMemcpy(e->rep, hr.data(), hr.size() * 2, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(e->nc, hnc.data(), hnc.size() * 4, hipMemcpyHostToDevice));
     if (e->B) {
+        std::vector<uint8_t> zero(e->B, 0);
         HIPCHK(hipMemcpy(e->load, ld.data(), ld.size() * 8, hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(e->lerr, le.data(), le.size() * 8, hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(e->dirty, zero.data(), zero.size(), hipMemcpyHostToDevice));
         HIPCHK(hipMemcpy(e->cnt, cn.data(), cn.size() * 4, hipMemcpyHostToDevice));
         HIPCHK(hipMemcpy(e->incfg, hin.data(), hin.size(), hipMemcpyHostToDevice));
     }
+    HIPCHK(hipMemcpy(e->bset_off, hbo.data(), hbo.size() * 4, hipMemcpyHostToDevice));
+    if (!hbi.empty()) HIPCHK(hipMemcpy(e->bset_ids, hbi.data(), hbi.size() * 4, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(e->setbits, hsb.data(), hsb.size() * 8, hipMemcpyHostToDevice));
     if (!e->integral) {
-        HIPCHK(dalloc(&e->lstart, e->B));
-        HIPCHK(dalloc(&e->llen, e->B));
-        HIPCHK(dalloc(&e->lcap, e->B));
-        HIPCHK(dalloc(&e->lent, hle.size()));
+        HIPCHK(dalloc(&e->L.lstart, e->B));
+        HIPCHK(dalloc(&e->L.llen, e->B));
+        HIPCHK(dalloc(&e->L.lcap, e->B));
+        HIPCHK(dalloc(&e->L.lent, hle.size()));
         if (e->B) {
-            HIPCHK(hipMemcpy(e->lstart, hls.data(), hls.size() * 4, hipMemcpyHostToDevice));
-            HIPCHK(hipMemcpy(e->llen, hll.data(), hll.size() * 4, hipMemcpyHostToDevice));
-            HIPCHK(hipMemcpy(e->lcap, hlc.data(), hlc.size() * 4, hipMemcpyHostToDevice));
+            HIPCHK(hipMemcpy(e->L.lstart, hls.data(), hls.size() * 4, hipMemcpyHostToDevice));
+            HIPCHK(hipMemcpy(e->L.llen, hll.data(), hll.size() * 4, hipMemcpyHostToDevice));
+            HIPCHK(hipMemcpy(e->L.lcap, hlc.data(), hlc.size() * 4, hipMemcpyHostToDevice));
         }
-        HIPCHK(hipMemcpy(e->lent, hle.data(), hle.size() * 4, hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(e->L.lent, hle.data(), hle.size() * 4, hipMemcpyHostToDevice));
     }
     DevCtl z;
     memset(&z, 0, sizeof z);
     z.logcap = e->logcap;
+    z.full_prep = 1;
     HIPCHK(hipMemcpy(e->ctl, &z, sizeof z, hipMemcpyHostToDevice));
     HIPCHK(hipEventCreate(&e->ev0));
     HIPCHK(hipEventCreate(&e->ev1));
@@ -447,99 +502,126 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
 static void fill_scan_args(kb_engine* e, ScanArgs& s) {
     s.ctl = e->ctl; s.w = e->w; s.rep = e->rep; s.meta = e->meta;
     s.Ppad = e->Ppad; s.shard_begin = e->shard_begin; s.shard_end = e->shard_end;
-    s.K = e->K; s.W64 = e->W64; s.stride = sr_stride(e->K); s.setbits = e->setbits; s.setrec = e->setrec;
-    s.r = e->r; s.blm = e->blm; s.posm = e->posm;
+    s.ntiles = (int)e->ntiles; s.nscan = (int)e->nscan;
+    s.B = (int)e->B; s.nsets = (int)e->nsets; s.W64 = e->W64; s.units = e->units;
+    s.setbits = e->setbits; s.setrec = e->setrec; s.r = e->r; s.blm = e->blm; s.posm = e->posm;
     s.allow_leader = e->allow_leader; s.rebalance = e->rebalance; s.sem_go = e->sem == KB_SEM_GO;
-    s.blockrec = e->blockrec; s.cont = e->cont; s.cont_cap = e->cont_cap;
+    s.recs = e->recs; s.cont = e->cont; s.cont_cap = e->cont_cap;
+    s.listwg = e->integral ? 0 : 1;
+    s.L = e->L;
 }
 
-static void fill_resolve_args(kb_engine* e, ResolveArgs& r) {
-    r.ctl = e->ctl; r.w = e->w; r.rep = e->rep; r.meta = e->meta; r.nc = e->nc; r.Ppad = e->Ppad;
-    r.RC = e->rc_dev; r.K = e->K; r.W64 = e->W64; r.B = (int)e->B;
-    r.setbits = e->setbits; r.lists = e->lists; r.blm = e->blm; r.posm = e->posm; r.r = e->r;
-    r.load = e->load; r.cnt = e->cnt; r.cont = e->cont; r.cont_cap = e->cont_cap;
-    r.allow_leader = e->allow_leader; r.rebalance = e->rebalance; r.sem_go = e->sem == KB_SEM_GO;
-    r.integral = e->integral ? 1 : 0; r.minrep = e->minrep; r.min_unbalance = e->min_unb;
-    r.exact_unb = e->exact_unb;
-    r.lstart = e->lstart; r.llen = e->llen; r.lcap = e->lcap; r.lent = e->lent; r.log = e->log;
+static void fill_step_args(kb_engine* e, StepArgs& a, const unsigned char* recs, int nrec, int stride,
+                           int keys, int use_spill) {
+    a.ctl = e->ctl; a.w = e->w; a.rep = e->rep; a.meta = e->meta; a.nc = e->nc; a.Ppad = e->Ppad;
+    a.RC = e->rc_dev; a.KR = e->KR; a.K = e->K; a.units = e->units; a.W64 = e->W64; a.B = (int)e->B;
+    a.nsets = (int)e->nsets; a.NP2 = e->NP2;
+    a.setbits = e->setbits; a.setrec = e->setrec; a.lists = e->lists;
+    a.order = e->order; a.posu = e->posu; a.blm = e->blm; a.posm = e->posm; a.r = e->r;
+    a.load = e->load; a.lerr = e->lerr; a.dirty = e->dirty; a.cnt = e->cnt; a.incfg = e->incfg;
+    a.bset_off = e->bset_off; a.bset_ids = e->bset_ids;
+    a.recs = recs; a.nrec = nrec; a.rec_stride = stride; a.rec_keys = keys;
+    a.cont = e->cont; a.cont_cap = e->cont_cap; a.use_spill = use_spill;
+    a.allow_leader = e->allow_leader; a.rebalance = e->rebalance; a.sem_go = e->sem == KB_SEM_GO;
+    a.integral = e->integral ? 1 : 0; a.exact_unb = e->exact_unb;
+    a.minrep = e->minrep; a.min_unbalance = e->min_unb; a.wmax = e->wmax;
+    a.log = e->log; a.L = e->L;
 }
 
 static const int kStepBatch = 64;
 
-static void mark(kb_engine* e, int k) {
+static void mark(kb_engine* e, int kind_next) {
     if (!e->time_kernels) return;
     if (e->tev.empty()) {
-        e->tev.resize((size_t)kStepBatch * 7 + 14);
+        e->tev.resize((size_t)kStepBatch * 2 + 8);
+        e->tkind.resize(e->tev.size());
         for (auto& v : e->tev) hipEventCreate(&v);
     }
-    if (e->tev_used < (int)e->tev.size()) hipEventRecord(e->tev[e->tev_used++], e->st);
-    (void)k;
+    if (e->tev_used < (int)e->tev.size()) {
+        e->tkind[e->tev_used] = kind_next;
+        hipEventRecord(e->tev[e->tev_used++], e->st);
+    }
 }
 
 // accumulate the durations of the marks recorded since the last harvest
 static void harvest(kb_engine* e) {
     if (!e->time_kernels || e->tev_used == 0) return;
     hipEventSynchronize(e->tev[e->tev_used - 1]);
-    for (int s = 0; s + 6 < e->tev_used; s += 7) {
-        for (int k = 0; k < 6; k++) {
-            float ms = 0;
-            if (hipEventElapsedTime(&ms, e->tev[s + k], e->tev[s + k + 1]) == hipSuccess) {
-                e->kms[k] += ms;
-                e->klaunch[k]++;
-            }
+    for (int i = 0; i + 1 < e->tev_used; i++) {
+        const int k = e->tkind[i];
+        if (k < 0 || k >= TK_N) continue;
+        float ms = 0;
+        if (hipEventElapsedTime(&ms, e->tev[i], e->tev[i + 1]) == hipSuccess) {
+            e->kms[k] += ms;
+            e->klaunch[k]++;
         }
     }
     e->tev_used = 0;
 }
 
-// prep + setlists + scan (the local half of a step)
-static void enqueue_front(kb_engine* e) {
-    PrepArgs pa;
-    pa.ctl = e->ctl; pa.load = e->load; pa.cnt = e->cnt; pa.incfg = e->incfg;
-    pa.B = (int)e->B; pa.NP2 = e->NP2; pa.order = e->order; pa.blm = e->blm; pa.posm = e->posm;
-    pa.r = e->r; pa.rmax_w = e->wmax;
-    mark(e, 0);
-    launch_prep(pa, e->st);
-    mark(e, 1);
-    SetArgs sa;
-    sa.ctl = e->ctl; sa.nsets = (int)e->nsets; sa.B = (int)e->B; sa.W64 = e->W64; sa.K = e->K;
-    sa.stride = sr_stride(e->K); sa.setbits = e->setbits; sa.order = e->order; sa.posm = e->posm;
-    sa.cnt = e->cnt; sa.r = e->r; sa.setrec = e->setrec; sa.lists = e->lists;
-    launch_setlists(sa, e->st);
-    if (e->tiles > 0) {
-        ScanArgs s;
-        fill_scan_args(e, s);
-        mark(e, 2);
-        launch_scan(s, e->rc_dev, (int)e->tiles, e->st);
-        mark(e, 3);
-        ReduceArgs ra;
-        ra.ctl = e->ctl; ra.blockrec = e->blockrec; ra.tiles = (int)e->tiles;
-        launch_reduce(ra, e->st);
-        mark(e, 4);
-        launch_census(s, e->rc_dev, (int)e->tiles, e->st);
-    } else {
-        mark(e, 2);
-        mark(e, 3);
-        mark(e, 4);
-    }
+static void enqueue_scan(kb_engine* e) {
+    if (e->nscan == 0 && e->integral) return;
+    ScanArgs s;
+    fill_scan_args(e, s);
+    if (e->nscan == 0) s.listwg = 1;
+    launch_scan(s, e->rc_dev, e->lds_sets, e->scan_lds, e->st);
 }
 
 static void enqueue_step(kb_engine* e) {
-    enqueue_front(e);
-    ResolveArgs r;
-    fill_resolve_args(e, r);
-    mark(e, 5);
-    launch_resolve(r, e->st);
-    mark(e, 6);
+    StepArgs a;
+    fill_step_args(e, a, e->recs, (int)e->nscan, WGREC_BYTES, TILE_KEYS, 1);
+    launch_step(a, e->st);
 }
 
-static int reset_ctl(kb_engine* e, int logcap) {
-    // halted = 0, logpos = 0, logcap
-    int32_t hdr[4];
-    HIPCHK(hipMemcpyAsync(hdr, e->ctl, sizeof hdr, hipMemcpyDeviceToHost, e->st));
+// one Balance(): scan (if prepped) then resolve + apply + prep of the next step
+static void enqueue_pair(kb_engine* e) {
+    mark(e, TK_SCAN);
+    enqueue_scan(e);
+    mark(e, TK_STEP);
+    enqueue_step(e);
+}
+
+// exact refolds of the approximate loads (k_refresh), then a full prep
+static int refresh(kb_engine* e) {
+    if (e->integral) return KB_OK;
+    mark(e, -1);
+    launch_listop(e->ctl, e->L, e->st);
+    RefreshArgs ra;
+    ra.ctl = e->ctl; ra.w = e->w; ra.rep = e->rep; ra.meta = e->meta; ra.nc = e->nc;
+    ra.load = e->load; ra.lerr = e->lerr; ra.dirty = e->dirty; ra.cnt = e->cnt; ra.B = (int)e->B;
+    ra.L = e->L;
+    mark(e, TK_REFRESH);
+    launch_refresh(ra, e->st);
+    mark(e, -1);
+    HIPCHK(hipGetLastError());
+    // halted (if NEED_EXACT) -> run, prepped = 0, full_prep = 1, ndirty = 0
+    HIPCHK(hipMemcpyAsync(e->h_ctl, e->ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, e->st));
     HIPCHK(hipStreamSynchronize(e->st));
-    hdr[0] = 0; hdr[2] = 0; hdr[3] = logcap;
-    HIPCHK(hipMemcpyAsync(e->ctl, hdr, sizeof hdr, hipMemcpyHostToDevice, e->st));
+    DevCtl c = *e->h_ctl;
+    if (c.halted == H_NEED_EXACT) c.halted = H_RUN;
+    c.prepped = 0; c.full_prep = 1; c.ndirty = 0; c.want_refresh = 0;
+    HIPCHK(hipMemcpyAsync(e->ctl, &c, sizeof c, hipMemcpyHostToDevice, e->st));
+    HIPCHK(hipStreamSynchronize(e->st));
+    e->refreshes++;
+    return KB_OK;
+}
+
+static int reset_ctl(kb_engine* e, int64_t budget_steps) {
+    HIPCHK(hipMemcpyAsync(e->h_ctl, e->ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, e->st));
+    HIPCHK(hipStreamSynchronize(e->st));
+    DevCtl c = *e->h_ctl;
+    if (c.halted == H_NEED_EXACT) {
+        if (refresh(e) != KB_OK) return KB_ERR_HIP;
+        c = *e->h_ctl;
+        c.halted = H_RUN; c.prepped = 0; c.full_prep = 1; c.ndirty = 0; c.want_refresh = 0;
+    }
+    c.halted = H_RUN;
+    c.logpos = 0;
+    c.logcap = e->logcap;
+    const long long bud = (long long)c.steps + budget_steps;
+    c.budget = bud > 0x7FFFFFFF ? 0x7FFFFFFF : (int32_t)bud;
+    HIPCHK(hipMemcpyAsync(e->ctl, &c, sizeof c, hipMemcpyHostToDevice, e->st));
+    *e->h_ctl = c;
     return KB_OK;
 }
 
@@ -595,19 +677,55 @@ static int pending_result(kb_engine* e, kb_change* o) {
     return e->pending;
 }
 
-extern "C" int kb_engine_balance(kb_engine* e, kb_change* out) {
-    if (!e || !out) return KB_ERR_INVALID;
-    if (e->pending) return pending_result(e, out);
-    if (reset_ctl(e, e->logcap) != KB_OK) return KB_ERR_HIP;
+// run up to max_steps Balance() calls device-resident; returns the number of
+// log entries written (changes + the terminating no-change / error)
+static int run_steps(kb_engine* e, int64_t max_steps) {
+    if (max_steps > e->logcap) {
+        hipFree(e->log);
+        e->logcap = (int)std::min<int64_t>(max_steps, 1 << 30);
+        HIPCHK(dalloc(&e->log, e->logcap));
+    }
+    if (reset_ctl(e, max_steps) != KB_OK) return KB_ERR_HIP;
+    const int steps0 = e->h_ctl->steps;
+    bool prepped = e->h_ctl->prepped != 0;
     HIPCHK(hipEventRecord(e->ev0, e->st));
-    enqueue_step(e);
+    for (;;) {
+        const int64_t done = e->h_ctl->steps - steps0;
+        if (done >= max_steps) break;
+        const int64_t pairs = std::min<int64_t>(kStepBatch, max_steps - done + (prepped ? 0 : 1));
+        for (int64_t s = 0; s < pairs; s++) enqueue_pair(e);
+        mark(e, -1);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpyAsync(e->h_ctl, e->ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, e->st));
+        HIPCHK(hipStreamSynchronize(e->st));
+        harvest(e);
+        const DevCtl& c = *e->h_ctl;
+        if (c.halted == H_DONE) break;
+        if (c.halted == H_NEED_EXACT || (c.want_refresh && c.steps - steps0 < max_steps)) {
+            const int logpos = c.logpos;
+            if (refresh(e) != KB_OK) return KB_ERR_HIP;
+            // refresh() cleared halted; keep the step log position
+            (void)logpos;
+            prepped = false;
+            continue;
+        }
+        prepped = c.prepped != 0;
+    }
     HIPCHK(hipEventRecord(e->ev1, e->st));
-    HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(e->st));
-    harvest(e);
     float ms = 0;
     hipEventElapsedTime(&ms, e->ev0, e->ev1);
     e->last_ms = ms;
+    HIPCHK(hipMemcpy(e->h_ctl, e->ctl, sizeof(DevCtl), hipMemcpyDeviceToHost));
+    return (int)std::min<int64_t>(e->h_ctl->logpos, e->logcap);
+}
+
+extern "C" int kb_engine_balance(kb_engine* e, kb_change* out) {
+    if (!e || !out) return KB_ERR_INVALID;
+    if (e->pending) return pending_result(e, out);
+    const int nlog = run_steps(e, 1);
+    if (nlog < 0) return nlog;
+    if (nlog == 0) { memset(out, 0, sizeof *out); out->status = KB_NOCHANGE; return KB_NOCHANGE; }
     ChangeDev d;
     HIPCHK(hipMemcpy(&d, e->log, sizeof d, hipMemcpyDeviceToHost));
     return convert(e, d, out);
@@ -618,34 +736,10 @@ extern "C" int kb_engine_plan(kb_engine* e, int64_t max_steps, kb_change* out, i
     *n_out = 0;
     if (max_steps == 0) return KB_NOCHANGE;
     if (e->pending) { if (out) pending_result(e, out); *n_out = 1; return e->pending; }
-    if (max_steps > e->logcap) {
-        hipFree(e->log);
-        e->logcap = (int)std::min<int64_t>(max_steps, 1 << 30);
-        HIPCHK(dalloc(&e->log, e->logcap));
-    }
-    if (reset_ctl(e, e->logcap) != KB_OK) return KB_ERR_HIP;
-    for (int k = 0; k < 6; k++) { e->kms[k] = 0; e->klaunch[k] = 0; }
+    for (int k = 0; k < TK_N; k++) { e->kms[k] = 0; e->klaunch[k] = 0; }
     e->tev_used = 0;
-    HIPCHK(hipEventRecord(e->ev0, e->st));
-    int64_t done = 0;
-    const int64_t batch = kStepBatch;
-    while (done < max_steps) {
-        int64_t nb = std::min<int64_t>(batch, max_steps - done);
-        for (int64_t s = 0; s < nb; s++) enqueue_step(e);
-        done += nb;
-        HIPCHK(hipGetLastError());
-        HIPCHK(hipMemcpyAsync(e->h_ctl, e->ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, e->st));
-        HIPCHK(hipStreamSynchronize(e->st));
-        harvest(e);
-        if (e->h_ctl->halted) break;
-    }
-    HIPCHK(hipEventRecord(e->ev1, e->st));
-    HIPCHK(hipStreamSynchronize(e->st));
-    float ms = 0;
-    hipEventElapsedTime(&ms, e->ev0, e->ev1);
-    e->last_ms = ms;
-    HIPCHK(hipMemcpy(e->h_ctl, e->ctl, sizeof(DevCtl), hipMemcpyDeviceToHost));
-    int64_t nlog = std::min<int64_t>(e->h_ctl->logpos, e->logcap);
+    const int nlog = run_steps(e, max_steps);
+    if (nlog < 0) return nlog;
     std::vector<ChangeDev> logv((size_t)nlog);
     if (nlog) HIPCHK(hipMemcpy(logv.data(), e->log, (size_t)nlog * sizeof(ChangeDev), hipMemcpyDeviceToHost));
     int rc = KB_NOCHANGE;
@@ -668,8 +762,18 @@ extern "C" int64_t kb_engine_replicas(kb_engine* e, int64_t i, int64_t* buf, int
     return (int64_t)r.size();
 }
 
+// make every load the exact fold again (before reading them out)
+static int make_exact(kb_engine* e) {
+    if (e->integral) return KB_OK;
+    HIPCHK(hipMemcpyAsync(e->h_ctl, e->ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, e->st));
+    HIPCHK(hipStreamSynchronize(e->st));
+    if (e->h_ctl->ndirty == 0 && !e->h_ctl->pending_list) return KB_OK;
+    return refresh(e);
+}
+
 extern "C" int64_t kb_engine_loads(kb_engine* e, int64_t* ids, double* loads, int64_t cap) {
     if (!e) return KB_ERR_INVALID;
+    if (make_exact(e) != KB_OK) return KB_ERR_HIP;
     std::vector<double> ld(e->B);
     if (e->B && hipMemcpy(ld.data(), e->load, e->B * 8, hipMemcpyDeviceToHost) != hipSuccess) return KB_ERR_HIP;
     for (int64_t k = 0; k < e->B && k < cap; k++) { if (ids) ids[k] = e->ids[k]; if (loads) loads[k] = ld[k]; }
@@ -678,6 +782,7 @@ extern "C" int64_t kb_engine_loads(kb_engine* e, int64_t* ids, double* loads, in
 
 extern "C" double kb_engine_unbalance(kb_engine* e) {
     if (!e || e->B == 0) return 0.0;
+    if (make_exact(e) != KB_OK) return NAN;
     std::vector<double> ld(e->B);
     std::vector<int32_t> cn(e->B);
     std::vector<uint8_t> in(e->B);
@@ -712,16 +817,19 @@ extern "C" int kb_engine_stats(kb_engine* e, kb_stats* o) {
     o->n_sets = e->nsets;
     o->integral = e->integral ? 1 : 0;
     o->max_replicas = e->rc_dev;
+    o->refreshes = e->refreshes;
+    o->exact_halts = (int64_t)c.total_exact_halts;
+    o->scan_workgroups = e->nscan;
     return KB_OK;
 }
 
 extern "C" int kb_engine_timings(kb_engine* e, double* ms, int64_t* launches, int n) {
     if (!e) return KB_ERR_INVALID;
-    for (int k = 0; k < 6 && k < n; k++) {
+    for (int k = 0; k < TK_N && k < n; k++) {
         if (ms) ms[k] = e->kms[k];
         if (launches) launches[k] = e->klaunch[k];
     }
-    return 6;
+    return TK_N;
 }
 
 extern "C" int kb_engine_stamps(kb_engine* e, uint64_t* out, int n) {
@@ -740,9 +848,10 @@ extern "C" int kb_engine_last_error(kb_engine* e, char* buf, size_t n) {
 
 extern "C" void kb_engine_destroy(kb_engine* e) {
     if (!e) return;
-    void* ptrs[] = {e->w, e->rep, e->meta, e->nc, e->load, e->cnt, e->incfg, e->setbits, e->lists,
-                    e->setrec, e->order, e->blm, e->posm, e->r, e->blockrec, e->cont, e->ctl,
-                    e->log, e->lstart, e->llen, e->lcap, e->lent};
+    void* ptrs[] = {e->w, e->rep, e->meta, e->nc, e->load, e->lerr, e->dirty, e->cnt, e->incfg,
+                    e->setbits, e->lists, e->setrec, e->order, e->posu, e->blm, e->posm, e->r,
+                    e->bset_off, e->bset_ids, e->recs, e->cont, e->ctl, e->log,
+                    e->L.lstart, e->L.llen, e->L.lcap, e->L.lent};
     for (void* p : ptrs) if (p) hipFree(p);
     if (e->h_ctl) hipHostFree(e->h_ctl);
     if (e->ev0) hipEventDestroy(e->ev0);
@@ -754,7 +863,7 @@ extern "C" void kb_engine_destroy(kb_engine* e) {
 
 // ----------------------------------------------------- multi-GPU phases
 
-extern "C" int64_t kb_engine_summary_bytes(kb_engine* e) { (void)e; return (int64_t)sizeof(Summary); }
+extern "C" int64_t kb_engine_summary_bytes(kb_engine* e) { (void)e; return (int64_t)SUMMARY_BYTES; }
 
 extern "C" int kb_engine_set_stream(kb_engine* e, void* s) {
     if (!e) return KB_ERR_INVALID;
@@ -767,10 +876,12 @@ extern "C" int kb_engine_set_stream(kb_engine* e, void* s) {
 extern "C" int kb_engine_step_begin(kb_engine* e, void* summary_dev) {
     if (!e || !summary_dev) return KB_ERR_INVALID;
     if (e->pending) return e->pending;
-    if (reset_ctl(e, e->logcap) != KB_OK) return KB_ERR_HIP;
-    enqueue_front(e);
+    if (reset_ctl(e, 1) != KB_OK) return KB_ERR_HIP;
+    if (!e->h_ctl->prepped) enqueue_step(e);       // prep only (nothing to resolve yet)
+    enqueue_scan(e);
     SumArgs s;
-    s.ctl = e->ctl; s.cont = e->cont; s.cont_cap = e->cont_cap; s.out = (Summary*)summary_dev;
+    s.ctl = e->ctl; s.recs = e->recs; s.nrec = (int)e->nscan; s.cont = e->cont; s.cont_cap = e->cont_cap;
+    s.r = e->r; s.out = (unsigned char*)summary_dev;
     launch_summary(s, e->st);
     HIPCHK(hipGetLastError());
     return KB_OK;
@@ -779,16 +890,27 @@ extern "C" int kb_engine_step_begin(kb_engine* e, void* summary_dev) {
 extern "C" int kb_engine_step_finish(kb_engine* e, const void* gathered_dev, int32_t n_ranks, kb_change* out) {
     if (!e || !gathered_dev || n_ranks < 1 || !out) return KB_ERR_INVALID;
     if (e->pending) return pending_result(e, out);
-    MergeArgs m;
-    m.ctl = e->ctl; m.all = (const Summary*)gathered_dev; m.nranks = n_ranks; m.cont = e->cont;
-    m.cont_cap = e->cont_cap; m.r = e->r;
-    launch_merge(m, e->st);
-    ResolveArgs r;
-    fill_resolve_args(e, r);
-    launch_resolve(r, e->st);
+    StepArgs a;
+    fill_step_args(e, a, (const unsigned char*)gathered_dev, n_ranks, SUMMARY_BYTES, SUMMARY_KEYS, 0);
+    launch_step(a, e->st);
     HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(e->h_ctl, e->ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, e->st));
     HIPCHK(hipStreamSynchronize(e->st));
-    ChangeDev d;
-    HIPCHK(hipMemcpy(&d, e->log, sizeof d, hipMemcpyDeviceToHost));
-    return convert(e, d, out);
+    const DevCtl c = *e->h_ctl;
+    if (c.logpos > 0) {
+        // the step committed (a change, no change or an error); a NEED_EXACT raised by
+        // the prep that followed the apply only asks for exact loads before the next step
+        ChangeDev d;
+        HIPCHK(hipMemcpy(&d, e->log, sizeof d, hipMemcpyDeviceToHost));
+        const int rc = convert(e, d, out);
+        if (rc == KB_CHANGE && (c.halted == H_NEED_EXACT || c.want_refresh))
+            if (refresh(e) != KB_OK) return KB_ERR_HIP;
+        return rc;
+    }
+    // the resolve could not certify its decision from the bounds: every rank reaches
+    // the same verdict on the same state -- refold, then redo the step
+    if (c.halted == H_NEED_EXACT && refresh(e) != KB_OK) return KB_ERR_HIP;
+    memset(out, 0, sizeof *out);
+    out->status = KB_RETRY;
+    return KB_RETRY;
 }

@@ -5,18 +5,22 @@
 
 namespace kbe {
 
-constexpr int MAXB = 4096;          // dense broker universe limit (prep sorts it in LDS)
+constexpr int MAXB = 4096;          // dense broker universe limit (sorted in LDS)
 constexpr int MAXR = 16;            // replica slots per partition
-constexpr int TILE = 1024;          // partitions per scan/census workgroup
-constexpr int SCAN_THREADS = 256;   // 4 consecutive partitions per lane
-constexpr int PER_LANE = 4;
-constexpr int RESOLVE_THREADS = 1024;
-constexpr int PREP_THREADS = 1024;
+constexpr int SCAN_THREADS = 512;   // k_scan workgroup
+constexpr int PER_LANE = 4;         // consecutive partitions per lane (vector loads)
+constexpr int TILE = SCAN_THREADS * PER_LANE;   // 2048 partitions per scan tile
+constexpr int SHARD_ALIGN = 1024;   // shard boundaries (multi-GPU) are multiples of this
+constexpr int STEP_THREADS = 1024;  // k_step: one workgroup
 constexpr uint32_t NONE32 = 0xFFFFFFFFu;
 constexpr unsigned long long NONE64 = ~0ull;
-constexpr int SUMMARY_CONT = 1024;  // distinct near-tie keys carried per rank in a summary
-constexpr int DEDUP_RESOLVE = 2048; // LDS key table of k_resolve / k_summary
-constexpr int DEDUP_CENSUS = 512;   // LDS key table of one k_census workgroup
+constexpr uint16_t NONE16 = 0xFFFFu;
+constexpr int TILE_KEYS = 16;       // near-tie keys carried in a scan workgroup record
+constexpr int SUMMARY_KEYS = 1024;  // near-tie keys carried per rank in a summary
+constexpr int DEDUP_STEP = 2048;    // LDS key table of k_step / k_summary
+constexpr int DEDUP_SCAN = 256;     // LDS key table of one k_scan workgroup
+constexpr int TMAX = 2 * MAXR + 4;  // brokers touched by one applied change (bound)
+constexpr int LDS_SETS_MAX = 65536; // set records staged in LDS when they fit in this
 
 // first-index predicates reduced by the scan (min over partition index)
 enum {
@@ -47,27 +51,33 @@ __host__ __device__ inline uint32_t make_meta(uint32_t nrep, uint32_t want, uint
 }
 constexpr uint32_t MAX_SETS = 1u << 15;
 
-// per-set target record, rebuilt every step by k_setlists:
-//   int32 nelig (|set ∩ bl_move|), int32 nlist, int32 ids[K] (first K eligible
-//   brokers in bl_move order), double r[K] (their relative loads L/avg - 1)
-__host__ __device__ inline int sr_ids_off() { return 8; }
-__host__ __device__ inline int sr_r_off(int K) { return (8 + 4 * K + 15) & ~15; }
-__host__ __device__ inline int sr_stride(int K) { return sr_r_off(K) + 8 * K; }
+// Per-set target record, maintained by k_step (16-byte units, u16 fields):
+//   [0] nelig = |set ∩ bl_move|, [1] nl = valid ids, [2 .. 2+KR) the first KR
+//   brokers of set ∩ bl_move in bl order (dense ids, NONE16 past nl).
+// KR >= RC + 1 so the first eligible non-replica target is always inside.
+__host__ __device__ constexpr int sr_units(int rc) { return (rc + 1 + 2 + 7) / 8; }
+__host__ __device__ constexpr int sr_kr(int rc) { return sr_units(rc) * 8 - 2; }
 
 struct Contender {                  // a near-tie candidate move (32 B)
     int32_t s, t;                   // dense source / target broker
-    double w;                       // partition weight (scored delta, steps.go:250,272)
+    double w;                       // partition weight (scored delta, steps.go:185,207)
     unsigned long long iter;        // (partition << 21) | (slot << 16) | target bl position
     int32_t kind;                   // 0 = leader move, 1 = non-leader move
     int32_t pad;
 };
 
-// per-tile scan record (64 B): no global atomics in the scan, k_reduce combines
-struct BlockRec {
+// header of a scan-workgroup record and of a rank summary (multi-GPU); the
+// near-tie keys follow it (TILE_KEYS resp. SUMMARY_KEYS slots)
+struct RecHdr {
     double dmin[2];                 // min score delta {leader, non-leader}
     unsigned long long cand[2];     // reference candidate counts
     uint32_t first[NF];             // first-index predicates
+    uint32_t nkeys;                 // keys stored after the header
+    uint32_t flags;                 // bit0: keys spilled / overflowed (see k_step)
+    uint32_t pad[2];
 };
+constexpr int WGREC_BYTES = (int)sizeof(RecHdr) + TILE_KEYS * (int)sizeof(Contender);
+constexpr int SUMMARY_BYTES = (int)sizeof(RecHdr) + SUMMARY_KEYS * (int)sizeof(Contender);
 
 struct ChangeDev {
     int32_t status, step, kind, slot;
@@ -78,18 +88,21 @@ struct ChangeDev {
     int32_t err_broker, pad;
 };
 
+// halted codes
+enum { H_RUN = 0, H_DONE = 1, H_NEED_EXACT = 2 };
+
 struct DevCtl {
     int32_t halted, steps, logpos, logcap;
-    int32_t nblm, heavy, light, npresent;
-    double S, avg, inv_avg, U0, eps, V;
-    unsigned long long gmin[2];     // order-preserving encoded min score delta per kind
-    uint32_t first[NF];
-    unsigned long long ncand[2];    // reference candidate count of this step per kind
-    uint32_t ncont, cont_overflow;
-    int32_t list_overflow, pad0;
-    unsigned long long total_cand, total_cont, total_folds;
+    int32_t prepped, budget, full_prep, want_refresh;
+    int32_t nblm, heavy, light, ndirty;
+    double S, avg, inv_avg, U0, eps, V, E;
+    uint32_t ncont, cont_overflow;  // raw near-tie spill buffer (scan -> step)
+    int32_t list_overflow, pending_list;
+    int32_t pl_kind, pl_from, pl_to, pl_pad;  // pending per-broker list operation
+    long long pl_part;
+    unsigned long long total_cand, total_cont, total_folds, total_exact_halts;
     // diagnostic phase stamps (builds with -DKB_STAMPS): accumulated
-    // wall_clock64 ticks (100 MHz) per phase of k_prep [0..7] and k_resolve [8..15]
+    // wall_clock64 ticks (100 MHz) per phase of k_step
     unsigned long long stamps[16];
 };
 
@@ -97,6 +110,7 @@ struct DevCtl {
 #define KB_STAMP_BEGIN() unsigned long long _kb_t0 = wall_clock64()
 #define KB_STAMP(ctl, i)                                                        \
     do {                                                                        \
+        __syncthreads();                                                        \
         if (threadIdx.x == 0) {                                                 \
             unsigned long long _t = wall_clock64();                             \
             (ctl)->stamps[i] += _t - _kb_t0;                                    \
@@ -107,15 +121,6 @@ struct DevCtl {
 #define KB_STAMP_BEGIN() (void)0
 #define KB_STAMP(ctl, i) (void)0
 #endif
-
-// summary exchanged between ranks each step (multi-GPU)
-struct Summary {
-    unsigned long long gmin[2];
-    uint32_t first[NF];
-    unsigned long long ncand[2];
-    uint32_t ncont, overflow;
-    Contender cont[SUMMARY_CONT];
-};
 
 // errors recorded in ChangeDev.err_code
 enum {

@@ -1,31 +1,34 @@
 // kernels.hip -- CDNA4 (gfx950) kernels of the kafkabalancer move-search engine.
 //
-// One Balance() step (balancer.go:49-65) is six launches on one stream:
-//   k_prep      1 WG   sort brokers by (load, id) (getBL, utils.go:107-117), exact
-//                      sequential folds of su (getUnbalanceBL, utils.go:119-147),
-//                      relative loads r = L/avg - 1, error bound eps
-//   k_setlists  nsets/4 WGs  per allowed-broker set: the first K brokers of the set
-//                      in bl order with their r (move targets, steps.go:257-266), and
-//                      the last K (Add / Disallowed picks, steps.go:102,130-134)
-//   k_scan      P/1024 WGs  the HBM stream over the SoA partition arrays: the Remove /
-//                      Add / Disallowed / distributeLeaders first-index predicates
-//                      (from the packed meta word) and the O(1)-delta score of every
-//                      leader / non-leader slot against its first eligible target
-//                      (steps.go:232-288); one 64-B record per workgroup
-//   k_reduce    1 WG   combines the per-workgroup records
-//   k_census    P/1024 WGs  exits unless its minimum is within 8*eps of the global one;
-//                      then enumerates the near-tie (partition, slot, target) moves and
-//                      de-duplicates them by key (source, target, weight) in LDS
-//   k_resolve   1 WG   the reference's step order; exact sequential folds for the
-//                      distinct near-tie keys (strict-< first minimum in (partition,
-//                      slot, target) order, steps.go:276); the certified decision; the
-//                      on-device apply (replacepl/addpl, utils.go:166-202) with an exact
-//                      partition-ordered refold of touched loads (utils.go:92-105).
+// One Balance() step (balancer.go:49-65) is two launches on one stream:
 //
-// Exactness: values the reference's decision depends on are computed in the
-// reference's own operation order (IEEE binary64, no FMA: the file is built with
-// -ffp-contract=off; true division), or bounded by eps and resolved exactly when
-// the bound does not decide (DESIGN.md "Exactness").
+//   k_scan   grid   the HBM stream over the SoA partition arrays.  Every workgroup
+//                   stages the relative-load table r[B] and the per-set target
+//                   records in LDS, then for each of its tiles of 2048 partitions
+//                   evaluates the Remove / Add / Disallowed / distributeLeaders
+//                   first-index predicates (from the packed meta word) and the
+//                   O(1)-delta score of every leader / non-leader slot against its
+//                   first eligible target (steps.go:167-222); the tile minimum is
+//                   found with wave shuffles + LDS, and the near-tie census (all
+//                   (partition, slot, target) within 4*eps of it) is taken right
+//                   away, de-duplicated by key in LDS.  One record per workgroup.
+//   k_step   1 WG   the serial half: combine the records; the reference's step
+//                   order (RemoveExtra / AddMissing / MoveDisallowed /
+//                   ReassignLeaders / MoveLeaders / MoveNonLeaders, balancer.go:34-44);
+//                   certified decision or exact sequential folds for near ties
+//                   (strict-< first minimum in (partition, slot, target) order,
+//                   steps.go:211); the on-device apply (replacepl/addpl,
+//                   utils.go:166-202); then the prep of the next step: incremental
+//                   re-sort of the touched brokers (getBL, utils.go:107-117), bl_move
+//                   compaction, relative loads, error bound eps, set records.
+//
+// Loads are exact in integral mode.  Otherwise a step updates the touched loads
+// incrementally and tracks a rigorous error bound; whenever a decision or the
+// broker order cannot be certified from the bounds, the step halts with
+// H_NEED_EXACT, the host runs k_refresh (exact partition-ordered refolds,
+// utils.go:92-105) and the step is re-run.  Values the reference's decision
+// depends on are then computed in the reference's own operation order (IEEE
+// binary64, no FMA: the file is built with -ffp-contract=off; true division).
 #include <hip/hip_runtime.h>
 #include <cfloat>
 #include <cstdint>
@@ -38,16 +41,6 @@ namespace kbe {
 
 __device__ __forceinline__ unsigned long long d2u(double d) { return (unsigned long long)__double_as_longlong(d); }
 __device__ __forceinline__ double u2d(unsigned long long u) { return __longlong_as_double((long long)u); }
-
-// order-preserving encoding of a double into u64
-__device__ __forceinline__ unsigned long long enc(double d) {
-    unsigned long long u = d2u(d);
-    return (u >> 63) ? ~u : (u | 0x8000000000000000ull);
-}
-__device__ __forceinline__ double dec(unsigned long long e) {
-    unsigned long long u = (e >> 63) ? (e & 0x7FFFFFFFFFFFFFFFull) : ~e;
-    return u2d(u);
-}
 
 // reference term (utils.go:136-143): r = L/avg - 1; r>0 ? r*r : r*r/2 (exact ops)
 __device__ __forceinline__ double term_x(double L, double avg) {
@@ -76,10 +69,35 @@ __device__ __forceinline__ T wave_min(T v) {
     return v;
 }
 template <typename T>
+__device__ __forceinline__ T wave_max(T v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) { T x = __shfl_xor(v, o); v = x > v ? x : v; }
+    return v;
+}
+template <typename T>
 __device__ __forceinline__ T wave_sum(T v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
     return v;
+}
+
+// u16 field idx of a set record held in registers / memory as 16-B units
+__device__ __forceinline__ uint32_t rec_u16(const uint4* v, int idx) {
+    const uint4 q = v[idx >> 3];
+    const int c = (idx >> 1) & 3;
+    const uint32_t word = c == 0 ? q.x : (c == 1 ? q.y : (c == 2 ? q.z : q.w));
+    return (idx & 1) ? (word >> 16) : (word & 0xFFFFu);
+}
+
+// gamma_n bound of a sequential n-term fold of non-negative terms (|fold - sum| <= gamma_n * sum)
+__device__ __forceinline__ double gamma_n(int n) { return 1.01 * (double)(n > 1 ? n : 1) * (DBL_EPSILON / 2); }
+
+// error bound of an approximate (dirty) load against the reference's fold
+__device__ __forceinline__ double load_err(const double* load, const double* lerr, const uint8_t* dirty,
+                                           const int32_t* cnt, int b) {
+    if (!dirty[b]) return 0.0;
+    const double a = lerr[b];
+    return a + gamma_n(cnt[b]) * (load[b] + a);
 }
 
 // Sequential fold of n doubles held in LDS, in order (the reference's fold).
@@ -98,8 +116,8 @@ __device__ __forceinline__ double fold_lds(const double* x, int n, double acc = 
     return acc;
 }
 
-// getUnbalanceBL (utils.go:119-147) of the bl_move order with bl[ps] = Ls and
-// bl[pt] = Lt (steps.go:250,272): two sequential folds, the reference's order.
+// getUnbalanceBL (utils.go:119-147) of the bl order with bl[ps] = Ls and
+// bl[pt] = Lt (steps.go:185,207): two sequential folds, the reference's order.
 __device__ double exact_unbalance_lds(const double* Lm, int n, int ps, int pt, double Ls, double Lt) {
     double S = 0.0;
     int k = 0;
@@ -132,7 +150,7 @@ __device__ double exact_unbalance_lds(const double* Lm, int n, int ps, int pt, d
 // LDS open-addressing table keyed by (kind, source, target); the weight bits are
 // claimed by the first insert; a different weight under the same key is a
 // "conflict" handled by the caller.  Contenders with one key have one exact U,
-// so only the earliest iteration index per key matters (steps.go:276).
+// so only the earliest iteration index per key matters (steps.go:211).
 
 struct Dedup {
     uint32_t* key;
@@ -179,202 +197,84 @@ __device__ __forceinline__ Contender dedup_entry(const Dedup& T, int h) {
     return c;
 }
 
-// --------------------------------------------------------------- k_prep
-
-__global__ __launch_bounds__(PREP_THREADS) void k_prep(PrepArgs a) {
-    extern __shared__ __align__(16) unsigned char smem[];
-    const int NP2 = a.NP2;
-    unsigned long long* keys = (unsigned long long*)smem;        // NP2
-    double* Tm = (double*)(keys + NP2);                           // NP2
-    uint32_t* idx = (uint32_t*)(Tm + NP2);                        // NP2
-    __shared__ double s_red[PREP_THREADS / 64];
-    __shared__ int s_wcnt[PREP_THREADS / 64];
-    __shared__ double s_avg, s_S, s_U0;
-    __shared__ int s_nblm;
-    DevCtl* ctl = a.ctl;
-    const int tid = threadIdx.x;
-    if (ctl->halted) return;
-    KB_STAMP_BEGIN();
-    if (tid == 0) {
-        ctl->gmin[0] = ctl->gmin[1] = NONE64;
-        for (int f = 0; f < NF; f++) ctl->first[f] = NONE32;
-        ctl->ncand[0] = ctl->ncand[1] = 0;
-        ctl->ncont = 0;
-        ctl->cont_overflow = 0;
-    }
-    for (int i = tid; i < NP2; i += PREP_THREADS) {
-        if (i < a.B) { keys[i] = d2u(a.load[i]); idx[i] = (uint32_t)i; }
-        else { keys[i] = NONE64; idx[i] = NONE32; }
-    }
-    __syncthreads();
-    KB_STAMP(ctl, 0);
-    // bitonic sort by (load bits, dense id); loads are finite and >= 0, so the
-    // IEEE bit pattern orders like the value (byBrokerLoad.Less, utils.go:23-28)
-    for (int k = 2; k <= NP2; k <<= 1) {
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int i = tid; i < NP2; i += PREP_THREADS) {
-                int ixj = i ^ j;
-                if (ixj > i) {
-                    unsigned long long ki = keys[i], kj = keys[ixj];
-                    uint32_t ii = idx[i], ij = idx[ixj];
-                    bool less = (kj < ki) || (kj == ki && ij < ii);
-                    bool up = (i & k) == 0;
-                    if (up == less) { keys[i] = kj; keys[ixj] = ki; idx[i] = ij; idx[ixj] = ii; }
-                }
-            }
-            __syncthreads();
-        }
-    }
-    KB_STAMP(ctl, 1);
-    // compaction of the bl_move subsequence (NP2 <= 4096 => 4 elements / thread)
-    int base = tid * 4;
-    int flag[4]; unsigned long long kv[4]; uint32_t iv[4];
-    int c = 0;
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-        int i = base + q;
-        flag[q] = 0;
-        kv[q] = 0; iv[q] = NONE32;
-        if (i < a.B) {
-            uint32_t b = idx[i];
-            kv[q] = keys[i]; iv[q] = b;
-            a.order[i] = (int32_t)b;
-            flag[q] = (a.cnt[b] > 0 || a.incfg[b]) ? 1 : 0;
-            c += flag[q];
-        }
-    }
-    const int lane = tid & 63, wid = tid >> 6;
-    int incl = c;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) { int y = __shfl_up(incl, o); if (lane >= o) incl += y; }
-    if (lane == 63) s_wcnt[wid] = incl;
-    __syncthreads();
-    int woff = 0, total = 0;
-    for (int w = 0; w < PREP_THREADS / 64; w++) { if (w < wid) woff += s_wcnt[w]; total += s_wcnt[w]; }
-    int pos = woff + incl - c;
-    __syncthreads();   // all reads of keys[] done before the in-place compaction
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-        int i = base + q;
-        if (i < a.B) {
-            uint32_t b = iv[q];
-            if (flag[q]) { keys[pos] = kv[q]; a.blm[pos] = (int32_t)b; a.posm[b] = pos; pos++; }
-            else a.posm[b] = -1;
-        }
-    }
-    if (tid == 0) s_nblm = total;
-    __syncthreads();
-    const int nblm = s_nblm;
-    const double* Lm = (const double*)keys;
-    KB_STAMP(ctl, 2);
-    // S: sequential fold in bl order (utils.go:123-128)
-    if (tid == 0) {
-        const double S = fold_lds(Lm, nblm);
-        s_S = S;
-        s_avg = S / (double)nblm;
-    }
-    __syncthreads();
-    KB_STAMP(ctl, 3);
-    const double avg = s_avg;
-    for (int k = tid; k < nblm; k += PREP_THREADS) Tm[k] = term_x(Lm[k], avg);
-    __syncthreads();
-    KB_STAMP(ctl, 4);
-    // su: sequential fold of the terms (utils.go:134-143)
-    if (tid == 0) s_U0 = fold_lds(Tm, nblm);
-    KB_STAMP(ctl, 5);
-    // error-bound ingredients: V = sum |r|(1+|r|), Rmax = max |r|
-    const double inv_avg = 1.0 / avg;
-    double v = 0.0, rm = 0.0;
-    for (int k = tid; k < nblm; k += PREP_THREADS) {
-        double r = fabs(Lm[k] * inv_avg - 1.0);
-        v += r * (1.0 + r);
-        rm = r > rm ? r : rm;
-    }
-    v = wave_sum(v);
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) { double x = __shfl_xor(rm, o); rm = x > rm ? x : rm; }
-    if (lane == 0) s_red[wid] = v;
-    __syncthreads();
-    double V = 0.0;
-    for (int w = 0; w < PREP_THREADS / 64; w++) V += s_red[w];
-    __syncthreads();
-    if (lane == 0) s_red[wid] = rm;
-    __syncthreads();
-    double Rm = 0.0;
-    for (int w = 0; w < PREP_THREADS / 64; w++) Rm = s_red[w] > Rm ? s_red[w] : Rm;
-    KB_STAMP(ctl, 6);
-    for (int b = tid; b < a.B; b += PREP_THREADS)
-        a.r[b] = a.posm[b] >= 0 ? __fma_rn(a.load[b], inv_avg, -1.0) : 0.0;
-    if (tid == 0) {
-        const double u = DBL_EPSILON / 2;
-        double R = Rm + a.rmax_w * inv_avg;
-        double eps = 64.0 * u * ((double)(nblm + 8) * (s_U0 + 2.0 * V) + 4.0 * (1.0 + R) * (1.0 + R));
-        if (!(eps > 1e-300)) eps = 1e-300;
-        ctl->S = s_S; ctl->avg = avg; ctl->inv_avg = inv_avg; ctl->U0 = s_U0;
-        ctl->V = V; ctl->eps = eps; ctl->nblm = nblm;
-        ctl->heavy = nblm > 0 ? a.blm[nblm - 1] : -1;
-        ctl->light = nblm > 0 ? a.blm[0] : -1;
-    }
-    KB_STAMP(ctl, 7);
+__device__ __forceinline__ double cont_delta(const double* r, const Contender& c, double inv_avg) {
+    const double delta = c.w * inv_avg;
+    return dsrc(r[c.s], delta) + dtgt(r[c.t], delta);
 }
 
-// ------------------------------------------------------------ k_setlists
+// ------------------------------------------------ per-broker list upkeep
+// (partition lists sorted by index, for the exact refold of k_refresh)
 
-__global__ __launch_bounds__(256) void k_setlists(SetArgs a) {
-    if (a.ctl->halted) return;
-    __shared__ int32_t s_order[MAXB];
-    __shared__ unsigned long long s_blm[MAXB / 64], s_pres[MAXB / 64];
-    __shared__ unsigned long long s_sb[4][MAXB / 64];
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    for (int i = tid; i < a.W64; i += 256) { s_blm[i] = 0; s_pres[i] = 0; }
-    const int set = blockIdx.x * 4 + wv;
-    for (int i = lane; i < a.W64; i += 64) s_sb[wv][i] = set < a.nsets ? a.setbits[(size_t)set * a.W64 + i] : 0ull;
+// remove partition q from broker b's list (block-wide, all threads call)
+__device__ void list_remove(const Lists& L, int b, uint32_t q, int* s_i) {
+    const uint32_t st = L.lstart[b], n = L.llen[b];
+    const uint32_t nt = blockDim.x;
+    if (threadIdx.x == 0) *s_i = -1;
     __syncthreads();
-    for (int i = tid; i < a.B; i += 256) {
-        s_order[i] = a.order[i];
-        if (a.posm[i] >= 0) atomicOr(&s_blm[i >> 6], 1ull << (i & 63));
-        if (a.cnt[i] > 0) atomicOr(&s_pres[i >> 6], 1ull << (i & 63));
+    for (uint32_t i = threadIdx.x; i < n; i += nt)
+        if (L.lent[st + i] == q) *s_i = (int)i;
+    __syncthreads();
+    const int at = *s_i;
+    if (at < 0) return;
+    for (uint32_t c = (uint32_t)at; c + 1 < n; c += nt) {
+        uint32_t j = c + threadIdx.x;
+        uint32_t v = 0;
+        bool act = j + 1 < n;
+        if (act) v = L.lent[st + j + 1];
+        __syncthreads();
+        if (act) L.lent[st + j] = v;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) L.llen[b] = n - 1;
+    __syncthreads();
+}
+
+// insert partition q into broker b's sorted list
+__device__ bool list_insert(const Lists& L, int b, uint32_t q, int* s_i) {
+    const uint32_t st = L.lstart[b], n = L.llen[b];
+    const uint32_t nt = blockDim.x;
+    if (n >= L.lcap[b]) return false;
+    if (threadIdx.x == 0) *s_i = 0;
+    __syncthreads();
+    int c = 0;
+    for (uint32_t i = threadIdx.x; i < n; i += nt) c += L.lent[st + i] < q ? 1 : 0;
+    c = wave_sum(c);
+    if ((threadIdx.x & 63) == 0 && c) atomicAdd(s_i, c);
+    __syncthreads();
+    const uint32_t at = (uint32_t)*s_i;
+    long long hi = (long long)n;
+    while (hi > (long long)at) {
+        long long lo = hi - (long long)nt;
+        if (lo < (long long)at) lo = at;
+        long long j = lo + threadIdx.x;
+        bool act = j < hi;
+        uint32_t v = 0;
+        if (act) v = L.lent[st + j];
+        __syncthreads();
+        if (act) L.lent[st + j + 1] = v;
+        __syncthreads();
+        hi = lo;
+    }
+    if (threadIdx.x == 0) { L.lent[st + at] = q; L.llen[b] = n + 1; }
+    __syncthreads();
+    return true;
+}
+
+// the list change of the last applied move (kind 1 replace, 2 remove, 3 add)
+__device__ void do_list_op(DevCtl* ctl, const Lists& L, int* s_i) {
+    if (!ctl->pending_list) return;
+    const int kind = ctl->pl_kind, from = ctl->pl_from, to = ctl->pl_to;
+    const uint32_t p = (uint32_t)ctl->pl_part;
+    bool ok = true;
+    if (kind == 1) { list_remove(L, from, p, s_i); ok = list_insert(L, to, p, s_i); }
+    else if (kind == 2) list_remove(L, from, p, s_i);
+    else if (kind == 3) ok = list_insert(L, to, p, s_i);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        if (!ok) ctl->list_overflow = 1;
+        ctl->pending_list = 0;
     }
     __syncthreads();
-    if (set >= a.nsets) return;
-    const unsigned long long* sb = s_sb[wv];
-    const unsigned long long lt = (1ull << lane) - 1ull;
-    unsigned char* rec = a.setrec + (size_t)set * a.stride;
-    int32_t* ids = (int32_t*)(rec + sr_ids_off());
-    double* rr = (double*)(rec + sr_r_off(a.K));
-    // kind 0: first K of set ∩ bl_move ascending; 1: last K of set ∩ present; 2: last K of set
-    for (int kind = 0; kind < 3; kind++) {
-        int found = 0;
-        for (int base = 0; base < a.B && found < a.K; base += 64) {
-            const int k = base + lane;
-            bool mem = false;
-            int b = -1;
-            if (k < a.B) {
-                b = s_order[kind == 0 ? k : a.B - 1 - k];
-                mem = (sb[b >> 6] >> (b & 63)) & 1ull;
-                if (kind == 0) mem = mem && ((s_blm[b >> 6] >> (b & 63)) & 1ull);
-                else if (kind == 1) mem = mem && ((s_pres[b >> 6] >> (b & 63)) & 1ull);
-            }
-            const unsigned long long m = __ballot(mem);
-            if (mem) {
-                const int rk = found + __popcll(m & lt);
-                if (rk < a.K) {
-                    if (kind == 0) { ids[rk] = b; rr[rk] = a.r[b]; }
-                    else a.lists[((size_t)set * 2 + (kind - 1)) * a.K + rk] = b;
-                }
-            }
-            found += __popcll(m);
-        }
-        for (int rk = found + lane; rk < a.K; rk += 64) {
-            if (kind == 0) { ids[rk] = -1; rr[rk] = 0.0; }
-            else a.lists[((size_t)set * 2 + (kind - 1)) * a.K + rk] = -1;
-        }
-        if (kind == 0 && lane == 0) ((int32_t*)rec)[1] = found < a.K ? found : a.K;
-    }
-    int n = 0;
-    for (int i = lane; i < a.W64; i += 64) n += __popcll(sb[i] & s_blm[i]);
-    n = wave_sum(n);
-    if (lane == 0) ((int32_t*)rec)[0] = n;
 }
 
 // --------------------------------------------------------------- k_scan
@@ -401,169 +301,1144 @@ __device__ __forceinline__ void load_parts(const ScanArgs& a, long long base, Pa
     }
 }
 
-// the first KT entries of a set record always contain the first eligible target
-// (at most nrep <= RC of them are replicas)
-template <int RC>
-struct TargetRegs {
-    static constexpr int KT = RC + 1;
-    int32_t id[PER_LANE][KT];
-    double r[PER_LANE][KT];
-    int32_t nelig[PER_LANE];
-    double rs[PER_LANE][RC];
-};
+__device__ __forceinline__ void emit_global(DevCtl* ctl, Contender* cont, uint32_t cap, const Contender& c) {
+    uint32_t i = atomicAdd(&ctl->ncont, 1u);
+    if (i < cap) cont[i] = c;
+    else ctl->cont_overflow = 1;
+}
 
-template <int RC>
-__global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
-    DevCtl* ctl = a.ctl;
-    if (ctl->halted) return;
-    const double inv_avg = ctl->inv_avg;
-    const int heavy = ctl->heavy;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const long long base = a.shard_begin + (long long)blockIdx.x * TILE + (long long)tid * PER_LANE;
-    constexpr int KT = TargetRegs<RC>::KT;
-    const int roff = sr_r_off(a.K);
-
-    PartRegs<RC> P;
-    load_parts<RC>(a, base, P);
-    // issue every per-broker lookup of the 4 partitions before using any
-    // (one L1/L2 round trip): set records and source relative loads
-    TargetRegs<RC> T;
-#pragma unroll
-    for (int j = 0; j < PER_LANE; j++) {
-        const unsigned char* rec = a.setrec + (size_t)meta_set(P.m[j]) * a.stride;
-        T.nelig[j] = ((const int32_t*)rec)[0];
-#pragma unroll
-        for (int i = 0; i < KT; i++) {
-            T.id[j][i] = ((const int32_t*)(rec + sr_ids_off()))[i];
-            T.r[j][i] = ((const double*)(rec + roff))[i];
-        }
-#pragma unroll
-        for (int k = 0; k < RC; k++) T.rs[j][k] = a.r[P.r[k][j]];
+__device__ __forceinline__ void emit(const ScanArgs& a, const Dedup& T, int kind, int s, int t, double w,
+                                     unsigned long long iter) {
+    if (dedup_insert(T, kind, s, t, w, iter) < 0) {   // table full or weight conflict: spill it raw
+        Contender c;
+        c.s = s; c.t = t; c.w = w; c.iter = iter; c.kind = kind; c.pad = 0;
+        emit_global(a.ctl, a.cont, a.cont_cap, c);
     }
+}
 
-    double dminL = HUGE_VAL, dminN = HUGE_VAL;
+// walk every allowed, non-replica target in bl order for one (partition, slot)
+// and emit the ones within 4*eps of the tile minimum g; stop once 8*eps is
+// exceeded (the approximate delta is monotone in the target load up to 2*eps).
+template <int RC>
+__device__ void walk_targets(const ScanArgs& a, const Dedup& T, const double* s_r, const uint16_t* rec16,
+                             int kind, long long p, int slot, int src, const uint32_t (&reps)[RC], int nrep,
+                             int set, double w, double ds, double g, double eps, double inv_avg, int nblm) {
+    constexpr int KR = sr_kr(RC);
+    const unsigned long long ib = ((unsigned long long)p << 21) | ((unsigned long long)slot << 16);
+    const double delta = w * inv_avg;
+    const int nl = rec16[1];
+    int last = -1;
+    for (int i = 0; i < nl; i++) {                // the set's first KR eligible brokers
+        const int b = rec16[2 + i];
+        last = b;
+        bool isrep = false;
+#pragma unroll
+        for (int q = 0; q < RC; q++) isrep |= (q < nrep) && ((int)reps[q] == b);
+        if (isrep) continue;
+        const double d = ds + dtgt(s_r[b], delta);
+        if (d <= g + 4.0 * eps) emit(a, T, kind, src, b, w, ib | (unsigned long long)a.posm[b]);
+        if (d > g + 8.0 * eps) return;
+    }
+    if (nl < KR || last < 0) return;              // the set is exhausted
+    const uint64_t* sb = a.setbits + (size_t)set * a.W64;
+    for (int k = a.posm[last] + 1; k < nblm; k++) {   // rare: more than KR near-tied targets
+        const int b = a.blm[k];
+        if (!setbit(sb, b)) continue;
+        bool isrep = false;
+#pragma unroll
+        for (int q = 0; q < RC; q++) isrep |= (q < nrep) && ((int)reps[q] == b);
+        if (isrep) continue;
+        const double d = ds + dtgt(s_r[b], delta);
+        if (d <= g + 4.0 * eps) emit(a, T, kind, src, b, w, ib | (unsigned long long)k);
+        if (d > g + 8.0 * eps) return;
+    }
+}
+
+// first allowed target in bl order that is not a replica (steps.go:192-201):
+// among the first RC+1 entries of the partition's set record
+template <int RC, bool LSETS>
+__device__ __forceinline__ int first_target(const ScanArgs& a, const uint4* s_set, uint32_t m,
+                                            const uint32_t (&reps)[RC], int nrep, int* nelig) {
+    constexpr int U = sr_units(RC);
+    constexpr int KT = RC + 1;
+    const uint32_t set = meta_set(m);
+    uint4 R[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) R[u] = LSETS ? s_set[set * U + u] : a.setrec[(size_t)set * U + u];
+    *nelig = (int)rec_u16(R, 0);
+    int tb = -1;
+#pragma unroll
+    for (int i = KT - 1; i >= 0; i--) {
+        const int b = (int)rec_u16(R, 2 + i);
+        bool isrep = false;
+#pragma unroll
+        for (int k = 0; k < RC; k++) isrep |= (k < nrep) && ((int)reps[k] == b);
+        if (b != (int)NONE16 && !isrep) tb = b;
+    }
+    return tb;
+}
+
+// the lane's slots within 8*eps of the tile minima: rescore and walk their targets
+template <int RC, bool LSETS>
+__device__ __forceinline__ void census(const ScanArgs& a, const Dedup& T, const double* s_r, const uint4* s_set,
+                                       long long base, bool wl, bool wn, double tL,
+                                       double tN, double eps, double inv_avg, int nblm) {
+    constexpr int U = sr_units(RC);
+#pragma unroll 1
+    for (int j = 0; j < PER_LANE; j++) {
+        const long long p = base + j;
+        if (p >= a.shard_end) continue;
+        // re-read the partition (rare path: keeps the stream's registers out of scratch)
+        const uint32_t m = a.meta[p];
+        const int nrep = (int)meta_nrep(m), set = (int)meta_set(m);
+        if (!meta_elig(m) || nrep == 0) continue;
+        uint32_t reps[RC];
+#pragma unroll
+        for (int k = 0; k < RC; k++) reps[k] = a.rep[(long long)k * a.Ppad + p];
+        int nelig;
+        const int tb = first_target<RC, LSETS>(a, s_set, m, reps, nrep, &nelig);
+        if (tb < 0) continue;
+        const uint16_t* rec16 = LSETS ? (const uint16_t*)(s_set + (size_t)set * U)
+                                      : (const uint16_t*)(a.setrec + (size_t)set * U);
+        const double w = a.w[p];
+        const double delta = w * inv_avg;
+        const double dt = dtgt(s_r[tb], delta);
+        if (wl && a.allow_leader) {
+            const double ds = dsrc(s_r[reps[0]], delta);
+            if (ds + dt <= tL + 8.0 * eps)
+                walk_targets<RC>(a, T, s_r, rec16, 0, p, 0, (int)reps[0], reps, nrep, set, w, ds, tL, eps,
+                                 inv_avg, nblm);
+        }
+        if (wn)
+#pragma unroll 1
+            for (int k = 1; k < nrep; k++) {
+                uint32_t src = reps[0];
+#pragma unroll
+                for (int q = 1; q < RC; q++) src = k == q ? reps[q] : src;
+                const double ds = dsrc(s_r[src], delta);
+                if (ds + dt <= tN + 8.0 * eps)
+                    walk_targets<RC>(a, T, s_r, rec16, 1, p, k, (int)src, reps, nrep, set, w, ds, tN, eps,
+                                     inv_avg, nblm);
+            }
+    }
+}
+
+template <int RC, bool LSETS>
+__global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
+    extern __shared__ __align__(16) unsigned char smem[];
+    __shared__ int s_i;
+    DevCtl* ctl = a.ctl;
+    if (a.listwg && (int)blockIdx.x == a.nscan) { do_list_op(ctl, a.L, &s_i); return; }
+    if (ctl->halted != H_RUN || !ctl->prepped || ctl->steps >= ctl->budget) return;
+    constexpr int U = sr_units(RC);
+    constexpr int NW = SCAN_THREADS / 64;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const double inv_avg = ctl->inv_avg, eps = ctl->eps;
+    const int heavy = ctl->heavy, nblm = ctl->nblm;
+
+    double* s_r = (double*)smem;
+    const size_t rbytes = ((size_t)a.B * 8 + 15) & ~(size_t)15;
+    uint4* s_set = (uint4*)(smem + rbytes);
+    const size_t setbytes = LSETS ? (size_t)a.nsets * U * 16 : 0;
+    uint32_t* s_key = (uint32_t*)(smem + rbytes + setbytes);
+    unsigned long long* s_wb = (unsigned long long*)(s_key + DEDUP_SCAN);
+    unsigned long long* s_it = s_wb + DEDUP_SCAN;
+    Dedup T{s_key, s_wb, s_it, DEDUP_SCAN};
+    __shared__ double s_red[2][NW];
+    __shared__ uint32_t s_f[NF][NW];
+    __shared__ unsigned long long s_c[2][NW];
+    __shared__ uint32_t s_nk;
+
+    int tile = blockIdx.x;
+    PartRegs<RC> P;
+    // issue the first tile's stream before staging the lookup tables
+    if (tile < a.ntiles) load_parts<RC>(a, a.shard_begin + (long long)tile * TILE + (long long)tid * PER_LANE, P);
+    for (int i = tid; i < a.B; i += SCAN_THREADS) s_r[i] = a.r[i];
+    if (LSETS) for (int i = tid; i < a.nsets * U; i += SCAN_THREADS) s_set[i] = a.setrec[i];
+    for (int i = tid; i < DEDUP_SCAN; i += SCAN_THREADS) { s_key[i] = NONE32; s_wb[i] = NONE64; s_it[i] = NONE64; }
+    if (tid == 0) s_nk = 0;
+    __syncthreads();
+
+    double wgL = HUGE_VAL, wgN = HUGE_VAL;
     uint32_t fst[NF];
 #pragma unroll
     for (int f = 0; f < NF; f++) fst[f] = NONE32;
     unsigned long long cL = 0, cN = 0;
 
+    for (bool first = true; tile < a.ntiles; tile += a.nscan, first = false) {
+        const long long base = a.shard_begin + (long long)tile * TILE + (long long)tid * PER_LANE;
+        if (!first) load_parts<RC>(a, base, P);
+        // lane minima only: the per-slot scores are recomputed by the (rare) census
+        double lL = HUGE_VAL, lN = HUGE_VAL;
 #pragma unroll
-    for (int j = 0; j < PER_LANE; j++) {
-        const long long p = base + j;
-        const bool valid = p < a.shard_end;
-        const uint32_t m = P.m[j];
-        const int nrep = (int)meta_nrep(m), want = (int)meta_want(m);
-        const bool elig = valid && meta_elig(m);
-        const uint32_t pi = valid ? (uint32_t)p : NONE32;
-        if (a.sem_go) {
-            bool dup = false;
+        for (int j = 0; j < PER_LANE; j++) {
+            const long long p = base + j;
+            const bool valid = p < a.shard_end;
+            const uint32_t m = P.m[j];
+            const int nrep = (int)meta_nrep(m), want = (int)meta_want(m);
+            const bool elig = valid && meta_elig(m);
+            const uint32_t pi = valid ? (uint32_t)p : NONE32;
+            if (a.sem_go) {
+                bool dup = false;
 #pragma unroll
-            for (int x = 0; x < RC; x++)
+                for (int x = 0; x < RC; x++)
 #pragma unroll
-                for (int y = x + 1; y < RC; y++) dup |= (y < nrep) && P.r[x][j] == P.r[y][j];
-            if (dup) fst[F_DUP] = min(fst[F_DUP], pi);
-        }
-        if (want < nrep) fst[F_REMOVE] = min(fst[F_REMOVE], pi);
-        if (want > nrep) fst[F_ADD] = min(fst[F_ADD], pi);
-        if (nrep == 0) {
-            fst[F_EMPTY] = min(fst[F_EMPTY], pi);
-            if (elig) fst[F_EMPTY_ELIG] = min(fst[F_EMPTY_ELIG], pi);
-        }
-        if (meta_dis(m)) fst[F_DIS] = min(fst[F_DIS], pi);
-        if (a.rebalance && elig && nrep > 0 && (int)P.r[0][j] == heavy) fst[F_LEAD] = min(fst[F_LEAD], pi);
-        // first allowed target in bl order that is not a replica (steps.go:257-266)
-        double rt = 0.0;
-        bool have = false;
+                    for (int y = x + 1; y < RC; y++) dup |= (y < nrep) && P.r[x][j] == P.r[y][j];
+                if (dup) fst[F_DUP] = min(fst[F_DUP], pi);
+            }
+            if (want < nrep) fst[F_REMOVE] = min(fst[F_REMOVE], pi);
+            if (want > nrep) fst[F_ADD] = min(fst[F_ADD], pi);
+            if (nrep == 0) {
+                fst[F_EMPTY] = min(fst[F_EMPTY], pi);
+                if (elig) fst[F_EMPTY_ELIG] = min(fst[F_EMPTY_ELIG], pi);
+            }
+            if (meta_dis(m)) fst[F_DIS] = min(fst[F_DIS], pi);
+            if (a.rebalance && elig && nrep > 0 && (int)P.r[0][j] == heavy) fst[F_LEAD] = min(fst[F_LEAD], pi);
+            if (!elig || nrep == 0) continue;
+            uint32_t reps[RC];
 #pragma unroll
-        for (int i = KT - 1; i >= 0; i--) {
-            const int b = T.id[j][i];
-            bool isrep = false;
-#pragma unroll
-            for (int k = 0; k < RC; k++) isrep |= (k < nrep) && ((int)P.r[k][j] == b);
-            if (b >= 0 && !isrep) { rt = T.r[j][i]; have = true; }
-        }
-        if (elig && nrep > 0 && have) {
+            for (int k = 0; k < RC; k++) reps[k] = P.r[k][j];
+            int nelig;
+            const int tb = first_target<RC, LSETS>(a, s_set, m, reps, nrep, &nelig);
+            if (tb < 0) continue;
             const double delta = P.w[j] * inv_avg;
-            const double dt = dtgt(rt, delta);
-            const unsigned long long ne = (unsigned long long)(T.nelig[j] - (int)meta_nin(m));
+            const double dt = dtgt(s_r[tb], delta);
+            const unsigned long long ne = (unsigned long long)(nelig - (int)meta_nin(m));
             if (a.allow_leader) {
-                const double d = dsrc(T.rs[j][0], delta) + dt;
-                dminL = d < dminL ? d : dminL;
+                const double d = dsrc(s_r[P.r[0][j]], delta) + dt;
+                lL = d < lL ? d : lL;
                 cL += ne;
             }
 #pragma unroll
-            for (int k = 1; k < RC; k++) {
+            for (int k = 1; k < RC; k++)
                 if (k < nrep) {
-                    const double d = dsrc(T.rs[j][k], delta) + dt;
-                    dminN = d < dminN ? d : dminN;
+                    const double d = dsrc(s_r[P.r[k][j]], delta) + dt;
+                    lN = d < lN ? d : lN;
                 }
-            }
             cN += ne * (unsigned long long)(nrep - 1);
         }
+        // tile minimum: wave shuffles, then LDS across the waves
+        double tL = wave_min(lL), tN = wave_min(lN);
+        if (lane == 0) { s_red[0][wid] = tL; s_red[1][wid] = tN; }
+        __syncthreads();
+#pragma unroll
+        for (int x = 0; x < NW; x++) {
+            tL = s_red[0][x] < tL ? s_red[0][x] : tL;
+            tN = s_red[1][x] < tN ? s_red[1][x] : tN;
+        }
+        __syncthreads();
+        // near-tie census against the tile minimum (usually one slot per tile)
+        const bool wl = tL < HUGE_VAL && lL <= tL + 8.0 * eps;
+        const bool wn = tN < HUGE_VAL && lN <= tN + 8.0 * eps;
+        if (wl || wn) census<RC, LSETS>(a, T, s_r, s_set, base, wl, wn, tL, tN, eps, inv_avg, nblm);
+        wgL = tL < wgL ? tL : wgL;
+        wgN = tN < wgN ? tN : wgN;
     }
-    // workgroup reduction: wave shuffles, then LDS across the 4 waves
-    __shared__ double s_d[2][SCAN_THREADS / 64];
-    __shared__ uint32_t s_f[NF][SCAN_THREADS / 64];
-    __shared__ unsigned long long s_c[2][SCAN_THREADS / 64];
-    dminL = wave_min(dminL);
-    dminN = wave_min(dminN);
+    // workgroup record: counts, first-index predicates, minima, near-tie keys
     cL = wave_sum(cL);
     cN = wave_sum(cN);
 #pragma unroll
     for (int f = 0; f < NF; f++) fst[f] = wave_min(fst[f]);
     if (lane == 0) {
-        s_d[0][wid] = dminL; s_d[1][wid] = dminN;
         s_c[0][wid] = cL; s_c[1][wid] = cN;
 #pragma unroll
         for (int f = 0; f < NF; f++) s_f[f][wid] = fst[f];
     }
+    __syncthreads();   // also orders every census insert before the flush
+    RecHdr* hdr = (RecHdr*)(a.recs + (size_t)blockIdx.x * WGREC_BYTES);
+    Contender* keys = (Contender*)(hdr + 1);
+    for (int h = tid; h < DEDUP_SCAN; h += SCAN_THREADS) {
+        if (s_key[h] == NONE32 || s_wb[h] == NONE64) continue;
+        const Contender c = dedup_entry(T, h);
+        const double g = c.kind == 0 ? wgL : wgN;
+        if (!(cont_delta(s_r, c, inv_avg) <= g + 4.0 * eps)) continue;
+        const uint32_t k = atomicAdd(&s_nk, 1u);
+        if (k < (uint32_t)TILE_KEYS) keys[k] = c;
+        else emit_global(ctl, a.cont, a.cont_cap, c);
+    }
     __syncthreads();
     if (tid == 0) {
-        for (int x = 1; x < SCAN_THREADS / 64; x++) {
-            dminL = s_d[0][x] < dminL ? s_d[0][x] : dminL;
-            dminN = s_d[1][x] < dminN ? s_d[1][x] : dminN;
+        RecHdr r;
+        for (int x = 1; x < NW; x++) {
             cL += s_c[0][x]; cN += s_c[1][x];
 #pragma unroll
             for (int f = 0; f < NF; f++) fst[f] = min(fst[f], s_f[f][x]);
         }
-        BlockRec r;
-        r.dmin[0] = dminL; r.dmin[1] = dminN;
+        r.dmin[0] = wgL; r.dmin[1] = wgN;
         r.cand[0] = cL; r.cand[1] = cN;
 #pragma unroll
         for (int f = 0; f < NF; f++) r.first[f] = fst[f];
-        a.blockrec[blockIdx.x] = r;
+        r.nkeys = s_nk < (uint32_t)TILE_KEYS ? s_nk : (uint32_t)TILE_KEYS;
+        r.flags = 0;
+        r.pad[0] = r.pad[1] = 0;
+        *hdr = r;
     }
 }
 
-// ------------------------------------------------------------- k_reduce
-// one workgroup combines the per-tile records (instead of same-address atomics,
-// which serialise at ~90 ops/us per word)
-__global__ __launch_bounds__(1024) void k_reduce(ReduceArgs a) {
-    DevCtl* ctl = a.ctl;
-    if (ctl->halted) return;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    double d0 = HUGE_VAL, d1 = HUGE_VAL;
-    unsigned long long c0 = 0, c1 = 0;
-    uint32_t f[NF];
-#pragma unroll
-    for (int q = 0; q < NF; q++) f[q] = NONE32;
-    for (int i = tid; i < a.tiles; i += 1024) {
-        const BlockRec r = a.blockrec[i];
-        d0 = r.dmin[0] < d0 ? r.dmin[0] : d0;
-        d1 = r.dmin[1] < d1 ? r.dmin[1] : d1;
-        c0 += r.cand[0]; c1 += r.cand[1];
-#pragma unroll
-        for (int q = 0; q < NF; q++) f[q] = min(f[q], r.first[q]);
+// --------------------------------------------------------------- k_step
+
+struct Decision {
+    int32_t status, step, kind, slot;
+    long long part;
+    int32_t from, to;
+    double su, cu;
+    int32_t exact, err, err_broker, pad;
+};
+
+// every near-tie contender of `kind` within 4*eps of g: the keys of the
+// records whose minimum is within 8*eps, then the raw spill buffer
+template <typename F>
+__device__ void for_each_contender(const StepArgs& a, int kind, double g, double eps, double inv_avg, F f) {
+    const int nt = blockDim.x;
+    for (int i = threadIdx.x; i < a.nrec; i += nt) {
+        const RecHdr* h = (const RecHdr*)(a.recs + (size_t)i * a.rec_stride);
+        if (!(h->dmin[kind] <= g + 8.0 * eps)) continue;
+        const Contender* keys = (const Contender*)(h + 1);
+        const int nk = (int)min(h->nkeys, (uint32_t)a.rec_keys);
+        for (int k = 0; k < nk; k++) {
+            const Contender c = keys[k];
+            if (c.kind != kind) continue;
+            if (cont_delta(a.r, c, inv_avg) <= g + 4.0 * eps) f(c);
+        }
     }
-    d0 = wave_min(d0); d1 = wave_min(d1); c0 = wave_sum(c0); c1 = wave_sum(c1);
+    if (a.use_spill) {
+        const uint32_t n = min(a.ctl->ncont, a.cont_cap);
+        for (uint32_t i = threadIdx.x; i < n; i += nt) {
+            const Contender c = a.cont[i];
+            if (c.kind != kind) continue;
+            if (cont_delta(a.r, c, inv_avg) <= g + 4.0 * eps) f(c);
+        }
+    }
+}
+
+__global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
+    DevCtl* ctl = a.ctl;
+    if (ctl->halted != H_RUN) return;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    constexpr int NW = STEP_THREADS / 64;
+    __shared__ Decision D;
+    __shared__ int s_done, s_i, s_fail, s_ndist, s_exact_need, s_nT, s_unc, s_nblm;
+    __shared__ unsigned long long s_u[NW];
+    __shared__ double s_dv[NW], s_dv2[NW], s_dv3[NW];
+    __shared__ int s_bs[NW], s_bt[NW];
+    __shared__ double s_bw[NW];
+    __shared__ double s_g[2];
+    __shared__ unsigned long long s_cand[2];
+    __shared__ uint32_t s_first[NF];
+    __shared__ uint32_t s_flags;
+    __shared__ double s_sux;
+    __shared__ uint32_t s_key[DEDUP_STEP];
+    __shared__ unsigned long long s_wb[DEDUP_STEP], s_it[DEDUP_STEP];
+    __shared__ double s_ld[MAXB];                    // loads (by id) / exact loads in bl order
+    __shared__ unsigned long long s_k64[MAXB];       // sort keys
+    __shared__ int32_t s_ord[MAXB];                  // universe order
+    __shared__ int32_t s_ord2[MAXB];
+    __shared__ uint8_t s_tm[MAXB];                   // touched-broker marks
+    __shared__ int s_T[TMAX];
+    __shared__ int s_cntT[TMAX], s_posT[TMAX];
+    __shared__ uint64_t s_blmb[MAXB / 64], s_presb[MAXB / 64];
+    __shared__ uint32_t s_smark[MAX_SETS / 32];
+    Dedup T{s_key, s_wb, s_it, DEDUP_STEP};
+    const double eps = ctl->eps, inv_avg = ctl->inv_avg, U0h = ctl->U0;
+    const int nblm0 = ctl->nblm;
+    KB_STAMP_BEGIN();
+
+    if (tid == 0) { s_nT = 0; s_done = 0; s_exact_need = 0; }
+    const bool do_res = ctl->prepped && ctl->steps < ctl->budget;
+    __syncthreads();
+
+    // ================================================================ resolve
+    if (do_res) {
+        if (ctl->pending_list) do_list_op(ctl, a.L, &s_i);   // not consumed by a scan: do it here
+        // ---- combine the scan records (or the gathered rank summaries)
+        double d0 = HUGE_VAL, d1 = HUGE_VAL;
+        unsigned long long c0 = 0, c1 = 0;
+        uint32_t f[NF];
 #pragma unroll
-    for (int q = 0; q < NF; q++) f[q] = wave_min(f[q]);
+        for (int q = 0; q < NF; q++) f[q] = NONE32;
+        uint32_t flg = 0;
+        for (int i = tid; i < a.nrec; i += STEP_THREADS) {
+            const RecHdr* h = (const RecHdr*)(a.recs + (size_t)i * a.rec_stride);
+            d0 = h->dmin[0] < d0 ? h->dmin[0] : d0;
+            d1 = h->dmin[1] < d1 ? h->dmin[1] : d1;
+            c0 += h->cand[0]; c1 += h->cand[1];
+#pragma unroll
+            for (int q = 0; q < NF; q++) f[q] = min(f[q], h->first[q]);
+            flg |= h->flags;
+        }
+        d0 = wave_min(d0); d1 = wave_min(d1); c0 = wave_sum(c0); c1 = wave_sum(c1);
+#pragma unroll
+        for (int q = 0; q < NF; q++) f[q] = wave_min(f[q]);
+        for (int o = 32; o > 0; o >>= 1) flg |= __shfl_xor(flg, o);
+        if (lane == 0) { s_dv[wid] = d0; s_dv2[wid] = d1; s_u[wid] = c0; s_bw[wid] = 0; s_bs[wid] = (int)flg; }
+        if (lane == 0) s_bt[wid] = 0;
+        __shared__ unsigned long long s_c1w[NW];
+        __shared__ uint32_t s_fw[NF][NW];
+        if (lane == 0) {
+            s_c1w[wid] = c1;
+#pragma unroll
+            for (int q = 0; q < NF; q++) s_fw[q][wid] = f[q];
+        }
+        __syncthreads();
+        if (tid == 0) {
+            for (int x = 1; x < NW; x++) {
+                d0 = s_dv[x] < d0 ? s_dv[x] : d0;
+                d1 = s_dv2[x] < d1 ? s_dv2[x] : d1;
+                c0 += s_u[x]; c1 += s_c1w[x];
+                flg |= (uint32_t)s_bs[x];
+                for (int q = 0; q < NF; q++) f[q] = min(f[q], s_fw[q][x]);
+            }
+            s_g[0] = d0; s_g[1] = d1; s_cand[0] = c0; s_cand[1] = c1;
+            for (int q = 0; q < NF; q++) s_first[q] = f[q];
+            s_flags = flg | (a.use_spill && ctl->cont_overflow ? 1u : 0u);
+        }
+        __syncthreads();
+        KB_STAMP(ctl, 0);
+
+        // ---- Validate(dup) / RemoveExtra / AddMissing / MoveDisallowed / ReassignLeaders
+        if (tid == 0) {
+            const double su = U0h;
+            D.status = 0; D.step = -1; D.kind = 0; D.slot = -1; D.part = -1;
+            D.from = -1; D.to = -1; D.su = su; D.cu = su; D.exact = 0; D.err = E_NONE; D.err_broker = -1;
+            const uint32_t* F = s_first;
+            auto rd = [&](uint32_t p, int k) -> int { return (int)a.rep[(long long)k * a.Ppad + p]; };
+            if (ctl->list_overflow) {
+                D.status = -1; D.step = 8; D.err = E_LIST_OVERFLOW; s_done = 1;
+            } else if (a.sem_go && F[F_DUP] != NONE32) {
+                D.status = -1; D.step = 1; D.err = E_DUP; D.part = F[F_DUP]; s_done = 1;
+            } else if (F[F_REMOVE] != NONE32) {                      // steps.go:70-89
+                const uint32_t p = F[F_REMOVE];
+                const uint32_t m = a.meta[p];
+                const int nrep = (int)meta_nrep(m), set = (int)meta_set(m);
+                const uint64_t* sb = a.setbits + (size_t)set * a.W64;
+                // lightest allowed replica in (load, id) order = smallest universe position
+                int best = -1, bslot = -1, bpos = 0x7FFFFFFF;
+                for (int k = 0; k < nrep; k++) {
+                    const int b = rd(p, k);
+                    if (!setbit(sb, b)) continue;
+                    const int ps = a.posu[b];
+                    if (ps < bpos) { bpos = ps; best = b; bslot = k; }
+                }
+                D.step = 3; D.part = p;
+                if (best < 0) { D.status = -1; D.err = E_REMOVE; }
+                else {
+                    // replacepl removes the FIRST slot holding that broker (utils.go:167-178)
+                    D.status = 1; D.kind = 2; D.slot = bslot; D.from = best; D.to = -1;
+                }
+                s_done = 1;
+            } else if (F[F_ADD] != NONE32) {                         // steps.go:93-113
+                const uint32_t p = F[F_ADD];
+                const uint32_t m = a.meta[p];
+                const int nrep = (int)meta_nrep(m), set = (int)meta_set(m);
+                const int32_t* dl = a.lists + ((size_t)set * 2 + 1) * a.K;
+                int t = -1;
+                for (int i = 0; i < a.K && t < 0; i++) {
+                    const int b = dl[i];
+                    if (b < 0) break;
+                    bool isrep = false;
+                    for (int k = 0; k < nrep; k++) isrep |= rd(p, k) == b;
+                    if (!isrep) t = b;
+                }
+                D.step = 4; D.part = p;
+                if (t < 0) { D.status = -1; D.err = E_ADD; }
+                else { D.status = 1; D.kind = 3; D.slot = nrep; D.from = -1; D.to = t; }
+                s_done = 1;
+            } else if (F[F_DIS] != NONE32) {                         // steps.go:117-143
+                const uint32_t p = F[F_DIS];
+                const uint32_t m = a.meta[p];
+                const int nrep = (int)meta_nrep(m), set = (int)meta_set(m);
+                const uint64_t* sb = a.setbits + (size_t)set * a.W64;
+                int vslot = -1;
+                for (int k = 0; k < nrep && vslot < 0; k++) if (!setbit(sb, rd(p, k))) vslot = k;
+                const int32_t* dl = a.lists + ((size_t)set * 2 + 0) * a.K;
+                int t = -1;
+                for (int i = 0; i < a.K && t < 0; i++) {
+                    const int b = dl[i];
+                    if (b < 0) break;
+                    bool isrep = false;
+                    for (int k = 0; k < nrep; k++) isrep |= rd(p, k) == b;
+                    if (!isrep) t = b;
+                }
+                D.step = 5; D.part = p; D.slot = vslot; D.from = rd(p, vslot);
+                if (t < 0) { D.status = -1; D.err = E_DIS; D.err_broker = D.from; }
+                else { D.status = 1; D.kind = 1; D.to = t; }
+                s_done = 1;
+            } else if (a.rebalance) {                                 // steps.go:234-282
+                // su < MinUnbalance decides; certify it against eps or ask for exact loads
+                const bool lo = su + 2.0 * eps < a.min_unbalance, hi = su - 2.0 * eps >= a.min_unbalance;
+                if (!lo && !hi) {
+                    if (!a.integral && ctl->ndirty > 0) s_exact_need = 1;
+                    else s_exact_need = 2;       // exact su decides (below)
+                } else if (hi) {
+                    if (F[F_EMPTY] != NONE32 || nblm0 == 0) {
+                        D.status = -1; D.step = 6; D.err = E_PANIC; D.part = F[F_EMPTY]; s_done = 1;
+                    } else if (F[F_LEAD] != NONE32) {
+                        const uint32_t p = F[F_LEAD];
+                        const int nrep = (int)meta_nrep(a.meta[p]);
+                        const int light = ctl->light;
+                        int ex = -1;
+                        for (int k = 0; k < nrep && ex < 0; k++) if (rd(p, k) == light) ex = k;
+                        D.status = 1; D.step = 6; D.part = p; D.slot = 0; D.from = rd(p, 0); D.to = light;
+                        D.kind = ex >= 0 ? 4 : 1;       // swap when bl[0] is already a replica
+                        s_done = 1;
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        // exact su (sequential folds in bl order) when a decision needs it
+        auto exact_su = [&]() {
+            for (int k = tid; k < nblm0; k += STEP_THREADS) s_ld[k] = a.load[a.blm[k]];
+            __syncthreads();
+            if (tid == 0) {
+                const double S = fold_lds(s_ld, nblm0);
+                const double avg = S / (double)nblm0;
+                double U = 0.0;
+                for (int k = 0; k < nblm0; k++) U += term_x(s_ld[k], avg);
+                s_sux = U;
+                atomicAdd(&ctl->total_folds, 1ull);
+            }
+            __syncthreads();
+        };
+        if (s_exact_need == 2) {
+            // ReassignLeaders on the exact su (utils-folds, integral or clean loads)
+            exact_su();
+            if (tid == 0) {
+                s_exact_need = 0;
+                const uint32_t* F = s_first;
+                if (!(s_sux < a.min_unbalance)) {
+                    auto rd = [&](uint32_t p, int k) -> int { return (int)a.rep[(long long)k * a.Ppad + p]; };
+                    if (F[F_EMPTY] != NONE32 || nblm0 == 0) {
+                        D.status = -1; D.step = 6; D.err = E_PANIC; D.part = F[F_EMPTY]; s_done = 1;
+                    } else if (F[F_LEAD] != NONE32) {
+                        const uint32_t p = F[F_LEAD];
+                        const int nrep = (int)meta_nrep(a.meta[p]);
+                        const int light = ctl->light;
+                        int ex = -1;
+                        for (int k = 0; k < nrep && ex < 0; k++) if (rd(p, k) == light) ex = k;
+                        D.status = 1; D.step = 6; D.part = p; D.slot = 0; D.from = rd(p, 0); D.to = light;
+                        D.kind = ex >= 0 ? 4 : 1;
+                        s_done = 1;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+        KB_STAMP(ctl, 1);
+
+        // ---- move(): leader step (if allowed), then non-leader step (steps.go:284-298)
+        for (int kind = a.allow_leader ? 0 : 1; kind < 2 && !s_done && !s_exact_need; kind++) {
+            const int step = kind == 0 ? 7 : 8;
+            const double g = s_g[kind];
+            if (tid == 0) {
+                if (s_first[F_EMPTY_ELIG] != NONE32) {
+                    D.status = -1; D.step = step; D.err = E_PANIC; D.part = s_first[F_EMPTY_ELIG]; s_done = 1;
+                } else if (s_flags & 1u) {
+                    D.status = -1; D.step = step; D.err = E_CONT_OVERFLOW; s_done = 1;
+                }
+                s_fail = 0;
+                s_ndist = 0;
+            }
+            dedup_clear(T);
+            __syncthreads();
+            if (s_done) break;
+            // (1) distinct keys of this kind (earliest iteration index per key)
+            if (g < HUGE_VAL)
+                for_each_contender(a, kind, g, eps, inv_avg, [&](const Contender& c) {
+                    if (dedup_insert(T, c.kind, c.s, c.t, c.w, c.iter) < 0) s_fail = 1;
+                });
+            __syncthreads();
+            int nd = 0;
+            for (int h = tid; h < DEDUP_STEP; h += STEP_THREADS) nd += s_key[h] != NONE32 ? 1 : 0;
+            nd = wave_sum(nd);
+            if (lane == 0 && nd) atomicAdd(&s_ndist, nd);
+            __syncthreads();
+            const int ndist = s_ndist;
+            const bool fail = s_fail != 0;
+            const bool have = ndist > 0 || fail;
+            // (2) certified decision for one key; exact folds otherwise
+            double Ua = 0.0;
+            Contender cw;
+            cw.s = cw.t = -1; cw.w = 0; cw.iter = NONE64; cw.kind = kind; cw.pad = 0;
+            bool certain = false, c_improved = false, c_take = false;
+            if (!fail && ndist == 1) {
+                if (tid == 0) s_i = -1;
+                __syncthreads();
+                for (int h = tid; h < DEDUP_STEP; h += STEP_THREADS) if (s_key[h] != NONE32) s_i = h;
+                __syncthreads();
+                cw = dedup_entry(T, s_i);
+                Ua = U0h + cont_delta(a.r, cw, inv_avg);
+                // |Ua - U'| <= eps and |U0h - su| <= eps; margins of 3*eps on both decisions
+                const double thr = U0h - a.min_unbalance;
+                const double rel = 4.0 * DBL_EPSILON * fabs(thr);
+                const bool imp_t = Ua + 3.0 * eps < U0h, imp_f = Ua - 3.0 * eps >= U0h;
+                const bool take_t = Ua + 3.0 * eps + rel < thr, take_f = Ua - 3.0 * eps - rel >= thr;
+                certain = (imp_t || imp_f) && (take_t || take_f) && !a.exact_unb;
+                c_improved = imp_t;
+                c_take = take_t;
+            } else if (!have) {
+                // no candidate: cu = su; the decision is su < su - MinUnbalance
+                const bool t_t = a.min_unbalance < 0.0, t_f = a.min_unbalance >= 0.0;
+                certain = (t_t || t_f) && !a.exact_unb;
+                c_improved = false;
+                c_take = t_t;
+            }
+            if (!certain && !a.integral && ctl->ndirty > 0) {
+                if (tid == 0) { s_exact_need = 1; }
+                __syncthreads();
+                break;
+            }
+            double Ustar = U0h, sux = U0h;
+            unsigned long long witer = NONE64;
+            int exact = 0;
+            bool improved = false, take = false;
+            if (certain) {
+                improved = c_improved;
+                take = c_take;
+                Ustar = Ua;
+                witer = cw.iter;
+            } else {
+                exact = 1;
+                exact_su();                      // also stages the exact loads in bl order
+                sux = s_sux;
+                if (!fail && ndist == 1) {
+                    if (tid == 0) {
+                        s_dv[0] = exact_unbalance_lds(s_ld, nblm0, a.posm[cw.s], a.posm[cw.t],
+                                                      a.load[cw.s] - cw.w, a.load[cw.t] + cw.w);
+                        atomicAdd(&ctl->total_folds, 1ull);
+                    }
+                    __syncthreads();
+                    Ustar = s_dv[0];
+                    witer = cw.iter;
+                } else if (have) {
+                    // several keys (or an overfull table): exact sequential folds, lexicographic min
+                    double bu = HUGE_VAL;
+                    unsigned long long bi = NONE64;
+                    int bs = -1, bt = -1;
+                    double bw = 0.0;
+                    unsigned long long nf = 0;
+                    auto consider = [&](const Contender& c) {
+                        const double u = exact_unbalance_lds(s_ld, nblm0, a.posm[c.s], a.posm[c.t],
+                                                             a.load[c.s] - c.w, a.load[c.t] + c.w);
+                        nf++;
+                        if (u < bu || (u == bu && c.iter < bi)) { bu = u; bi = c.iter; bs = c.s; bt = c.t; bw = c.w; }
+                    };
+                    if (!fail) {
+                        for (int h = tid; h < DEDUP_STEP; h += STEP_THREADS)
+                            if (s_key[h] != NONE32) consider(dedup_entry(T, h));
+                    } else {
+                        for_each_contender(a, kind, g, eps, inv_avg, consider);
+                    }
+                    nf = wave_sum(nf);
+                    if (lane == 0 && nf) atomicAdd(&ctl->total_folds, nf);
+                    for (int o = 32; o > 0; o >>= 1) {
+                        const double ou = __shfl_xor(bu, o);
+                        const unsigned long long oi = __shfl_xor(bi, o);
+                        const int os = __shfl_xor(bs, o), ot = __shfl_xor(bt, o);
+                        const double ow = __shfl_xor(bw, o);
+                        if (ou < bu || (ou == bu && oi < bi)) { bu = ou; bi = oi; bs = os; bt = ot; bw = ow; }
+                    }
+                    __syncthreads();
+                    if (lane == 0) { s_dv[wid] = bu; s_u[wid] = bi; s_bs[wid] = bs; s_bt[wid] = bt; s_bw[wid] = bw; }
+                    __syncthreads();
+                    if (tid == 0) {
+                        for (int q = 1; q < NW; q++)
+                            if (s_dv[q] < s_dv[0] || (s_dv[q] == s_dv[0] && s_u[q] < s_u[0])) {
+                                s_dv[0] = s_dv[q]; s_u[0] = s_u[q]; s_bs[0] = s_bs[q]; s_bt[0] = s_bt[q]; s_bw[0] = s_bw[q];
+                            }
+                    }
+                    __syncthreads();
+                    Ustar = s_dv[0]; witer = s_u[0];
+                    cw.s = s_bs[0]; cw.t = s_bt[0]; cw.w = s_bw[0]; cw.iter = witer;
+                }
+                // cu starts at su and only a strictly smaller u replaces it (steps.go:163,211)
+                improved = have && Ustar < sux;
+                const double cu = improved ? Ustar : sux;
+                take = cu < sux - a.min_unbalance;
+            }
+            __syncthreads();
+            if (tid == 0) {
+                if (take) {
+                    if (!improved) {
+                        // replacepl on the zero Partition: the reference panics
+                        D.status = -1; D.step = step; D.err = E_PANIC; s_done = 1;
+                    } else {
+                        D.status = 1; D.step = step; D.kind = 1;
+                        D.part = (long long)(witer >> 21); D.slot = (int)((witer >> 16) & 31);
+                        D.from = cw.s; D.to = cw.t; D.su = sux; D.cu = Ustar; D.exact = exact;
+                        s_done = 1;
+                    }
+                } else {
+                    D.su = sux; D.cu = sux; D.exact = exact;
+                }
+            }
+            __syncthreads();
+        }
+        KB_STAMP(ctl, 2);
+
+        if (s_exact_need) {
+            // the bounds cannot decide and some loads are approximate: refold first
+            if (tid == 0) {
+                ctl->halted = H_NEED_EXACT;
+                ctl->prepped = 0;
+                ctl->total_exact_halts++;
+            }
+            return;
+        }
+
+        // ---------------------------------------------------------- apply
+        __shared__ int s_aff[2 * MAXR + 2];
+        __shared__ double s_oldc[2 * MAXR + 2];
+        __shared__ int s_naff;
+        if (tid == 0) {
+            s_naff = 0;
+            if (D.status == 1) {
+                const long long p = D.part;
+                const uint32_t m = a.meta[p];
+                const int nrep = (int)meta_nrep(m);
+                int r[MAXR + 1];
+                for (int k = 0; k < nrep; k++) r[k] = (int)a.rep[(long long)k * a.Ppad + p];
+                const double wv = a.w[p];
+                const int ncp = a.nc[p];
+                for (int k = 0; k < nrep; k++) {             // old contributions of p's brokers
+                    s_aff[s_naff] = r[k];
+                    s_oldc[s_naff] = k == 0 ? wv * (double)(nrep + ncp) : wv;
+                    s_naff++;
+                }
+                int nn = nrep;
+                bool state_changed = true;
+                if (D.kind == 1) {                           // replace at slot (utils.go:186-190)
+                    r[D.slot] = D.to;
+                } else if (D.kind == 4) {                    // swap with the existing replica (utils.go:179-185)
+                    int ex = 0;
+                    for (int k = 0; k < nrep; k++) if (r[k] == D.to) { ex = k; break; }
+                    const int old = r[D.slot];
+                    r[D.slot] = D.to;
+                    r[ex] = old;
+                } else if (D.kind == 2) {                    // remove (utils.go:176-178)
+                    for (int k = D.slot; k + 1 < nrep; k++) r[k] = r[k + 1];
+                    if (a.sem_go) state_changed = false;     // pl keeps its length: duplicates
+                    else nn = nrep - 1;
+                } else if (D.kind == 3) {                    // add (utils.go:199-202)
+                    if (a.sem_go) state_changed = false;     // the append is not visible through pl
+                    else { r[nrep] = D.to; nn = nrep + 1; }
+                }
+                // the meta bits that depend on the replicas (Disallowed trigger, in-set count)
+                const uint64_t* sb = a.setbits + (size_t)meta_set(m) * a.W64;
+                auto remeta = [&](int n) {
+                    uint32_t dis = 0, nin = 0;
+                    for (int k = 0; k < n; k++) { const bool in = setbit(sb, r[k]); dis |= in ? 0u : 1u; nin += in ? 1u : 0u; }
+                    return make_meta((uint32_t)n, meta_want(m), meta_elig(m), dis, nin, meta_set(m));
+                };
+                if (a.sem_go && (D.kind == 2 || D.kind == 3)) {
+                    // Go aliasing: the remove shifted the shared backing array in place
+                    if (D.kind == 2) {
+                        for (int k = 0; k < nrep; k++) a.rep[(long long)k * a.Ppad + p] = (uint16_t)r[k];
+                        a.meta[p] = remeta(nrep);
+                    }
+                    s_naff = 0;
+                } else if (state_changed) {
+                    for (int k = 0; k < nn; k++) a.rep[(long long)k * a.Ppad + p] = (uint16_t)r[k];
+                    a.meta[p] = remeta(nn);
+                    if (D.kind == 1) { a.cnt[D.from]--; a.cnt[D.to]++; }
+                    if (D.kind == 2) { a.cnt[D.from]--; }
+                    if (D.kind == 3) { a.cnt[D.to]++; }
+                    // new contributions: exact +- in integral mode, bounded increments otherwise
+                    const double u = DBL_EPSILON / 2;
+                    auto upd = [&](int b, double oldc, double newc) {
+                        const double L = a.load[b];
+                        if (a.integral) { a.load[b] = (L - oldc) + newc; return; }
+                        const double x1 = L - oldc;
+                        double x2 = x1 + newc;
+                        double e = a.lerr[b] + 1.01 * u * (fabs(x1) + fabs(x2));
+                        if (!(x2 > 0.0)) x2 = 0.0;           // loads are sums of non-negative terms
+                        if (a.cnt[b] == 0) { x2 = 0.0; e = 0.0; }   // empty fold: exactly 0
+                        a.load[b] = x2;
+                        a.lerr[b] = e;
+                        const uint8_t dn = a.cnt[b] > 0 ? 1 : 0;
+                        if (dn != a.dirty[b]) ctl->ndirty += dn ? 1 : -1;
+                        a.dirty[b] = dn;
+                    };
+                    const int base_aff = s_naff;
+                    for (int k = 0; k < nn; k++) {
+                        const int b = r[k];
+                        const double cc = k == 0 ? wv * (double)(nn + ncp) : wv;
+                        int f2 = -1;
+                        for (int x = 0; x < base_aff; x++) if (s_aff[x] == b) f2 = x;
+                        if (f2 >= 0) {
+                            if (s_oldc[f2] == cc) { s_aff[f2] = -1 - s_aff[f2]; }  // unchanged contribution
+                            else upd(b, s_oldc[f2], cc);
+                        } else {
+                            upd(b, 0.0, cc);
+                            s_aff[s_naff] = b; s_oldc[s_naff] = 0.0; s_naff++;
+                        }
+                    }
+                    for (int x = 0; x < base_aff; x++) {
+                        const int b = s_aff[x];
+                        if (b < 0) continue;
+                        bool still = false;
+                        for (int k = 0; k < nn; k++) still |= r[k] == b;
+                        if (!still) upd(b, s_oldc[x], 0.0);
+                    }
+                    int n2 = 0;                              // brokers whose contribution changed
+                    for (int x = 0; x < s_naff; x++) if (s_aff[x] >= 0) s_aff[n2++] = s_aff[x];
+                    s_naff = n2;
+                    // the per-broker partition lists follow in the next scan (k_scan's list workgroup)
+                    if (!a.integral && (D.kind == 1 || D.kind == 2 || D.kind == 3)) {
+                        ctl->pl_kind = D.kind; ctl->pl_from = D.from; ctl->pl_to = D.to; ctl->pl_part = p;
+                        ctl->pending_list = 1;
+                    }
+                } else {
+                    s_naff = 0;
+                }
+            }
+            for (int x = 0; x < s_naff && x < TMAX; x++) s_T[x] = s_aff[x];
+            s_nT = s_naff < TMAX ? s_naff : TMAX;
+            // log the step
+            ChangeDev ch;
+            ch.status = D.status; ch.step = D.step; ch.kind = D.kind; ch.slot = D.slot;
+            ch.part = D.part; ch.from = D.from; ch.to = D.to; ch.su = D.su; ch.cu = D.cu;
+            ch.exact = D.exact; ch.err_code = D.err; ch.err_broker = D.err_broker; ch.pad = 0;
+            if (ctl->logpos < ctl->logcap) a.log[ctl->logpos] = ch;
+            ctl->logpos++;
+            ctl->steps++;
+            // reference candidate count of the steps that actually ran this iteration
+            unsigned long long add = 0;
+            if (D.step < 0 || D.step >= 7) {
+                if (a.allow_leader) add += s_cand[0];
+                if (D.step != 7) add += s_cand[1];
+            }
+            ctl->total_cand += add;
+            ctl->total_cont += (unsigned long long)s_ndist;
+            ctl->ncont = 0;
+            ctl->cont_overflow = 0;
+            if (D.status != 1) { ctl->halted = H_DONE; ctl->prepped = 0; }
+        }
+        __syncthreads();
+        if (ctl->halted != H_RUN) return;
+        KB_STAMP(ctl, 3);
+    }
+
+    // ================================================================== prep
+    // (next step): getBL's (load, id) order, bl_move, relative loads, eps, sets
+    const int B = a.B;
+    const bool full = ctl->full_prep != 0;
+    for (int b = tid; b < B; b += STEP_THREADS) s_ld[b] = a.load[b];
+    if (full) {
+        const int NP2 = a.NP2;
+        for (int i = tid; i < NP2; i += STEP_THREADS) {
+            s_k64[i] = i < B ? d2u(a.load[i]) : NONE64;
+            s_ord[i] = i < B ? i : 0x7FFFFFFF;
+        }
+        __syncthreads();
+        // bitonic sort by (load bits, dense id); loads are finite and >= 0, so the
+        // IEEE bit pattern orders like the value (byBrokerLoad.Less, utils.go:23-28)
+        for (int k = 2; k <= NP2; k <<= 1) {
+            for (int j = k >> 1; j > 0; j >>= 1) {
+                for (int i = tid; i < NP2; i += STEP_THREADS) {
+                    int ixj = i ^ j;
+                    if (ixj > i) {
+                        unsigned long long ki = s_k64[i], kj = s_k64[ixj];
+                        int32_t ii = s_ord[i], ij = s_ord[ixj];
+                        bool less = (kj < ki) || (kj == ki && ij < ii);
+                        bool up = (i & k) == 0;
+                        if (up == less) { s_k64[i] = kj; s_k64[ixj] = ki; s_ord[i] = ij; s_ord[ixj] = ii; }
+                    }
+                }
+                __syncthreads();
+            }
+        }
+    } else {
+        // incremental: only the touched brokers moved (their loads changed)
+        const int nT = s_nT;
+        for (int b = tid; b < B; b += STEP_THREADS) s_tm[b] = 0;
+        if (tid < TMAX) s_cntT[tid] = 0;
+        __syncthreads();
+        if (tid < nT) { s_tm[s_T[tid]] = 1; s_posT[tid] = a.posu[s_T[tid]]; }
+        for (int i = tid; i < B; i += STEP_THREADS) s_ord2[i] = a.order[i];
+        __syncthreads();
+        if (nT == 0) {
+            for (int i = tid; i < B; i += STEP_THREADS) s_ord[i] = s_ord2[i];
+        } else {
+            // per untouched element: new position = old - (touched before it) + (touched keys below it)
+            for (int i0 = 0; i0 < B; i0 += STEP_THREADS) {
+                const int i = i0 + tid;
+                const bool in = i < B;
+                const int b = in ? s_ord2[i] : 0;
+                const bool untouched = in && !s_tm[b];
+                const double Lb = in ? s_ld[b] : 0.0;
+                int below = 0, before = 0;
+                for (int x = 0; x < nT; x++) {
+                    const int t = s_T[x];
+                    const double Lt = s_ld[t];
+                    const bool t_lt_b = (Lt < Lb) || (Lt == Lb && t < b);
+                    below += t_lt_b ? 1 : 0;
+                    before += s_posT[x] < i ? 1 : 0;
+                    // count, for touched t, the untouched brokers below it
+                    const bool b_lt_t = untouched && ((Lb < Lt) || (Lb == Lt && b < t));
+                    const unsigned long long bal = __ballot(b_lt_t);
+                    if (lane == 0 && bal) atomicAdd(&s_cntT[x], (int)__popcll(bal));
+                }
+                if (untouched) s_ord[i - before + below] = b;
+            }
+            __syncthreads();
+            if (tid < nT) {
+                const int t = s_T[tid];
+                const double Lt = s_ld[t];
+                int rank = 0;
+                for (int x = 0; x < nT; x++) {
+                    const int t2 = s_T[x];
+                    const double L2 = s_ld[t2];
+                    rank += ((L2 < Lt) || (L2 == Lt && t2 < t)) ? 1 : 0;
+                }
+                s_ord[s_cntT[tid] + rank] = t;
+            }
+        }
+    }
+    __syncthreads();
+    for (int i = tid; i < B; i += STEP_THREADS) { const int b = s_ord[i]; a.order[i] = b; a.posu[b] = i; }
+    // bl_move = brokers present in the load map or listed in -broker-ids (steps.go:150-157)
+    for (int w = tid; w < MAXB / 64; w += STEP_THREADS) { s_blmb[w] = 0; s_presb[w] = 0; }
+    __syncthreads();
+    {
+        int flag[4], c = 0;
+        const int base = tid * 4;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const int i = base + q;
+            flag[q] = 0;
+            if (i < B) {
+                const int b = s_ord[i];
+                const bool pres = a.cnt[b] > 0;
+                flag[q] = (pres || a.incfg[b]) ? 1 : 0;
+                if (flag[q]) atomicOr((unsigned long long*)&s_blmb[b >> 6], 1ull << (b & 63));
+                if (pres) atomicOr((unsigned long long*)&s_presb[b >> 6], 1ull << (b & 63));
+                c += flag[q];
+            }
+        }
+        int incl = c;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) { int y = __shfl_up(incl, o); if (lane >= o) incl += y; }
+        __shared__ int s_wcnt[NW];
+        if (lane == 63) s_wcnt[wid] = incl;
+        __syncthreads();
+        int woff = 0, total = 0;
+        for (int x = 0; x < NW; x++) { if (x < wid) woff += s_wcnt[x]; total += s_wcnt[x]; }
+        int pos = woff + incl - c;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const int i = base + q;
+            if (i < B) {
+                const int b = s_ord[i];
+                if (flag[q]) { a.blm[pos] = b; a.posm[b] = pos; pos++; }
+                else a.posm[b] = -1;
+            }
+        }
+        if (tid == 0) s_nblm = total;
+    }
+    __syncthreads();
+    const int nblm = s_nblm;
+    KB_STAMP(ctl, 4);
+    // order certification: with approximate loads, neighbours must be separated
+    // by more than their error bounds (else the exact order is unknown)
+    if (tid == 0) s_unc = 0;
+    __syncthreads();
+    if (!a.integral && ctl->ndirty > 0) {
+        for (int i = tid; i + 1 < B; i += STEP_THREADS) {
+            const int b1 = s_ord[i], b2 = s_ord[i + 1];
+            const double e = load_err(a.load, a.lerr, a.dirty, a.cnt, b1) + load_err(a.load, a.lerr, a.dirty, a.cnt, b2);
+            if (e > 0.0 && !(s_ld[b2] - s_ld[b1] > e)) s_unc = 1;
+        }
+    }
+    __syncthreads();
+    if (s_unc) {
+        if (tid == 0) { ctl->halted = H_NEED_EXACT; ctl->prepped = 0; ctl->total_exact_halts++; }
+        return;
+    }
+    // approximate S (exact in integral mode: integers below 2^52), total load error E
+    double sS = 0.0, sE = 0.0;
+    for (int k = tid; k < nblm; k += STEP_THREADS) {
+        const int b = a.blm[k];
+        sS += s_ld[b];
+        if (!a.integral) sE += load_err(a.load, a.lerr, a.dirty, a.cnt, b);
+    }
+    sS = wave_sum(sS); sE = wave_sum(sE);
+    if (lane == 0) { s_dv[wid] = sS; s_dv2[wid] = sE; }
+    __syncthreads();
+    double S = 0.0, E = 0.0;
+    for (int x = 0; x < NW; x++) { S += s_dv[x]; E += s_dv2[x]; }
+    __syncthreads();
+    const double avg = S / (double)nblm;
+    const double iav = 1.0 / avg;
+    double su = 0.0, v = 0.0, rm = 0.0;
+    for (int b = tid; b < B; b += STEP_THREADS) {
+        double r = 0.0;
+        if (a.posm[b] >= 0) {
+            r = __fma_rn(s_ld[b], iav, -1.0);
+            su += fsq(r);
+            const double ar = fabs(r);
+            v += ar * (1.0 + ar);
+            rm = ar > rm ? ar : rm;
+        }
+        a.r[b] = r;
+    }
+    su = wave_sum(su); v = wave_sum(v); rm = wave_max(rm);
+    if (lane == 0) { s_dv[wid] = su; s_dv2[wid] = v; s_dv3[wid] = rm; }
+    __syncthreads();
+    if (tid == 0) {
+        double U0 = 0.0, V = 0.0, Rm = 0.0;
+        for (int x = 0; x < NW; x++) { U0 += s_dv[x]; V += s_dv2[x]; Rm = s_dv3[x] > Rm ? s_dv3[x] : Rm; }
+        const double u = DBL_EPSILON / 2;
+        const double n = (double)nblm;
+        const double R = Rm + a.wmax * iav;
+        const double Ea = E * iav;
+        double epsf = 64.0 * u * ((n + 8.0) * (U0 + 2.0 * V) + 4.0 * (1.0 + R) * (1.0 + R));
+        double epsl = 16.0 * Ea * (V / (n > 0 ? n : 1.0) + R + 1.0) + 4.0 * Ea * Ea;
+        double ep = epsf + epsl;
+        if (!(ep > 1e-300)) ep = 1e-300;
+        ctl->S = S; ctl->avg = avg; ctl->inv_avg = iav; ctl->U0 = U0;
+        ctl->V = V; ctl->eps = ep; ctl->E = E; ctl->nblm = nblm;
+        ctl->heavy = nblm > 0 ? a.blm[nblm - 1] : -1;
+        ctl->light = nblm > 0 ? a.blm[0] : -1;
+        ctl->want_refresh = (epsl > epsf || ctl->ndirty >= 256) ? 1 : 0;
+    }
+    KB_STAMP(ctl, 5);
+    // ---- set records: full, or the sets containing a touched broker
+    for (int w = tid; w < (a.nsets + 31) / 32; w += STEP_THREADS) s_smark[w] = full ? 0xFFFFFFFFu : 0u;
+    __syncthreads();
+    if (!full) {
+        for (int x = 0; x < s_nT; x++) {
+            const int t = s_T[x];
+            for (int j = a.bset_off[t] + tid; j < a.bset_off[t + 1]; j += STEP_THREADS) {
+                const int s = a.bset_ids[j];
+                atomicOr(&s_smark[s >> 5], 1u << (s & 31));
+            }
+        }
+    }
+    __syncthreads();
+    {
+        const unsigned long long lt = (1ull << lane) - 1ull;
+        const int K = a.K, KR = a.KR;
+        for (int set = wid; set < a.nsets; set += NW) {
+            if (!((s_smark[set >> 5] >> (set & 31)) & 1u)) continue;
+            const uint64_t sbw = lane < a.W64 ? a.setbits[(size_t)set * a.W64 + lane] : 0ull;
+            auto inset = [&](int b) -> bool {
+                const unsigned long long wv = __shfl(sbw, b >> 6);
+                return (wv >> (b & 63)) & 1ull;
+            };
+            uint16_t* rec16 = (uint16_t*)(a.setrec + (size_t)set * a.units);
+            // kind 0: first KR of set ∩ bl_move ascending; 1: last K of set ∩ present; 2: last K of set
+            for (int kind = 0; kind < 3; kind++) {
+                const int cap = kind == 0 ? KR : K;
+                int found = 0;
+                for (int base = 0; base < B && found < cap; base += 64) {
+                    const int k = base + lane;
+                    const int b = k < B ? s_ord[kind == 0 ? k : B - 1 - k] : 0;
+                    bool mem = inset(b) && k < B;
+                    if (kind == 0) mem = mem && ((s_blmb[b >> 6] >> (b & 63)) & 1ull);
+                    else if (kind == 1) mem = mem && ((s_presb[b >> 6] >> (b & 63)) & 1ull);
+                    const unsigned long long m = __ballot(mem);
+                    if (mem) {
+                        const int rk = found + (int)__popcll(m & lt);
+                        if (rk < cap) {
+                            if (kind == 0) rec16[2 + rk] = (uint16_t)b;
+                            else a.lists[((size_t)set * 2 + (kind - 1)) * K + rk] = b;
+                        }
+                    }
+                    found += (int)__popcll(m);
+                }
+                for (int rk = found + lane; rk < cap; rk += 64) {
+                    if (kind == 0) rec16[2 + rk] = NONE16;
+                    else a.lists[((size_t)set * 2 + (kind - 1)) * K + rk] = -1;
+                }
+                if (kind == 0 && lane == 0) rec16[1] = (uint16_t)(found < cap ? found : cap);
+            }
+            int n = lane < a.W64 ? (int)__popcll(sbw & s_blmb[lane]) : 0;
+            n = wave_sum(n);
+            if (lane == 0) rec16[0] = (uint16_t)n;
+        }
+    }
+    if (tid == 0) { ctl->prepped = 1; ctl->full_prep = 0; }
+    KB_STAMP(ctl, 6);
+}
+
+// ------------------------------------------------------------- k_listop
+
+__global__ __launch_bounds__(1024) void k_listop(DevCtl* ctl, Lists L) {
+    __shared__ int s_i;
+    do_list_op(ctl, L, &s_i);
+}
+
+// ------------------------------------------------------------ k_refresh
+// exact partition-ordered refold (getBrokerLoad, utils.go:92-105) of every
+// dirty broker: one workgroup per broker; contributions staged in LDS chunks,
+// folded sequentially by one lane.
+
+constexpr int REFRESH_THREADS = 256;
+constexpr int REFRESH_CHUNK = 4096;
+
+__global__ __launch_bounds__(REFRESH_THREADS) void k_refresh(RefreshArgs a) {
+    const int b = blockIdx.x;
+    if (b >= a.B || !a.dirty[b]) return;
+    __shared__ double s_c[REFRESH_CHUNK];
+    const uint32_t st = a.L.lstart[b], n = a.L.llen[b];
+    double acc = 0.0;
+    for (uint32_t c0 = 0; c0 < n; c0 += REFRESH_CHUNK) {
+        const uint32_t m = n - c0 < (uint32_t)REFRESH_CHUNK ? n - c0 : (uint32_t)REFRESH_CHUNK;
+        for (uint32_t i = threadIdx.x; i < m; i += REFRESH_THREADS) {
+            const uint32_t q = a.L.lent[st + c0 + i];
+            const uint32_t mq = a.meta[q];
+            const double w = a.w[q];
+            // slot 0 carries the leader weight W * (len(R) + NumConsumers)
+            s_c[i] = (a.rep[q] == (uint16_t)b) ? w * (double)((int)meta_nrep(mq) + a.nc[q]) : w;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) acc = fold_lds(s_c, (int)m, acc);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        a.load[b] = acc;
+        a.lerr[b] = gamma_n((int)n) * acc;
+        a.dirty[b] = 0;
+    }
+}
+
+// --------------------------------------------------- multi-GPU summaries
+
+// pack this rank's scan result + its distinct near-tie keys (within 4*eps of the
+// rank's minimum, a superset of those within 4*eps of the global one)
+__global__ __launch_bounds__(1024) void k_summary(SumArgs a) {
+    DevCtl* ctl = a.ctl;
+    RecHdr* out = (RecHdr*)a.out;
+    Contender* okeys = (Contender*)(out + 1);
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    __shared__ uint32_t s_key[DEDUP_STEP];
+    __shared__ unsigned long long s_wb[DEDUP_STEP], s_it[DEDUP_STEP];
+    __shared__ uint32_t s_n, s_fail;
     __shared__ double s_d[2][16];
     __shared__ unsigned long long s_c[2][16];
     __shared__ uint32_t s_f[NF][16];
+    __shared__ double s_g[2];
+    Dedup T{s_key, s_wb, s_it, DEDUP_STEP};
+    dedup_clear(T);
+    if (tid == 0) { s_n = 0; s_fail = 0; }
+    const bool ran = ctl->halted == H_RUN && ctl->prepped;
+    double d0 = HUGE_VAL, d1 = HUGE_VAL;
+    unsigned long long c0 = 0, c1 = 0;
+    uint32_t f[NF];
+    for (int q = 0; q < NF; q++) f[q] = NONE32;
+    if (ran)
+        for (int i = tid; i < a.nrec; i += 1024) {
+            const RecHdr* h = (const RecHdr*)(a.recs + (size_t)i * WGREC_BYTES);
+            d0 = h->dmin[0] < d0 ? h->dmin[0] : d0;
+            d1 = h->dmin[1] < d1 ? h->dmin[1] : d1;
+            c0 += h->cand[0]; c1 += h->cand[1];
+            for (int q = 0; q < NF; q++) f[q] = min(f[q], h->first[q]);
+        }
+    d0 = wave_min(d0); d1 = wave_min(d1); c0 = wave_sum(c0); c1 = wave_sum(c1);
+    for (int q = 0; q < NF; q++) f[q] = wave_min(f[q]);
     if (lane == 0) {
         s_d[0][wid] = d0; s_d[1][wid] = d1; s_c[0][wid] = c0; s_c[1][wid] = c1;
-#pragma unroll
         for (int q = 0; q < NF; q++) s_f[q][wid] = f[q];
     }
     __syncthreads();
@@ -574,730 +1449,94 @@ __global__ __launch_bounds__(1024) void k_reduce(ReduceArgs a) {
             c0 += s_c[0][x]; c1 += s_c[1][x];
             for (int q = 0; q < NF; q++) f[q] = min(f[q], s_f[q][x]);
         }
-        ctl->gmin[0] = d0 < HUGE_VAL ? enc(d0) : NONE64;
-        ctl->gmin[1] = d1 < HUGE_VAL ? enc(d1) : NONE64;
-        ctl->ncand[0] = c0; ctl->ncand[1] = c1;
-        for (int q = 0; q < NF; q++) ctl->first[q] = f[q];
-    }
-}
-
-// ------------------------------------------------------------- k_census
-
-__device__ __forceinline__ void emit_global(const ScanArgs& a, const Contender& c) {
-    uint32_t i = atomicAdd(&a.ctl->ncont, 1u);
-    if (i < a.cont_cap) a.cont[i] = c;
-    else a.ctl->cont_overflow = 1;
-}
-
-__device__ __forceinline__ void emit(const ScanArgs& a, const Dedup& T, int kind, int s, int t, double w,
-                                     unsigned long long iter) {
-    if (dedup_insert(T, kind, s, t, w, iter) < 0) {   // table full or weight conflict: keep it raw
-        Contender c;
-        c.s = s; c.t = t; c.w = w; c.iter = iter; c.kind = kind; c.pad = 0;
-        emit_global(a, c);
-    }
-}
-
-// walk every allowed, non-replica target in bl_move order for one (partition, slot)
-// and emit the ones within 4*eps of the minimum; stop once 8*eps is exceeded
-// (the approximate delta is monotone in the target load up to 2*eps).
-template <int RC>
-__device__ void walk_targets(const ScanArgs& a, const Dedup& T, int kind, long long p, int slot, int src,
-                             const uint32_t (&reps)[RC], int nrep, int set, double w, double ds,
-                             double g, double eps, int nblm, double inv_avg) {
-    const unsigned long long ib = ((unsigned long long)p << 21) | ((unsigned long long)slot << 16);
-    const double delta = w * inv_avg;
-    const unsigned char* rec = a.setrec + (size_t)set * a.stride;
-    const int32_t* ids = (const int32_t*)(rec + sr_ids_off());
-    const double* rr = (const double*)(rec + sr_r_off(a.K));
-    const int nl = ((const int32_t*)rec)[1];
-    int start = 0;
-    for (int i = 0; i < nl; i++) {                // the set's first K eligible brokers
-        const int b = ids[i];
-        start = a.posm[b] + 1;
-        bool isrep = false;
-#pragma unroll
-        for (int q = 0; q < RC; q++) isrep |= (q < nrep) && ((int)reps[q] == b);
-        if (isrep) continue;
-        const double d = ds + dtgt(rr[i], delta);
-        if (d <= g + 4.0 * eps) emit(a, T, kind, src, b, w, ib | (unsigned long long)(start - 1));
-        if (d > g + 8.0 * eps) return;
-    }
-    if (nl < a.K) return;                          // the set is exhausted
-    const uint64_t* sb = a.setbits + (size_t)set * a.W64;
-    for (int k = start; k < nblm; k++) {           // rare: more than K near-tied targets
-        const int b = a.blm[k];
-        if (!setbit(sb, b)) continue;
-        bool isrep = false;
-#pragma unroll
-        for (int q = 0; q < RC; q++) isrep |= (q < nrep) && ((int)reps[q] == b);
-        if (isrep) continue;
-        const double d = ds + dtgt(a.r[b], delta);
-        if (d <= g + 4.0 * eps) emit(a, T, kind, src, b, w, ib | (unsigned long long)k);
-        if (d > g + 8.0 * eps) return;
-    }
-}
-
-template <int RC>
-__global__ __launch_bounds__(SCAN_THREADS) void k_census(ScanArgs a) {
-    DevCtl* ctl = a.ctl;
-    if (ctl->halted) return;
-    const double eps = ctl->eps;
-    const unsigned long long eL = ctl->gmin[0], eN = ctl->gmin[1];
-    const double gL = eL == NONE64 ? HUGE_VAL : dec(eL);
-    const double gN = eN == NONE64 ? HUGE_VAL : dec(eN);
-    const BlockRec& br = a.blockrec[blockIdx.x];
-    const bool doL = a.allow_leader && eL != NONE64 && br.dmin[0] <= gL + 8.0 * eps;
-    const bool doN = eN != NONE64 && br.dmin[1] <= gN + 8.0 * eps;
-    if (!doL && !doN) return;
-    __shared__ uint32_t s_key[DEDUP_CENSUS];
-    __shared__ unsigned long long s_wb[DEDUP_CENSUS], s_it[DEDUP_CENSUS];
-    Dedup T{s_key, s_wb, s_it, DEDUP_CENSUS};
-    dedup_clear(T);
-    __syncthreads();
-    const double inv_avg = ctl->inv_avg;
-    const int nblm = ctl->nblm;
-    const int roff = sr_r_off(a.K);
-    const long long base = a.shard_begin + (long long)blockIdx.x * TILE + (long long)threadIdx.x * PER_LANE;
-    PartRegs<RC> P;
-    load_parts<RC>(a, base, P);
-    for (int j = 0; j < PER_LANE; j++) {
-        const long long p = base + j;
-        if (p >= a.shard_end) continue;
-        const uint32_t m = P.m[j];
-        const int nrep = (int)meta_nrep(m), set = (int)meta_set(m);
-        if (!meta_elig(m) || nrep == 0) continue;
-        uint32_t reps[RC];
-#pragma unroll
-        for (int k = 0; k < RC; k++) reps[k] = P.r[k][j];
-        const unsigned char* rec = a.setrec + (size_t)set * a.stride;
-        const int32_t* ids = (const int32_t*)(rec + sr_ids_off());
-        const double* rr = (const double*)(rec + roff);
-        double rt = 0.0;
-        bool have = false;
-        for (int i = 0; i < a.K && !have; i++) {
-            const int b = ids[i];
-            if (b < 0) break;
-            bool isrep = false;
-#pragma unroll
-            for (int k = 0; k < RC; k++) isrep |= (k < nrep) && ((int)reps[k] == b);
-            if (!isrep) { rt = rr[i]; have = true; }
-        }
-        if (!have) continue;
-        const double w = P.w[j];
-        const double delta = w * inv_avg;
-        const double dt = dtgt(rt, delta);
-        if (doL) {
-            const double ds = dsrc(a.r[reps[0]], delta);
-            if (ds + dt <= gL + 8.0 * eps)
-                walk_targets<RC>(a, T, 0, p, 0, (int)reps[0], reps, nrep, set, w, ds, gL, eps, nblm, inv_avg);
-        }
-        if (doN) {
-#pragma unroll
-            for (int k = 1; k < RC; k++) {
-                if (k < nrep) {
-                    const double ds = dsrc(a.r[reps[k]], delta);
-                    if (ds + dt <= gN + 8.0 * eps)
-                        walk_targets<RC>(a, T, 1, p, k, (int)reps[k], reps, nrep, set, w, ds, gN, eps, nblm, inv_avg);
-                }
-            }
-        }
-    }
-    __syncthreads();
-    // flush the workgroup's distinct keys (earliest iteration index per key)
-    for (int h = threadIdx.x; h < DEDUP_CENSUS; h += SCAN_THREADS)
-        if (s_key[h] != NONE32 && s_wb[h] != NONE64) emit_global(a, dedup_entry(T, h));
-}
-
-// ------------------------------------------------------------ k_resolve
-
-struct Decision {
-    int32_t status, step, kind, slot;
-    long long part;
-    int32_t from, to;
-    double su, cu;
-    int32_t exact, err, err_broker, pad;
-};
-
-__device__ __forceinline__ double contribution(const ResolveArgs& a, uint32_t q, int b) {
-    const uint32_t m = a.meta[q];
-    const int lead = a.rep[q] == (uint16_t)b;   // slot 0 of partition q
-    const double w = a.w[q];
-    if (lead) return w * (double)((int)meta_nrep(m) + a.nc[q]);
-    return w;
-}
-
-// remove partition q from broker b's list (block-wide, all threads call)
-__device__ void list_remove(const ResolveArgs& a, int b, uint32_t q, int* s_i) {
-    const uint32_t st = a.lstart[b], n = a.llen[b];
-    if (threadIdx.x == 0) *s_i = -1;
-    __syncthreads();
-    for (uint32_t i = threadIdx.x; i < n; i += RESOLVE_THREADS)
-        if (a.lent[st + i] == q) *s_i = (int)i;
-    __syncthreads();
-    const int at = *s_i;
-    if (at < 0) return;
-    for (uint32_t c = (uint32_t)at; c + 1 < n; c += RESOLVE_THREADS) {
-        uint32_t j = c + threadIdx.x;
-        uint32_t v = 0;
-        bool act = j + 1 < n;
-        if (act) v = a.lent[st + j + 1];
-        __syncthreads();
-        if (act) a.lent[st + j] = v;
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) a.llen[b] = n - 1;
-    __syncthreads();
-}
-
-// insert partition q into broker b's sorted list
-__device__ bool list_insert(const ResolveArgs& a, int b, uint32_t q, int* s_i) {
-    const uint32_t st = a.lstart[b], n = a.llen[b];
-    if (n >= a.lcap[b]) return false;
-    if (threadIdx.x == 0) *s_i = 0;
-    __syncthreads();
-    int c = 0;
-    for (uint32_t i = threadIdx.x; i < n; i += RESOLVE_THREADS) c += a.lent[st + i] < q ? 1 : 0;
-    c = wave_sum(c);
-    if ((threadIdx.x & 63) == 0 && c) atomicAdd(s_i, c);
-    __syncthreads();
-    const uint32_t at = (uint32_t)*s_i;
-    long long hi = (long long)n;
-    while (hi > (long long)at) {
-        long long lo = hi - RESOLVE_THREADS;
-        if (lo < (long long)at) lo = at;
-        long long j = lo + threadIdx.x;
-        bool act = j < hi;
-        uint32_t v = 0;
-        if (act) v = a.lent[st + j];
-        __syncthreads();
-        if (act) a.lent[st + j + 1] = v;
-        __syncthreads();
-        hi = lo;
-    }
-    if (threadIdx.x == 0) { a.lent[st + at] = q; a.llen[b] = n + 1; }
-    __syncthreads();
-    return true;
-}
-
-__global__ __launch_bounds__(RESOLVE_THREADS) void k_resolve(ResolveArgs a) {
-    DevCtl* ctl = a.ctl;
-    if (ctl->halted) return;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    constexpr int NW = RESOLVE_THREADS / 64;
-    constexpr int FOLD_CHUNK = 512;
-    __shared__ Decision D;
-    __shared__ int s_done, s_i, s_fail, s_ndist;
-    __shared__ unsigned long long s_u[NW];
-    __shared__ double s_dv[NW];
-    __shared__ int s_flag[NW];
-    __shared__ double s_fold[8][FOLD_CHUNK];     // refold staging (non-integral mode)
-    __shared__ double s_Lm[MAXB];                // exact loads in bl_move order
-    __shared__ uint32_t s_key[DEDUP_RESOLVE];
-    __shared__ unsigned long long s_wb[DEDUP_RESOLVE], s_it[DEDUP_RESOLVE];
-    Dedup T{s_key, s_wb, s_it, DEDUP_RESOLVE};
-    const double su = ctl->U0;
-    const double eps = ctl->eps;
-    const int nblm = ctl->nblm;
-    KB_STAMP_BEGIN();
-    for (int k = tid; k < nblm; k += RESOLVE_THREADS) s_Lm[k] = a.load[a.blm[k]];
-
-    if (tid == 0) {
-        D.status = 0; D.step = -1; D.kind = 0; D.slot = -1; D.part = -1;
-        D.from = -1; D.to = -1; D.su = su; D.cu = su; D.exact = 1; D.err = E_NONE; D.err_broker = -1;
-        s_done = 0;
-        const uint32_t* F = ctl->first;
-        auto rd = [&](uint32_t p, int k) -> int { return (int)a.rep[(long long)k * a.Ppad + p]; };
-        if (a.sem_go && F[F_DUP] != NONE32) {
-            D.status = -1; D.step = 1; D.err = E_DUP; D.part = F[F_DUP]; s_done = 1;
-        } else if (F[F_REMOVE] != NONE32) {                      // steps.go:70-89
-            const uint32_t p = F[F_REMOVE];
-            const uint32_t m = a.meta[p];
-            const int nrep = (int)meta_nrep(m), set = (int)meta_set(m);
-            const uint64_t* sb = a.setbits + (size_t)set * a.W64;
-            // lightest allowed replica in (load, id) order = smallest bl position
-            int best = -1, bslot = -1, bpos = 0x7FFFFFFF;
-            for (int k = 0; k < nrep; k++) {
-                const int b = rd(p, k);
-                if (!setbit(sb, b)) continue;
-                const int ps = a.posm[b];
-                if (ps < bpos) { bpos = ps; best = b; bslot = k; }
-            }
-            D.step = 3; D.part = p;
-            if (best < 0) { D.status = -1; D.err = E_REMOVE; }
-            else {
-                // replacepl removes the FIRST slot holding that broker (utils.go:167-178)
-                D.status = 1; D.kind = 2; D.slot = bslot; D.from = best; D.to = -1;
-            }
-            s_done = 1;
-        } else if (F[F_ADD] != NONE32) {                         // steps.go:93-113
-            const uint32_t p = F[F_ADD];
-            const uint32_t m = a.meta[p];
-            const int nrep = (int)meta_nrep(m), set = (int)meta_set(m);
-            const int32_t* dl = a.lists + ((size_t)set * 2 + 1) * a.K;
-            int t = -1;
-            for (int i = 0; i < a.K && t < 0; i++) {
-                const int b = dl[i];
-                if (b < 0) break;
-                bool isrep = false;
-                for (int k = 0; k < nrep; k++) isrep |= rd(p, k) == b;
-                if (!isrep) t = b;
-            }
-            D.step = 4; D.part = p;
-            if (t < 0) { D.status = -1; D.err = E_ADD; }
-            else { D.status = 1; D.kind = 3; D.slot = nrep; D.from = -1; D.to = t; }
-            s_done = 1;
-        } else if (F[F_DIS] != NONE32) {                         // steps.go:117-143
-            const uint32_t p = F[F_DIS];
-            const uint32_t m = a.meta[p];
-            const int nrep = (int)meta_nrep(m), set = (int)meta_set(m);
-            const uint64_t* sb = a.setbits + (size_t)set * a.W64;
-            int vslot = -1;
-            for (int k = 0; k < nrep && vslot < 0; k++) if (!setbit(sb, rd(p, k))) vslot = k;
-            const int32_t* dl = a.lists + ((size_t)set * 2 + 0) * a.K;
-            int t = -1;
-            for (int i = 0; i < a.K && t < 0; i++) {
-                const int b = dl[i];
-                if (b < 0) break;
-                bool isrep = false;
-                for (int k = 0; k < nrep; k++) isrep |= rd(p, k) == b;
-                if (!isrep) t = b;
-            }
-            D.step = 5; D.part = p; D.slot = vslot; D.from = rd(p, vslot);
-            if (t < 0) { D.status = -1; D.err = E_DIS; D.err_broker = D.from; }
-            else { D.status = 1; D.kind = 1; D.to = t; }
-            s_done = 1;
-        } else if (a.rebalance && !(su < a.min_unbalance)) {     // steps.go:299-347
-            if (F[F_EMPTY] != NONE32 || nblm == 0) {
-                D.status = -1; D.step = 6; D.err = E_PANIC; D.part = F[F_EMPTY]; s_done = 1;
-            } else if (F[F_LEAD] != NONE32) {
-                const uint32_t p = F[F_LEAD];
-                const int nrep = (int)meta_nrep(a.meta[p]);
-                const int light = ctl->light;
-                int ex = -1;
-                for (int k = 0; k < nrep && ex < 0; k++) if (rd(p, k) == light) ex = k;
-                D.status = 1; D.step = 6; D.part = p; D.slot = 0; D.from = rd(p, 0); D.to = light;
-                D.kind = ex >= 0 ? 4 : 1;       // swap when bl[0] is already a replica
-                s_done = 1;
-            }
-        }
-    }
-    __syncthreads();
-    KB_STAMP(ctl, 8);
-
-    // move(): leader step (if allowed), then non-leader step (steps.go:284-298)
-    for (int kind = a.allow_leader ? 0 : 1; kind < 2 && !s_done; kind++) {
-        const int step = kind == 0 ? 7 : 8;
-        if (tid == 0) {
-            if (ctl->first[F_EMPTY_ELIG] != NONE32) {
-                D.status = -1; D.step = step; D.err = E_PANIC; D.part = ctl->first[F_EMPTY_ELIG]; s_done = 1;
-            } else if (ctl->cont_overflow) {
-                D.status = -1; D.step = step; D.err = E_CONT_OVERFLOW; s_done = 1;
-            }
-            s_fail = 0;
-            s_ndist = 0;
-        }
-        dedup_clear(T);
-        __syncthreads();
-        if (s_done) break;
-        const uint32_t nc = min(ctl->ncont, a.cont_cap);
-        // (1) distinct keys of this kind (earliest iteration index per key)
-        for (uint32_t i = tid; i < nc; i += RESOLVE_THREADS) {
-            const Contender c = a.cont[i];
-            if (c.kind == kind && dedup_insert(T, c.kind, c.s, c.t, c.w, c.iter) < 0) s_fail = 1;
-        }
-        __syncthreads();
-        int nd = 0;
-        for (int h = tid; h < DEDUP_RESOLVE; h += RESOLVE_THREADS) nd += s_key[h] != NONE32 ? 1 : 0;
-        nd = wave_sum(nd);
-        if (lane == 0 && nd) atomicAdd(&s_ndist, nd);
-        __syncthreads();
-        const int ndist = s_ndist;
-        const bool fail = s_fail != 0;
-        double Ustar = su;
-        unsigned long long witer = NONE64;
-        Contender cw;
-        cw.s = cw.t = -1; cw.w = 0; cw.iter = NONE64; cw.kind = kind; cw.pad = 0;
-        int exact = 1;
-        const double thr = su - a.min_unbalance;          // steps.go:292
-        const bool have = ndist > 0 || fail;
-        if (!fail && ndist == 1) {
-            // one key: every contender scores the same exact U; the first in iteration order wins
-            if (tid == 0) s_i = -1;
-            __syncthreads();
-            for (int h = tid; h < DEDUP_RESOLVE; h += RESOLVE_THREADS) if (s_key[h] != NONE32) s_i = h;
-            __syncthreads();
-            cw = dedup_entry(T, s_i);
-            witer = cw.iter;
-            const double delta = cw.w * ctl->inv_avg;
-            const double Ua = su + (dsrc(a.r[cw.s], delta) + dtgt(a.r[cw.t], delta));
-            const double lim = thr < su ? thr : su;
-            const bool certain = (Ua + 2.0 * eps < lim) || (Ua - 2.0 * eps >= (thr > su ? thr : su));
-            if (certain && !a.exact_unb) { Ustar = Ua; exact = 0; }
-            else {
-                if (tid == 0) {
-                    s_dv[0] = exact_unbalance_lds(s_Lm, nblm, a.posm[cw.s], a.posm[cw.t],
-                                                  a.load[cw.s] - cw.w, a.load[cw.t] + cw.w);
-                    atomicAdd(&ctl->total_folds, 1ull);
-                }
-                __syncthreads();
-                Ustar = s_dv[0];
-            }
-        } else if (have) {
-            // several keys (or an overfull table): exact sequential folds, lexicographic min
-            double bu = HUGE_VAL;
-            unsigned long long bi = NONE64;
-            int bs = -1, bt = -1;
-            double bw = 0.0;
-            unsigned long long nf = 0;
-            if (!fail) {
-                for (int h = tid; h < DEDUP_RESOLVE; h += RESOLVE_THREADS) {
-                    if (s_key[h] == NONE32) continue;
-                    const Contender c = dedup_entry(T, h);
-                    const double u = exact_unbalance_lds(s_Lm, nblm, a.posm[c.s], a.posm[c.t],
-                                                         a.load[c.s] - c.w, a.load[c.t] + c.w);
-                    nf++;
-                    if (u < bu || (u == bu && c.iter < bi)) { bu = u; bi = c.iter; bs = c.s; bt = c.t; bw = c.w; }
-                }
-            } else {
-                for (uint32_t i = tid; i < nc; i += RESOLVE_THREADS) {
-                    const Contender c = a.cont[i];
-                    if (c.kind != kind) continue;
-                    const double u = exact_unbalance_lds(s_Lm, nblm, a.posm[c.s], a.posm[c.t],
-                                                         a.load[c.s] - c.w, a.load[c.t] + c.w);
-                    nf++;
-                    if (u < bu || (u == bu && c.iter < bi)) { bu = u; bi = c.iter; bs = c.s; bt = c.t; bw = c.w; }
-                }
-            }
-            nf = wave_sum(nf);
-            if (lane == 0 && nf) atomicAdd(&ctl->total_folds, nf);
-            for (int o = 32; o > 0; o >>= 1) {
-                const double ou = __shfl_xor(bu, o);
-                const unsigned long long oi = __shfl_xor(bi, o);
-                const int os = __shfl_xor(bs, o), ot = __shfl_xor(bt, o);
-                const double ow = __shfl_xor(bw, o);
-                if (ou < bu || (ou == bu && oi < bi)) { bu = ou; bi = oi; bs = os; bt = ot; bw = ow; }
-            }
-            if (lane == 0) { s_dv[wid] = bu; s_u[wid] = bi; s_flag[wid] = wid; }
-            __shared__ int s_bs[NW], s_bt[NW];
-            __shared__ double s_bw[NW];
-            if (lane == 0) { s_bs[wid] = bs; s_bt[wid] = bt; s_bw[wid] = bw; }
-            __syncthreads();
-            if (tid == 0) {
-                for (int q = 1; q < NW; q++)
-                    if (s_dv[q] < s_dv[0] || (s_dv[q] == s_dv[0] && s_u[q] < s_u[0])) {
-                        s_dv[0] = s_dv[q]; s_u[0] = s_u[q]; s_bs[0] = s_bs[q]; s_bt[0] = s_bt[q]; s_bw[0] = s_bw[q];
-                    }
-            }
-            __syncthreads();
-            Ustar = s_dv[0]; witer = s_u[0];
-            cw.s = s_bs[0]; cw.t = s_bt[0]; cw.w = s_bw[0]; cw.iter = witer;
-        }
-        __syncthreads();
-        if (tid == 0) {
-            // cu starts at su and only a strictly smaller u replaces it (steps.go:227-229,276)
-            const bool improved = have && Ustar < su;
-            const double cu = improved ? Ustar : su;
-            if (cu < thr) {
-                if (!improved) {
-                    // replacepl on the zero Partition: the reference panics
-                    D.status = -1; D.step = step; D.err = E_PANIC; s_done = 1;
-                } else {
-                    D.status = 1; D.step = step; D.kind = 1;
-                    D.part = (long long)(witer >> 21); D.slot = (int)((witer >> 16) & 31);
-                    D.from = cw.s; D.to = cw.t; D.su = su; D.cu = cu; D.exact = exact;
-                    s_done = 1;
-                }
-            }
-        }
-        __syncthreads();
-    }
-    KB_STAMP(ctl, 9);
-
-    // ---------------------------------------------------------- apply
-    __shared__ int s_aff[2 * MAXR + 2];
-    __shared__ double s_oldc[2 * MAXR + 2];
-    __shared__ int s_naff;
-    if (tid == 0) {
-        s_naff = 0;
-        if (D.status == 1) {
-            const long long p = D.part;
-            const uint32_t m = a.meta[p];
-            const int nrep = (int)meta_nrep(m);
-            int r[MAXR + 1];
-            for (int k = 0; k < nrep; k++) r[k] = (int)a.rep[(long long)k * a.Ppad + p];
-            const double wv = a.w[p];
-            const int ncp = a.nc[p];
-            for (int k = 0; k < nrep; k++) {             // old contributions of p's brokers
-                s_aff[s_naff] = r[k];
-                s_oldc[s_naff] = k == 0 ? wv * (double)(nrep + ncp) : wv;
-                s_naff++;
-            }
-            int nn = nrep;
-            bool state_changed = true;
-            if (D.kind == 1) {                           // replace at slot (utils.go:186-190)
-                r[D.slot] = D.to;
-            } else if (D.kind == 4) {                    // swap with the existing replica (utils.go:179-185)
-                int ex = 0;
-                for (int k = 0; k < nrep; k++) if (r[k] == D.to) { ex = k; break; }
-                const int old = r[D.slot];
-                r[D.slot] = D.to;
-                r[ex] = old;
-            } else if (D.kind == 2) {                    // remove (utils.go:176-178)
-                for (int k = D.slot; k + 1 < nrep; k++) r[k] = r[k + 1];
-                if (a.sem_go) state_changed = false;     // pl keeps its length: duplicates
-                else nn = nrep - 1;
-            } else if (D.kind == 3) {                    // add (utils.go:199-202)
-                if (a.sem_go) state_changed = false;     // the append is not visible through pl
-                else { r[nrep] = D.to; nn = nrep + 1; }
-            }
-            // the meta bits that depend on the replicas (Disallowed trigger, in-set count)
-            const uint64_t* sb = a.setbits + (size_t)meta_set(m) * a.W64;
-            auto remeta = [&](int n) {
-                uint32_t dis = 0, nin = 0;
-                for (int k = 0; k < n; k++) { const bool in = setbit(sb, r[k]); dis |= in ? 0u : 1u; nin += in ? 1u : 0u; }
-                return make_meta((uint32_t)n, meta_want(m), meta_elig(m), dis, nin, meta_set(m));
-            };
-            if (a.sem_go && (D.kind == 2 || D.kind == 3)) {
-                // Go aliasing: the remove shifted the shared backing array in place
-                if (D.kind == 2) {
-                    for (int k = 0; k < nrep; k++) a.rep[(long long)k * a.Ppad + p] = (uint16_t)r[k];
-                    a.meta[p] = remeta(nrep);
-                }
-                s_naff = 0;
-            } else if (state_changed) {
-                for (int k = 0; k < nn; k++) a.rep[(long long)k * a.Ppad + p] = (uint16_t)r[k];
-                a.meta[p] = remeta(nn);
-                if (D.kind == 1) { a.cnt[D.from]--; a.cnt[D.to]++; }
-                if (D.kind == 2) { a.cnt[D.from]--; }
-                if (D.kind == 3) { a.cnt[D.to]++; }
-                // new contributions; integral mode updates loads incrementally (exact)
-                const int base_aff = s_naff;
-                for (int k = 0; k < nn; k++) {
-                    const int b = r[k];
-                    const double cc = k == 0 ? wv * (double)(nn + ncp) : wv;
-                    int f = -1;
-                    for (int x = 0; x < base_aff; x++) if (s_aff[x] == b) f = x;
-                    if (f >= 0) {
-                        if (s_oldc[f] == cc) { s_aff[f] = -1 - s_aff[f]; }  // unchanged contribution
-                        else if (a.integral) a.load[b] = (a.load[b] - s_oldc[f]) + cc;
-                    } else {
-                        if (a.integral) a.load[b] = a.load[b] + cc;
-                        s_aff[s_naff] = b; s_oldc[s_naff] = 0.0; s_naff++;
-                    }
-                }
-                for (int x = 0; x < base_aff; x++) {
-                    const int b = s_aff[x];
-                    if (b < 0) continue;
-                    bool still = false;
-                    for (int k = 0; k < nn; k++) still |= r[k] == b;
-                    if (!still && a.integral) a.load[b] = a.load[b] - s_oldc[x];
-                }
-                int n2 = 0;                              // brokers whose contribution changed
-                for (int x = 0; x < s_naff; x++) if (s_aff[x] >= 0) s_aff[n2++] = s_aff[x];
-                s_naff = n2;
-            } else {
-                s_naff = 0;
-            }
-        }
-    }
-    __syncthreads();
-    KB_STAMP(ctl, 10);
-    // non-integral: maintain per-broker partition lists and refold touched loads exactly
-    if (D.status == 1 && !a.integral && s_naff > 0) {
-        const uint32_t p = (uint32_t)D.part;
-        bool ok = true;
-        if (D.kind == 1) {
-            list_remove(a, D.from, p, &s_i);
-            ok = list_insert(a, D.to, p, &s_i);
-        } else if (D.kind == 2 && !a.sem_go) {
-            list_remove(a, D.from, p, &s_i);
-        } else if (D.kind == 3 && !a.sem_go) {
-            ok = list_insert(a, D.to, p, &s_i);
-        }
-        KB_STAMP(ctl, 11);
-        if (!ok) {
-            if (tid == 0) { ctl->list_overflow = 1; D.status = -1; D.err = E_LIST_OVERFLOW; }
-        } else {
-            const int naff = s_naff;
-            for (int x0 = 0; x0 < naff; x0 += 8) {
-                // stage up to 8 brokers' contributions chunk by chunk; lane 0 of wave x folds
-                const int nb = naff - x0 < 8 ? naff - x0 : 8;
-                uint32_t maxn = 0;
-                for (int x = 0; x < nb; x++) { const uint32_t n = a.llen[s_aff[x0 + x]]; maxn = n > maxn ? n : maxn; }
-                double acc = 0.0;
-                for (uint32_t c = 0; c < maxn; c += FOLD_CHUNK) {
-                    for (int e = tid; e < nb * FOLD_CHUNK; e += RESOLVE_THREADS) {
-                        const int x = e / FOLD_CHUNK, i = e % FOLD_CHUNK;
-                        const int b = s_aff[x0 + x];
-                        const uint32_t n = a.llen[b], st = a.lstart[b];
-                        if (c + (uint32_t)i < n) s_fold[x][i] = contribution(a, a.lent[st + c + i], b);
-                    }
-                    __syncthreads();
-                    if (lane == 0 && wid < nb) {
-                        const int b = s_aff[x0 + wid];
-                        const uint32_t n = a.llen[b];
-                        if (c < n) acc = fold_lds(&s_fold[wid][0], (int)(n - c < FOLD_CHUNK ? n - c : FOLD_CHUNK), acc);
-                    }
-                    __syncthreads();
-                }
-                if (lane == 0 && wid < nb) a.load[s_aff[x0 + wid]] = acc;
-                __syncthreads();
-            }
-        }
-    }
-    __syncthreads();
-    if (tid == 0) {
-        KB_STAMP(ctl, 12);
-        ChangeDev ch;
-        ch.status = D.status; ch.step = D.step; ch.kind = D.kind; ch.slot = D.slot;
-        ch.part = D.part; ch.from = D.from; ch.to = D.to; ch.su = D.su; ch.cu = D.cu;
-        ch.exact = D.exact; ch.err_code = D.err; ch.err_broker = D.err_broker; ch.pad = 0;
-        if (ctl->logpos < ctl->logcap) a.log[ctl->logpos] = ch;
-        ctl->logpos++;
-        ctl->steps++;
-        // reference candidate count of the steps that actually ran this iteration
-        unsigned long long add = 0;
-        if (D.step < 0 || D.step >= 7) {
-            if (a.allow_leader) add += ctl->ncand[0];
-            if (D.step != 7) add += ctl->ncand[1];
-        }
-        ctl->total_cand += add;
-        ctl->total_cont += min(ctl->ncont, a.cont_cap);
-        if (D.status != 1) ctl->halted = 1;
-    }
-}
-
-// --------------------------------------------------- multi-GPU summaries
-
-// pack this rank's scan result + its distinct local near-tie keys
-__global__ __launch_bounds__(1024) void k_summary(SumArgs a) {
-    DevCtl* ctl = a.ctl;
-    Summary* s = a.out;
-    __shared__ uint32_t s_key[DEDUP_RESOLVE];
-    __shared__ unsigned long long s_wb[DEDUP_RESOLVE], s_it[DEDUP_RESOLVE];
-    __shared__ uint32_t s_n;
-    __shared__ int s_fail;
-    Dedup T{s_key, s_wb, s_it, DEDUP_RESOLVE};
-    dedup_clear(T);
-    if (threadIdx.x == 0) { s_n = 0; s_fail = 0; }
-    __syncthreads();
-    const uint32_t nc = min(ctl->ncont, a.cont_cap);
-    for (uint32_t i = threadIdx.x; i < nc; i += blockDim.x) {
-        const Contender c = a.cont[i];
-        if (dedup_insert(T, c.kind, c.s, c.t, c.w, c.iter) < 0) s_fail = 1;
-    }
-    __syncthreads();
-    for (int h = threadIdx.x; h < DEDUP_RESOLVE; h += blockDim.x) {
-        if (s_key[h] == NONE32) continue;
-        const uint32_t k = atomicAdd(&s_n, 1u);
-        if (k < (uint32_t)SUMMARY_CONT) s->cont[k] = dedup_entry(T, h);
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        s->gmin[0] = ctl->gmin[0]; s->gmin[1] = ctl->gmin[1];
-        for (int f = 0; f < NF; f++) s->first[f] = ctl->first[f];
-        s->ncand[0] = ctl->ncand[0]; s->ncand[1] = ctl->ncand[1];
-        s->ncont = s_n < (uint32_t)SUMMARY_CONT ? s_n : (uint32_t)SUMMARY_CONT;
-        s->overflow = (ctl->cont_overflow || s_fail || s_n > (uint32_t)SUMMARY_CONT) ? 1u : 0u;
-        if (ctl->halted) s->overflow |= 2u;
-    }
-}
-
-// combine every rank's summary identically on every rank
-__global__ __launch_bounds__(256) void k_merge(MergeArgs a) {
-    DevCtl* ctl = a.ctl;
-    if (ctl->halted) return;
-    __shared__ unsigned long long g[2];
-    __shared__ uint32_t total;
-    if (threadIdx.x == 0) {
-        g[0] = g[1] = NONE64;
-        uint32_t f[NF];
-        for (int q = 0; q < NF; q++) f[q] = NONE32;
-        unsigned long long c0 = 0, c1 = 0;
-        uint32_t ov = 0;
-        for (int r = 0; r < a.nranks; r++) {
-            const Summary* s = a.all + r;
-            g[0] = s->gmin[0] < g[0] ? s->gmin[0] : g[0];
-            g[1] = s->gmin[1] < g[1] ? s->gmin[1] : g[1];
-            for (int q = 0; q < NF; q++) f[q] = min(f[q], s->first[q]);
-            c0 += s->ncand[0]; c1 += s->ncand[1];
-            ov |= s->overflow & 1u;
-        }
-        ctl->gmin[0] = g[0]; ctl->gmin[1] = g[1];
-        for (int q = 0; q < NF; q++) ctl->first[q] = f[q];
-        ctl->ncand[0] = c0; ctl->ncand[1] = c1;
-        ctl->cont_overflow = ov;
-        total = 0;
+        s_g[0] = d0; s_g[1] = d1;
+        out->dmin[0] = d0; out->dmin[1] = d1; out->cand[0] = c0; out->cand[1] = c1;
+        for (int q = 0; q < NF; q++) out->first[q] = f[q];
     }
     __syncthreads();
     const double eps = ctl->eps, inv_avg = ctl->inv_avg;
-    for (int r = 0; r < a.nranks; r++) {
-        const Summary* s = a.all + r;
-        for (uint32_t i = threadIdx.x; i < s->ncont; i += blockDim.x) {
-            const Contender c = s->cont[i];
-            // each rank emitted relative to its own minimum; keep those within the
-            // global bound (every rank holds the same loads, so d is identical)
-            if (g[c.kind] == NONE64) continue;
-            const double gm = dec(g[c.kind]);
-            const double delta = c.w * inv_avg;
-            const double d = dsrc(a.r[c.s], delta) + dtgt(a.r[c.t], delta);
-            if (!(d <= gm + 4.0 * eps)) continue;
-            const uint32_t k = atomicAdd(&total, 1u);
-            if (k < a.cont_cap) a.cont[k] = c;
+    auto ins = [&](const Contender& c) {
+        const double g = s_g[c.kind];
+        if (!(cont_delta(a.r, c, inv_avg) <= g + 4.0 * eps)) return;
+        if (dedup_insert(T, c.kind, c.s, c.t, c.w, c.iter) < 0) s_fail = 1;
+    };
+    if (ran) {
+        for (int i = tid; i < a.nrec; i += 1024) {
+            const RecHdr* h = (const RecHdr*)(a.recs + (size_t)i * WGREC_BYTES);
+            const Contender* keys = (const Contender*)(h + 1);
+            for (uint32_t k = 0; k < h->nkeys; k++) ins(keys[k]);
         }
+        const uint32_t nc = min(ctl->ncont, a.cont_cap);
+        for (uint32_t i = tid; i < nc; i += 1024) ins(a.cont[i]);
     }
     __syncthreads();
-    if (threadIdx.x == 0) ctl->ncont = total;
+    for (int h = tid; h < DEDUP_STEP; h += 1024) {
+        if (s_key[h] == NONE32) continue;
+        const uint32_t k = atomicAdd(&s_n, 1u);
+        if (k < (uint32_t)SUMMARY_KEYS) okeys[k] = dedup_entry(T, h);
+    }
+    __syncthreads();
+    if (tid == 0) {
+        out->nkeys = s_n < (uint32_t)SUMMARY_KEYS ? s_n : (uint32_t)SUMMARY_KEYS;
+        out->flags = ((ran && ctl->cont_overflow) || s_fail || s_n > (uint32_t)SUMMARY_KEYS) ? 1u : 0u;
+        out->pad[0] = ran ? 1u : 0u;
+        out->pad[1] = 0;
+    }
 }
 
 // ------------------------------------------------------- launch helpers
 
 template <int RC>
-static void launch_scan_rc(const ScanArgs& a, int tiles, hipStream_t st) {
-    hipLaunchKernelGGL(k_scan<RC>, dim3(tiles), dim3(SCAN_THREADS), 0, st, a);
+static void launch_scan_rc(const ScanArgs& a, bool lds_sets, size_t lds, hipStream_t st) {
+    const int grid = a.nscan + (a.listwg ? 1 : 0);
+    if (lds_sets) hipLaunchKernelGGL((k_scan<RC, true>), dim3(grid), dim3(SCAN_THREADS), lds, st, a);
+    else hipLaunchKernelGGL((k_scan<RC, false>), dim3(grid), dim3(SCAN_THREADS), lds, st, a);
+}
+
+void launch_scan(const ScanArgs& a, int rc, bool lds_sets, size_t lds, hipStream_t st) {
+    switch (rc) {
+        case 1: launch_scan_rc<1>(a, lds_sets, lds, st); break;
+        case 2: launch_scan_rc<2>(a, lds_sets, lds, st); break;
+        case 3: launch_scan_rc<3>(a, lds_sets, lds, st); break;
+        case 4: launch_scan_rc<4>(a, lds_sets, lds, st); break;
+        case 6: launch_scan_rc<6>(a, lds_sets, lds, st); break;
+        case 8: launch_scan_rc<8>(a, lds_sets, lds, st); break;
+        case 12: launch_scan_rc<12>(a, lds_sets, lds, st); break;
+        default: launch_scan_rc<16>(a, lds_sets, lds, st); break;
+    }
 }
 template <int RC>
-static void launch_census_rc(const ScanArgs& a, int tiles, hipStream_t st) {
-    hipLaunchKernelGGL(k_census<RC>, dim3(tiles), dim3(SCAN_THREADS), 0, st, a);
+static int scan_occ_rc(bool lds_sets, size_t lds) {
+    int n = 0;
+    if (lds_sets) hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_scan<RC, true>, SCAN_THREADS, lds);
+    else hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_scan<RC, false>, SCAN_THREADS, lds);
+    return n;
 }
 
-#define KB_RC_SWITCH(RCV, FN, ...)                  \
-    switch (RCV) {                                   \
-        case 1: FN<1>(__VA_ARGS__); break;           \
-        case 2: FN<2>(__VA_ARGS__); break;           \
-        case 3: FN<3>(__VA_ARGS__); break;           \
-        case 4: FN<4>(__VA_ARGS__); break;           \
-        case 6: FN<6>(__VA_ARGS__); break;           \
-        case 8: FN<8>(__VA_ARGS__); break;           \
-        case 12: FN<12>(__VA_ARGS__); break;         \
-        default: FN<16>(__VA_ARGS__); break;         \
+int scan_blocks_per_cu(int rc, bool lds_sets, size_t lds) {
+    switch (rc) {
+        case 1: return scan_occ_rc<1>(lds_sets, lds);
+        case 2: return scan_occ_rc<2>(lds_sets, lds);
+        case 3: return scan_occ_rc<3>(lds_sets, lds);
+        case 4: return scan_occ_rc<4>(lds_sets, lds);
+        case 6: return scan_occ_rc<6>(lds_sets, lds);
+        case 8: return scan_occ_rc<8>(lds_sets, lds);
+        case 12: return scan_occ_rc<12>(lds_sets, lds);
+        default: return scan_occ_rc<16>(lds_sets, lds);
     }
+}
 
-void launch_prep(const PrepArgs& a, hipStream_t st) {
-    const size_t lds = (size_t)a.NP2 * (8 + 8 + 4);
-    hipLaunchKernelGGL(k_prep, dim3(1), dim3(PREP_THREADS), lds, st, a);
+void launch_step(const StepArgs& a, hipStream_t st) {
+    hipLaunchKernelGGL(k_step, dim3(1), dim3(STEP_THREADS), 0, st, a);
 }
-void launch_setlists(const SetArgs& a, hipStream_t st) {
-    hipLaunchKernelGGL(k_setlists, dim3((a.nsets + 3) / 4), dim3(256), 0, st, a);
+void launch_listop(DevCtl* ctl, const Lists& L, hipStream_t st) {
+    hipLaunchKernelGGL(k_listop, dim3(1), dim3(1024), 0, st, ctl, L);
 }
-void launch_scan(const ScanArgs& a, int rc, int tiles, hipStream_t st) {
-    KB_RC_SWITCH(rc, launch_scan_rc, a, tiles, st);
-}
-void launch_census(const ScanArgs& a, int rc, int tiles, hipStream_t st) {
-    KB_RC_SWITCH(rc, launch_census_rc, a, tiles, st);
-}
-void launch_reduce(const ReduceArgs& a, hipStream_t st) {
-    hipLaunchKernelGGL(k_reduce, dim3(1), dim3(1024), 0, st, a);
-}
-void launch_resolve(const ResolveArgs& a, hipStream_t st) {
-    hipLaunchKernelGGL(k_resolve, dim3(1), dim3(RESOLVE_THREADS), 0, st, a);
+void launch_refresh(const RefreshArgs& a, hipStream_t st) {
+    if (a.B > 0) hipLaunchKernelGGL(k_refresh, dim3(a.B), dim3(REFRESH_THREADS), 0, st, a);
 }
 void launch_summary(const SumArgs& a, hipStream_t st) {
     hipLaunchKernelGGL(k_summary, dim3(1), dim3(1024), 0, st, a);
-}
-void launch_merge(const MergeArgs& a, hipStream_t st) {
-    hipLaunchKernelGGL(k_merge, dim3(1), dim3(256), 0, st, a);
 }
 
 }  // namespace kbe

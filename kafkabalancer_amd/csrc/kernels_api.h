@@ -6,29 +6,13 @@
 
 namespace kbe {
 
-struct PrepArgs {
-    DevCtl* ctl;
-    const double* load;
-    const int32_t* cnt;
-    const uint8_t* incfg;
-    int B, NP2;
-    int32_t* order;        // [B] universe sorted by (load, id)
-    int32_t* blm;          // [B] bl_move order (present or in cfg.Brokers)
-    int32_t* posm;         // [B] position in bl_move or -1
-    double* r;             // [B] relative load L/avg - 1 (approximate, scoring only)
-    double rmax_w;         // max weight (for the eps bound)
-};
-
-struct SetArgs {
-    const DevCtl* ctl;
-    int nsets, B, W64, K, stride;
-    const uint64_t* setbits;
-    const int32_t* order;
-    const int32_t* posm;
-    const int32_t* cnt;
-    const double* r;
-    unsigned char* setrec;  // [nsets][stride] first K eligible targets + their r + nelig
-    int32_t* lists;         // [nsets][2][K]: desc present (Disallowed), desc universe (Add)
+// per-broker partition lists (non-integral loads): CSR with slack, sorted by
+// partition index, the fold order of getBrokerLoad (utils.go:92-105)
+struct Lists {
+    uint32_t* lstart;
+    uint32_t* llen;
+    uint32_t* lcap;
+    uint32_t* lent;
 };
 
 struct ScanArgs {
@@ -37,75 +21,85 @@ struct ScanArgs {
     const uint16_t* rep;      // [RC][Ppad] slot-major dense broker ids
     const uint32_t* meta;     // [Ppad]
     long long Ppad, shard_begin, shard_end;
-    int K, W64, stride;
+    int ntiles, nscan;        // tiles of TILE partitions; workgroups that scan
+    int B, nsets, W64, units; // units: 16-B words per set record
     const uint64_t* setbits;
-    const unsigned char* setrec;
+    const uint4* setrec;
     const double* r;
     const int32_t* blm;
     const int32_t* posm;
     int allow_leader, rebalance, sem_go;
-    BlockRec* blockrec;       // [tiles] per-tile record (k_reduce combines)
-    Contender* cont;
+    unsigned char* recs;      // [nscan][WGREC_BYTES]
+    Contender* cont;          // spill buffer
     uint32_t cont_cap;
+    int listwg;               // 1: the last workgroup applies the pending list op
+    Lists L;
 };
 
-struct ReduceArgs {
-    DevCtl* ctl;
-    const BlockRec* blockrec;
-    int tiles;
-};
-
-struct ResolveArgs {
+struct StepArgs {
     DevCtl* ctl;
     double* w;
     uint16_t* rep;
     uint32_t* meta;
     const int32_t* nc;        // NumConsumers
     long long Ppad;
-    int RC, K, W64, B;
+    int RC, KR, K, units, W64, B, nsets, NP2;
     const uint64_t* setbits;
-    const int32_t* lists;
-    const int32_t* blm;
-    const int32_t* posm;
-    const double* r;
-    double* load;
-    int32_t* cnt;
-    const Contender* cont;
+    uint4* setrec;
+    int32_t* lists;           // [nsets][2][K]: desc present (Disallowed), desc universe (Add)
+    int32_t* order;           // [B] universe sorted by (load, id)
+    int32_t* posu;            // [B] position in order
+    int32_t* blm;             // [B] bl_move order
+    int32_t* posm;            // [B] position in bl_move or -1
+    double* r;                // [B] approximate relative loads
+    double* load;             // [B] loads (exact in integral mode / when clean)
+    double* lerr;             // [B] bound |load - real sum of contributions| (dirty brokers)
+    uint8_t* dirty;           // [B] 1: load is an incremental approximation
+    int32_t* cnt;             // [B] replicas held
+    const uint8_t* incfg;     // [B] listed in -broker-ids
+    const int32_t* bset_off;  // [B+1] sets containing each broker
+    const int32_t* bset_ids;
+    const unsigned char* recs;   // scan records or gathered rank summaries
+    int nrec, rec_stride, rec_keys;
+    const Contender* cont;    // spill buffer (single-GPU mode)
     uint32_t cont_cap;
+    int use_spill;
     int allow_leader, rebalance, sem_go, integral, exact_unb;
     long long minrep;
-    double min_unbalance;
-    // per-broker partition lists (non-integral mode): CSR with slack
-    uint32_t* lstart;
-    uint32_t* llen;
-    uint32_t* lcap;
-    uint32_t* lent;
+    double min_unbalance, wmax;
     ChangeDev* log;
+    Lists L;
+};
+
+struct RefreshArgs {
+    DevCtl* ctl;
+    const double* w;
+    const uint16_t* rep;
+    const uint32_t* meta;
+    const int32_t* nc;
+    double* load;
+    double* lerr;
+    uint8_t* dirty;
+    const int32_t* cnt;
+    int B;
+    Lists L;
 };
 
 struct SumArgs {
     DevCtl* ctl;
+    const unsigned char* recs;
+    int nrec;
     const Contender* cont;
     uint32_t cont_cap;
-    Summary* out;
-};
-
-struct MergeArgs {
-    DevCtl* ctl;
-    const Summary* all;
-    int nranks;
-    Contender* cont;
-    uint32_t cont_cap;
     const double* r;
+    unsigned char* out;       // SUMMARY_BYTES
 };
 
-void launch_prep(const PrepArgs& a, hipStream_t st);
-void launch_setlists(const SetArgs& a, hipStream_t st);
-void launch_scan(const ScanArgs& a, int rc, int tiles, hipStream_t st);
-void launch_census(const ScanArgs& a, int rc, int tiles, hipStream_t st);
-void launch_reduce(const ReduceArgs& a, hipStream_t st);
-void launch_resolve(const ResolveArgs& a, hipStream_t st);
+void launch_scan(const ScanArgs& a, int rc, bool lds_sets, size_t lds_bytes, hipStream_t st);
+int scan_blocks_per_cu(int rc, bool lds_sets, size_t lds_bytes);
+void launch_step(const StepArgs& a, hipStream_t st);
+void launch_listop(DevCtl* ctl, const Lists& L, hipStream_t st);
+void launch_refresh(const RefreshArgs& a, hipStream_t st);
 void launch_summary(const SumArgs& a, hipStream_t st);
-void launch_merge(const MergeArgs& a, hipStream_t st);
 
 }  // namespace kbe

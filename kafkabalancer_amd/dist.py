@@ -41,12 +41,17 @@ class ShardedPlanner:
 
     def step(self):
         import torch.distributed as dist
-        self.engine.step_begin(self.summary)
-        if self.summary.is_cuda:
-            dist.all_gather_into_tensor(self.gathered, self.summary, group=self.group)
-        else:
-            dist.all_gather(self.parts, self.summary, group=self.group)
-        return self.engine.step_finish(self.gathered, self.world)
+        while True:
+            self.engine.step_begin(self.summary)
+            if self.summary.is_cuda:
+                dist.all_gather_into_tensor(self.gathered, self.summary, group=self.group)
+            else:
+                dist.all_gather(self.parts, self.summary, group=self.group)
+            ch = self.engine.step_finish(self.gathered, self.world)
+            # "retry": the bounds could not decide on approximate loads; every rank
+            # refolded its loads exactly and the step runs again
+            if not (isinstance(ch, str) and ch == "retry"):
+                return ch
 
     def plan(self, steps):
         out = []

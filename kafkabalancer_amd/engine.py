@@ -12,7 +12,7 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("KB_ENGINE_LIB") or os.path.join(_HERE, "lib", "libkbengine.so")
 
-KB_NOCHANGE, KB_CHANGE = 0, 1
+KB_NOCHANGE, KB_CHANGE, KB_RETRY = 0, 1, 2
 KB_SEM_APPLIED, KB_SEM_GO = 0, 1
 ERRORS = {-1: "KB_ERR_INVALID", -2: "KB_ERR_HIP", -3: "KB_ERR_UNSUPPORTED", -4: "KB_ERR_STEP",
           -5: "KB_ERR_CAPACITY", -6: "KB_ERR_PANIC"}
@@ -58,7 +58,8 @@ class kb_stats(C.Structure):
     _fields_ = [("steps", C.c_int64), ("candidates", C.c_int64), ("contenders", C.c_int64),
                 ("exact_folds", C.c_int64), ("scan_bytes", C.c_int64), ("device_ms", C.c_double),
                 ("n_brokers", C.c_int64), ("n_sets", C.c_int64), ("integral", C.c_int32),
-                ("max_replicas", C.c_int32)]
+                ("max_replicas", C.c_int32), ("refreshes", C.c_int64), ("exact_halts", C.c_int64),
+                ("scan_workgroups", C.c_int64)]
 
 
 _lib = None
@@ -103,7 +104,7 @@ def lib():
         L.kb_engine_step_finish.restype = C.c_int
         L.kb_engine_set_stream.argtypes = [vp, vp]
         L.kb_engine_set_stream.restype = C.c_int
-        if L.kb_abi_version() != 1:
+        if L.kb_abi_version() != 2:
             raise ImportError("libkbengine.so ABI mismatch")
         _lib = L
     return _lib
@@ -292,17 +293,17 @@ class Engine:
         lib().kb_engine_stats(self.h, C.byref(s))
         return {f: getattr(s, f) for f, _ in s._fields_}
 
-    KERNELS = ("prep", "setlists", "scan", "reduce", "census", "resolve")
+    KERNELS = ("step", "scan", "refresh")
 
     def timings(self):
         """{kernel: (total_ms, launches)} of the last plan (time_kernels=True)."""
-        ms = np.zeros(6)
-        n = np.zeros(6, np.int64)
-        lib().kb_engine_timings(self.h, ms.ctypes.data_as(PD), n.ctypes.data_as(P64), 6)
+        ms = np.zeros(3)
+        n = np.zeros(3, np.int64)
+        lib().kb_engine_timings(self.h, ms.ctypes.data_as(PD), n.ctypes.data_as(P64), 3)
         return {k: (float(ms[i]), int(n[i])) for i, k in enumerate(self.KERNELS)}
 
     def stamps(self):
-        """Diagnostic build only: accumulated phase ticks (100 MHz) of k_prep / k_resolve."""
+        """Diagnostic build only: accumulated phase ticks (100 MHz) of the k_step phases."""
         out = np.zeros(16, np.int64)
         lib().kb_engine_stamps(self.h, out.ctypes.data_as(P64), 16)
         return out.tolist()
@@ -320,10 +321,14 @@ class Engine:
             raise EngineError(rc, self.last_error())
 
     def step_finish(self, gathered_ptr, n_ranks):
+        """The merged step; None for no change, "retry" when the step must be redone
+        (its loads were refolded exactly first); raises EngineError."""
         ch = kb_change()
         rc = lib().kb_engine_step_finish(self.h, C.c_void_p(gathered_ptr), n_ranks, C.byref(ch))
         if rc == KB_NOCHANGE:
             return None
+        if rc == KB_RETRY:
+            return "retry"
         if rc == KB_CHANGE:
             return _change_dict(ch)
         raise EngineError(rc, self.last_error(), _change_dict(ch))
