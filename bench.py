@@ -128,8 +128,11 @@ def main():
         st = eng.stamps()
         n = max(1, st1["steps"])
         names = ["res.reduce", "res.pred", "res.move", "res.apply", "prep.sort+blm", "prep.loads+eps",
-                 "prep.sets"]
-        print(json.dumps({"stamps_us_per_step": {k: st[i] / 100.0 / n for i, k in enumerate(names)}}))
+                 "prep.sets", None, "scan0.prologue", "scan0.tile", "scan0.reduce", "scan0.census", "scan0.final"]
+        counts = {"spills": 7, "walks": 13, "walk_iters": 14, "emits": 15}
+        print(json.dumps({"stamps_us_per_step": {k: st[i] / 100.0 / n for i, k in enumerate(names) if k},
+                          "counts_per_step": {k: st[i] / n for k, i in counts.items()},
+                          "stats": eng.stats()}))
         return
     if not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(cl, cfg, args.cpu_seconds)

@@ -177,6 +177,10 @@ int kb_engine_timings(kb_engine *e, double *ms, int64_t *launches, int n);
  * phases [0..6]; non-zero only in a -DKB_STAMPS build. */
 int kb_engine_stamps(kb_engine *e, uint64_t *out, int n);
 
+/* Diagnostic: average device time (us) of the scan kernel over `iters`
+ * back-to-back launches on the current state (nothing is applied). */
+int kb_engine_bench_scan(kb_engine *e, int iters, double *avg_us);
+
 /* Reference-format message of the last error ("<Step>: partition Partition(t,p,[..]) ..."). */
 int kb_engine_last_error(kb_engine *e, char *buf, size_t n);
 

@@ -11,6 +11,7 @@
 #include <cfloat>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <unordered_map>
@@ -67,9 +68,9 @@ struct kb_engine {
     int32_t* nc = nullptr;
     double* load = nullptr;
     double* lerr = nullptr;
-    uint8_t* dirty = nullptr;
+    double* eb = nullptr;
+    uint8_t* bfl = nullptr;
     int32_t* cnt = nullptr;
-    uint8_t* incfg = nullptr;
     uint64_t* setbits = nullptr;
     int32_t* lists = nullptr;
     uint4* setrec = nullptr;
@@ -100,6 +101,7 @@ struct kb_engine {
     double kms[TK_N] = {0, 0, 0};
     int64_t klaunch[TK_N] = {0, 0, 0};
     int64_t refreshes = 0;
+    int dbg_scan = 0;
     std::string last_err;
 };
 
@@ -426,11 +428,14 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
     const size_t setbytes = (size_t)e->nsets * e->units * 16;
     const size_t dedup = (size_t)DEDUP_SCAN * (4 + 8 + 8);
     e->lds_sets = setbytes <= (size_t)LDS_SETS_MAX;
-    e->scan_lds = rbytes + (e->lds_sets ? setbytes : 0) + dedup;
+    const size_t pbytes = ((size_t)e->B * 2 + 15) & ~(size_t)15;
+    e->scan_lds = rbytes + 2 * pbytes + (e->lds_sets ? setbytes : 0) + dedup;
     // one wave of resident workgroups; each loops over its tiles
     int per_cu = scan_blocks_per_cu(e->rc_dev, e->lds_sets, e->scan_lds);
     if (per_cu < 1) per_cu = 1;
     e->nscan = std::min<int64_t>(e->ntiles, (int64_t)per_cu * ncu);
+    if (const char* v = getenv("KB_NSCAN")) if (atoi(v) > 0) e->nscan = std::min<int64_t>(e->ntiles, atoi(v));  // diagnostic
+    if (const char* v = getenv("KB_DEBUG_SCAN")) e->dbg_scan = atoi(v);                                   // diagnostic
     HIPCHK(hipStreamCreateWithFlags(&e->st, hipStreamNonBlocking));
     e->own_st = true;
     HIPCHK(dalloc(&e->w, e->Ppad));
@@ -439,9 +444,9 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
     HIPCHK(dalloc(&e->nc, e->Ppad));
     HIPCHK(dalloc(&e->load, e->B));
     HIPCHK(dalloc(&e->lerr, e->B));
-    HIPCHK(dalloc(&e->dirty, e->B));
+    HIPCHK(dalloc(&e->eb, e->B));
+    HIPCHK(dalloc(&e->bfl, e->B));
     HIPCHK(dalloc(&e->cnt, e->B));
-    HIPCHK(dalloc(&e->incfg, e->B));
     HIPCHK(dalloc(&e->setbits, (size_t)e->nsets * e->W64));
     HIPCHK(dalloc(&e->lists, (size_t)e->nsets * 2 * e->K));
     HIPCHK(dalloc(&e->setrec, (size_t)e->nsets * e->units));
@@ -463,12 +468,15 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
     HIPCHK(hipMemcpy(e->rep, hr.data(), hr.size() * 2, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(e->nc, hnc.data(), hnc.size() * 4, hipMemcpyHostToDevice));
     if (e->B) {
-        std::vector<uint8_t> zero(e->B, 0);
+        // flags: bit0 present (holds a replica), bit1 listed in -broker-ids (BF_* in kernels.hip)
+        std::vector<uint8_t> fl(e->B, 0);
+        for (int64_t b = 0; b < e->B; b++) fl[b] = (uint8_t)((cn[b] > 0 ? 1 : 0) | (hin[b] ? 2 : 0));
+        std::vector<double> zero(e->B, 0.0);
         HIPCHK(hipMemcpy(e->load, ld.data(), ld.size() * 8, hipMemcpyHostToDevice));
         HIPCHK(hipMemcpy(e->lerr, le.data(), le.size() * 8, hipMemcpyHostToDevice));
-        HIPCHK(hipMemcpy(e->dirty, zero.data(), zero.size(), hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(e->eb, zero.data(), zero.size() * 8, hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(e->bfl, fl.data(), fl.size(), hipMemcpyHostToDevice));
         HIPCHK(hipMemcpy(e->cnt, cn.data(), cn.size() * 4, hipMemcpyHostToDevice));
-        HIPCHK(hipMemcpy(e->incfg, hin.data(), hin.size(), hipMemcpyHostToDevice));
     }
     HIPCHK(hipMemcpy(e->bset_off, hbo.data(), hbo.size() * 4, hipMemcpyHostToDevice));
     if (!hbi.empty()) HIPCHK(hipMemcpy(e->bset_ids, hbi.data(), hbi.size() * 4, hipMemcpyHostToDevice));
@@ -508,6 +516,7 @@ static void fill_scan_args(kb_engine* e, ScanArgs& s) {
     s.allow_leader = e->allow_leader; s.rebalance = e->rebalance; s.sem_go = e->sem == KB_SEM_GO;
     s.recs = e->recs; s.cont = e->cont; s.cont_cap = e->cont_cap;
     s.listwg = e->integral ? 0 : 1;
+    s.dbg = e->dbg_scan;
     s.L = e->L;
 }
 
@@ -518,7 +527,7 @@ static void fill_step_args(kb_engine* e, StepArgs& a, const unsigned char* recs,
     a.nsets = (int)e->nsets; a.NP2 = e->NP2;
     a.setbits = e->setbits; a.setrec = e->setrec; a.lists = e->lists;
     a.order = e->order; a.posu = e->posu; a.blm = e->blm; a.posm = e->posm; a.r = e->r;
-    a.load = e->load; a.lerr = e->lerr; a.dirty = e->dirty; a.cnt = e->cnt; a.incfg = e->incfg;
+    a.load = e->load; a.lerr = e->lerr; a.eb = e->eb; a.bfl = e->bfl; a.cnt = e->cnt;
     a.bset_off = e->bset_off; a.bset_ids = e->bset_ids;
     a.recs = recs; a.nrec = nrec; a.rec_stride = stride; a.rec_keys = keys;
     a.cont = e->cont; a.cont_cap = e->cont_cap; a.use_spill = use_spill;
@@ -588,7 +597,7 @@ static int refresh(kb_engine* e) {
     launch_listop(e->ctl, e->L, e->st);
     RefreshArgs ra;
     ra.ctl = e->ctl; ra.w = e->w; ra.rep = e->rep; ra.meta = e->meta; ra.nc = e->nc;
-    ra.load = e->load; ra.lerr = e->lerr; ra.dirty = e->dirty; ra.cnt = e->cnt; ra.B = (int)e->B;
+    ra.load = e->load; ra.lerr = e->lerr; ra.eb = e->eb; ra.bfl = e->bfl; ra.B = (int)e->B;
     ra.L = e->L;
     mark(e, TK_REFRESH);
     launch_refresh(ra, e->st);
@@ -784,13 +793,11 @@ extern "C" double kb_engine_unbalance(kb_engine* e) {
     if (!e || e->B == 0) return 0.0;
     if (make_exact(e) != KB_OK) return NAN;
     std::vector<double> ld(e->B);
-    std::vector<int32_t> cn(e->B);
-    std::vector<uint8_t> in(e->B);
+    std::vector<uint8_t> fl(e->B);
     hipMemcpy(ld.data(), e->load, e->B * 8, hipMemcpyDeviceToHost);
-    hipMemcpy(cn.data(), e->cnt, e->B * 4, hipMemcpyDeviceToHost);
-    hipMemcpy(in.data(), e->incfg, e->B, hipMemcpyDeviceToHost);
+    hipMemcpy(fl.data(), e->bfl, e->B, hipMemcpyDeviceToHost);
     std::vector<int> bl;
-    for (int64_t b = 0; b < e->B; b++) if (cn[b] > 0 || in[b]) bl.push_back((int)b);
+    for (int64_t b = 0; b < e->B; b++) if (fl[b] & 3) bl.push_back((int)b);
     std::sort(bl.begin(), bl.end(), [&](int x, int y) { return ld[x] != ld[y] ? ld[x] < ld[y] : x < y; });
     double S = 0;
     for (int b : bl) S += ld[b];
@@ -840,6 +847,35 @@ extern "C" int kb_engine_stamps(kb_engine* e, uint64_t* out, int n) {
     return 16;
 }
 
+// Diagnostic: average device time of k_scan over `iters` back-to-back launches on
+// the current prepped state (the scan only writes its records and spill buffer).
+extern "C" int kb_engine_bench_scan(kb_engine* e, int iters, double* avg_us) {
+    if (!e || iters < 1 || !avg_us) return KB_ERR_INVALID;
+    if (e->pending) return e->pending;
+    if (reset_ctl(e, 1) != KB_OK) return KB_ERR_HIP;
+    if (!e->h_ctl->prepped) {
+        enqueue_step(e);                              // prep only
+        HIPCHK(hipStreamSynchronize(e->st));
+    }
+    hipEvent_t a, b;
+    HIPCHK(hipEventCreate(&a));
+    HIPCHK(hipEventCreate(&b));
+    enqueue_scan(e);                                  // warm
+    HIPCHK(hipEventRecord(a, e->st));
+    for (int i = 0; i < iters; i++) enqueue_scan(e);
+    HIPCHK(hipEventRecord(b, e->st));
+    HIPCHK(hipEventSynchronize(b));
+    float ms = 0;
+    hipEventElapsedTime(&ms, a, b);
+    *avg_us = 1e3 * ms / iters;
+    hipEventDestroy(a);
+    hipEventDestroy(b);
+    // forget the spills of the repeated scans
+    HIPCHK(hipMemsetAsync(&e->ctl->ncont, 0, 8, e->st));
+    HIPCHK(hipStreamSynchronize(e->st));
+    return KB_OK;
+}
+
 extern "C" int kb_engine_last_error(kb_engine* e, char* buf, size_t n) {
     if (!e || !buf || n == 0) return KB_ERR_INVALID;
     snprintf(buf, n, "%s", e->last_err.c_str());
@@ -848,7 +884,7 @@ extern "C" int kb_engine_last_error(kb_engine* e, char* buf, size_t n) {
 
 extern "C" void kb_engine_destroy(kb_engine* e) {
     if (!e) return;
-    void* ptrs[] = {e->w, e->rep, e->meta, e->nc, e->load, e->lerr, e->dirty, e->cnt, e->incfg,
+    void* ptrs[] = {e->w, e->rep, e->meta, e->nc, e->load, e->lerr, e->eb, e->bfl, e->cnt,
                     e->setbits, e->lists, e->setrec, e->order, e->posu, e->blm, e->posm, e->r,
                     e->bset_off, e->bset_ids, e->recs, e->cont, e->ctl, e->log,
                     e->L.lstart, e->L.llen, e->L.lcap, e->L.lent};

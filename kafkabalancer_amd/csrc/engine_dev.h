@@ -8,8 +8,8 @@ namespace kbe {
 constexpr int MAXB = 4096;          // dense broker universe limit (sorted in LDS)
 constexpr int MAXR = 16;            // replica slots per partition
 constexpr int SCAN_THREADS = 512;   // k_scan workgroup
-constexpr int PER_LANE = 4;         // consecutive partitions per lane (vector loads)
-constexpr int TILE = SCAN_THREADS * PER_LANE;   // 2048 partitions per scan tile
+constexpr int PER_LANE = 2;         // consecutive partitions per lane (vector loads)
+constexpr int TILE = SCAN_THREADS * PER_LANE;   // 1024 partitions per scan tile
 constexpr int SHARD_ALIGN = 1024;   // shard boundaries (multi-GPU) are multiples of this
 constexpr int STEP_THREADS = 1024;  // k_step: one workgroup
 constexpr uint32_t NONE32 = 0xFFFFFFFFu;
@@ -96,6 +96,7 @@ struct DevCtl {
     int32_t prepped, budget, full_prep, want_refresh;
     int32_t nblm, heavy, light, ndirty;
     double S, avg, inv_avg, U0, eps, V, E;
+    double ub[2];                   // upper bound of the next step's minimum score delta per kind
     uint32_t ncont, cont_overflow;  // raw near-tie spill buffer (scan -> step)
     int32_t list_overflow, pending_list;
     int32_t pl_kind, pl_from, pl_to, pl_pad;  // pending per-broker list operation
@@ -117,9 +118,11 @@ struct DevCtl {
             _kb_t0 = _t;                                                        \
         }                                                                       \
     } while (0)
+#define KB_COUNT(ctl, i, v) atomicAdd(&(ctl)->stamps[i], (unsigned long long)(v))
 #else
 #define KB_STAMP_BEGIN() (void)0
 #define KB_STAMP(ctl, i) (void)0
+#define KB_COUNT(ctl, i, v) (void)0
 #endif
 
 // errors recorded in ChangeDev.err_code

@@ -92,14 +92,6 @@ __device__ __forceinline__ uint32_t rec_u16(const uint4* v, int idx) {
 // gamma_n bound of a sequential n-term fold of non-negative terms (|fold - sum| <= gamma_n * sum)
 __device__ __forceinline__ double gamma_n(int n) { return 1.01 * (double)(n > 1 ? n : 1) * (DBL_EPSILON / 2); }
 
-// error bound of an approximate (dirty) load against the reference's fold
-__device__ __forceinline__ double load_err(const double* load, const double* lerr, const uint8_t* dirty,
-                                           const int32_t* cnt, int b) {
-    if (!dirty[b]) return 0.0;
-    const double a = lerr[b];
-    return a + gamma_n(cnt[b]) * (load[b] + a);
-}
-
 // Sequential fold of n doubles held in LDS, in order (the reference's fold).
 // Loads are batched 16 at a time so the dependent add chain, not LDS latency,
 // sets the pace.
@@ -279,6 +271,8 @@ __device__ void do_list_op(DevCtl* ctl, const Lists& L, int* s_i) {
 
 // --------------------------------------------------------------- k_scan
 
+static_assert(PER_LANE == 2, "the scan's register layout assumes two partitions per lane");
+
 template <int RC>
 struct PartRegs {
     double w[PER_LANE];
@@ -286,18 +280,18 @@ struct PartRegs {
     uint32_t r[RC][PER_LANE];
 };
 
+// two consecutive partitions per lane: one 16-B weight load, one 8-B meta load
+// and one 4-B load per replica slot (coalesced across the wave)
 template <int RC>
 __device__ __forceinline__ void load_parts(const ScanArgs& a, long long base, PartRegs<RC>& P) {
-    const double2 w01 = *(const double2*)(a.w + base);
-    const double2 w23 = *(const double2*)(a.w + base + 2);
-    P.w[0] = w01.x; P.w[1] = w01.y; P.w[2] = w23.x; P.w[3] = w23.y;
-    const uint4 m4 = *(const uint4*)(a.meta + base);
-    P.m[0] = m4.x; P.m[1] = m4.y; P.m[2] = m4.z; P.m[3] = m4.w;
+    const double2 w2 = *(const double2*)(a.w + base);
+    P.w[0] = w2.x; P.w[1] = w2.y;
+    const uint2 m2 = *(const uint2*)(a.meta + base);
+    P.m[0] = m2.x; P.m[1] = m2.y;
 #pragma unroll
     for (int k = 0; k < RC; k++) {
-        const uint2 r2 = *(const uint2*)(a.rep + (long long)k * a.Ppad + base);
-        P.r[k][0] = r2.x & 0xFFFFu; P.r[k][1] = r2.x >> 16;
-        P.r[k][2] = r2.y & 0xFFFFu; P.r[k][3] = r2.y >> 16;
+        const uint32_t r2 = *(const uint32_t*)(a.rep + (long long)k * a.Ppad + base);
+        P.r[k][0] = r2 & 0xFFFFu; P.r[k][1] = r2 >> 16;
     }
 }
 
@@ -309,7 +303,9 @@ __device__ __forceinline__ void emit_global(DevCtl* ctl, Contender* cont, uint32
 
 __device__ __forceinline__ void emit(const ScanArgs& a, const Dedup& T, int kind, int s, int t, double w,
                                      unsigned long long iter) {
+    KB_COUNT(a.ctl, 15, 1);
     if (dedup_insert(T, kind, s, t, w, iter) < 0) {   // table full or weight conflict: spill it raw
+        KB_COUNT(a.ctl, 7, 1);
         Contender c;
         c.s = s; c.t = t; c.w = w; c.iter = iter; c.kind = kind; c.pad = 0;
         emit_global(a.ctl, a.cont, a.cont_cap, c);
@@ -320,29 +316,33 @@ __device__ __forceinline__ void emit(const ScanArgs& a, const Dedup& T, int kind
 // and emit the ones within 4*eps of the tile minimum g; stop once 8*eps is
 // exceeded (the approximate delta is monotone in the target load up to 2*eps).
 template <int RC>
-__device__ void walk_targets(const ScanArgs& a, const Dedup& T, const double* s_r, const uint16_t* rec16,
-                             int kind, long long p, int slot, int src, const uint32_t (&reps)[RC], int nrep,
-                             int set, double w, double ds, double g, double eps, double inv_avg, int nblm) {
+__device__ void walk_targets(const ScanArgs& a, const Dedup& T, const double* s_r, const int16_t* s_pos,
+                             const uint16_t* s_blm, const uint16_t* rec16, int kind, long long p, int slot, int src,
+                             const uint32_t (&reps)[RC], int nrep, int set, double w, double ds, double g,
+                             double eps, double inv_avg, int nblm) {
     constexpr int KR = sr_kr(RC);
     const unsigned long long ib = ((unsigned long long)p << 21) | ((unsigned long long)slot << 16);
     const double delta = w * inv_avg;
     const int nl = rec16[1];
     int last = -1;
+    KB_COUNT(a.ctl, 13, 1);
     for (int i = 0; i < nl; i++) {                // the set's first KR eligible brokers
         const int b = rec16[2 + i];
+        KB_COUNT(a.ctl, 14, 1);
         last = b;
         bool isrep = false;
 #pragma unroll
         for (int q = 0; q < RC; q++) isrep |= (q < nrep) && ((int)reps[q] == b);
         if (isrep) continue;
         const double d = ds + dtgt(s_r[b], delta);
-        if (d <= g + 4.0 * eps) emit(a, T, kind, src, b, w, ib | (unsigned long long)a.posm[b]);
+        if (d <= g + 4.0 * eps) emit(a, T, kind, src, b, w, ib | (unsigned long long)s_pos[b]);
         if (d > g + 8.0 * eps) return;
     }
     if (nl < KR || last < 0) return;              // the set is exhausted
     const uint64_t* sb = a.setbits + (size_t)set * a.W64;
-    for (int k = a.posm[last] + 1; k < nblm; k++) {   // rare: more than KR near-tied targets
-        const int b = a.blm[k];
+    for (int k = s_pos[last] + 1; k < nblm; k++) {   // rare: more than KR near-tied targets
+        KB_COUNT(a.ctl, 0, 1);
+        const int b = s_blm[k];
         if (!setbit(sb, b)) continue;
         bool isrep = false;
 #pragma unroll
@@ -378,49 +378,14 @@ __device__ __forceinline__ int first_target(const ScanArgs& a, const uint4* s_se
     return tb;
 }
 
-// the lane's slots within 8*eps of the tile minima: rescore and walk their targets
-template <int RC, bool LSETS>
-__device__ __forceinline__ void census(const ScanArgs& a, const Dedup& T, const double* s_r, const uint4* s_set,
-                                       long long base, bool wl, bool wn, double tL,
-                                       double tN, double eps, double inv_avg, int nblm) {
-    constexpr int U = sr_units(RC);
-#pragma unroll 1
-    for (int j = 0; j < PER_LANE; j++) {
-        const long long p = base + j;
-        if (p >= a.shard_end) continue;
-        // re-read the partition (rare path: keeps the stream's registers out of scratch)
-        const uint32_t m = a.meta[p];
-        const int nrep = (int)meta_nrep(m), set = (int)meta_set(m);
-        if (!meta_elig(m) || nrep == 0) continue;
-        uint32_t reps[RC];
-#pragma unroll
-        for (int k = 0; k < RC; k++) reps[k] = a.rep[(long long)k * a.Ppad + p];
-        int nelig;
-        const int tb = first_target<RC, LSETS>(a, s_set, m, reps, nrep, &nelig);
-        if (tb < 0) continue;
-        const uint16_t* rec16 = LSETS ? (const uint16_t*)(s_set + (size_t)set * U)
-                                      : (const uint16_t*)(a.setrec + (size_t)set * U);
-        const double w = a.w[p];
-        const double delta = w * inv_avg;
-        const double dt = dtgt(s_r[tb], delta);
-        if (wl && a.allow_leader) {
-            const double ds = dsrc(s_r[reps[0]], delta);
-            if (ds + dt <= tL + 8.0 * eps)
-                walk_targets<RC>(a, T, s_r, rec16, 0, p, 0, (int)reps[0], reps, nrep, set, w, ds, tL, eps,
-                                 inv_avg, nblm);
-        }
-        if (wn)
-#pragma unroll 1
-            for (int k = 1; k < nrep; k++) {
-                uint32_t src = reps[0];
-#pragma unroll
-                for (int q = 1; q < RC; q++) src = k == q ? reps[q] : src;
-                const double ds = dsrc(s_r[src], delta);
-                if (ds + dt <= tN + 8.0 * eps)
-                    walk_targets<RC>(a, T, s_r, rec16, 1, p, k, (int)src, reps, nrep, set, w, ds, tN, eps,
-                                     inv_avg, nblm);
-            }
-    }
+// order-preserving encoding of a double into u64 (LDS atomicMin of a minimum)
+__device__ __forceinline__ unsigned long long enc(double d) {
+    unsigned long long u = d2u(d);
+    return (u >> 63) ? ~u : (u | 0x8000000000000000ull);
+}
+__device__ __forceinline__ double dec(unsigned long long e) {
+    unsigned long long u = (e >> 63) ? (e & 0x7FFFFFFFFFFFFFFFull) : ~e;
+    return u2d(u);
 }
 
 template <int RC, bool LSETS>
@@ -429,35 +394,45 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
     __shared__ int s_i;
     DevCtl* ctl = a.ctl;
     if (a.listwg && (int)blockIdx.x == a.nscan) { do_list_op(ctl, a.L, &s_i); return; }
-    if (ctl->halted != H_RUN || !ctl->prepped || ctl->steps >= ctl->budget) return;
     constexpr int U = sr_units(RC);
     constexpr int NW = SCAN_THREADS / 64;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const double inv_avg = ctl->inv_avg, eps = ctl->eps;
-    const int heavy = ctl->heavy, nblm = ctl->nblm;
+    KB_STAMP_BEGIN();
 
     double* s_r = (double*)smem;
     const size_t rbytes = ((size_t)a.B * 8 + 15) & ~(size_t)15;
-    uint4* s_set = (uint4*)(smem + rbytes);
+    int16_t* s_pos = (int16_t*)(smem + rbytes);
+    const size_t pbytes = ((size_t)a.B * 2 + 15) & ~(size_t)15;
+    uint16_t* s_blm = (uint16_t*)(smem + rbytes + pbytes);
+    uint4* s_set = (uint4*)(smem + rbytes + 2 * pbytes);
     const size_t setbytes = LSETS ? (size_t)a.nsets * U * 16 : 0;
-    uint32_t* s_key = (uint32_t*)(smem + rbytes + setbytes);
+    uint32_t* s_key = (uint32_t*)(smem + rbytes + 2 * pbytes + setbytes);
     unsigned long long* s_wb = (unsigned long long*)(s_key + DEDUP_SCAN);
     unsigned long long* s_it = s_wb + DEDUP_SCAN;
     Dedup T{s_key, s_wb, s_it, DEDUP_SCAN};
-    __shared__ double s_red[2][NW];
     __shared__ uint32_t s_f[NF][NW];
     __shared__ unsigned long long s_c[2][NW];
     __shared__ uint32_t s_nk;
 
+    // every load that does not depend on the control block goes out first: the
+    // first tile's stream, then the lookup tables (one memory round trip)
     int tile = blockIdx.x;
     PartRegs<RC> P;
-    // issue the first tile's stream before staging the lookup tables
     if (tile < a.ntiles) load_parts<RC>(a, a.shard_begin + (long long)tile * TILE + (long long)tid * PER_LANE, P);
-    for (int i = tid; i < a.B; i += SCAN_THREADS) s_r[i] = a.r[i];
+    for (int i = tid; i < a.B; i += SCAN_THREADS) {
+        s_r[i] = a.r[i];
+        s_pos[i] = (int16_t)a.posm[i];
+        s_blm[i] = (uint16_t)a.blm[i];
+    }
     if (LSETS) for (int i = tid; i < a.nsets * U; i += SCAN_THREADS) s_set[i] = a.setrec[i];
     for (int i = tid; i < DEDUP_SCAN; i += SCAN_THREADS) { s_key[i] = NONE32; s_wb[i] = NONE64; s_it[i] = NONE64; }
     if (tid == 0) s_nk = 0;
+    const bool run = ctl->halted == H_RUN && ctl->prepped && ctl->steps < ctl->budget;
+    const double inv_avg = ctl->inv_avg, eps = ctl->eps;
+    const double ubL = ctl->ub[0], ubN = ctl->ub[1];
+    const int heavy = ctl->heavy, nblm = ctl->nblm;
     __syncthreads();
+    if (!run) return;
 
     double wgL = HUGE_VAL, wgN = HUGE_VAL;
     uint32_t fst[NF];
@@ -465,10 +440,13 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
     for (int f = 0; f < NF; f++) fst[f] = NONE32;
     unsigned long long cL = 0, cN = 0;
 
-    for (bool first = true; tile < a.ntiles; tile += a.nscan, first = false) {
+    for (int it = 0; tile < a.ntiles; tile += a.nscan, it++) {
         const long long base = a.shard_begin + (long long)tile * TILE + (long long)tid * PER_LANE;
-        if (!first) load_parts<RC>(a, base, P);
-        // lane minima only: the per-slot scores are recomputed by the (rare) census
+        // prefetch the next tile: its loads stay in flight while this one is scored
+        PartRegs<RC> Pn;
+        const bool more = tile + a.nscan < a.ntiles;
+        if (more) load_parts<RC>(a, base + (long long)a.nscan * TILE, Pn);
+        // lane minima of the leader / non-leader slot scores
         double lL = HUGE_VAL, lN = HUGE_VAL;
 #pragma unroll
         for (int j = 0; j < PER_LANE; j++) {
@@ -505,46 +483,90 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
             const double dt = dtgt(s_r[tb], delta);
             const unsigned long long ne = (unsigned long long)(nelig - (int)meta_nin(m));
             if (a.allow_leader) {
-                const double d = dsrc(s_r[P.r[0][j]], delta) + dt;
+                const double d = dsrc(s_r[reps[0]], delta) + dt;
                 lL = d < lL ? d : lL;
                 cL += ne;
             }
 #pragma unroll
             for (int k = 1; k < RC; k++)
                 if (k < nrep) {
-                    const double d = dsrc(s_r[P.r[k][j]], delta) + dt;
+                    const double d = dsrc(s_r[reps[k]], delta) + dt;
                     lN = d < lN ? d : lN;
                 }
             cN += ne * (unsigned long long)(nrep - 1);
         }
-        // tile minimum: wave shuffles, then LDS across the waves
-        double tL = wave_min(lL), tN = wave_min(lN);
-        if (lane == 0) { s_red[0][wid] = tL; s_red[1][wid] = tN; }
-        __syncthreads();
+        // wave minima; the census runs only where a wave minimum can be within 8*eps
+        // of the step's global minimum, which is at most ub (k_step's upper bound)
+        const double tL = wave_min(lL), tN = wave_min(lN);
+        // (g <= ub + 2*eps: the first-target score is monotone in the target up to 2*eps)
+        const bool hasL = tL < HUGE_VAL && tL <= ubL + 12.0 * eps;
+        const bool hasN = tN < HUGE_VAL && tN <= ubN + 12.0 * eps;
+        if (!(a.dbg & 1) && ((hasL && lL <= tL + 8.0 * eps) || (hasN && lN <= tN + 8.0 * eps))) {
+            // the (partition, slot) pairs within 8*eps of the tile minimum, as bits j*16 + slot
+            uint32_t todo = 0;
 #pragma unroll
-        for (int x = 0; x < NW; x++) {
-            tL = s_red[0][x] < tL ? s_red[0][x] : tL;
-            tN = s_red[1][x] < tN ? s_red[1][x] : tN;
+            for (int j = 0; j < PER_LANE; j++) {
+                const uint32_t m = P.m[j];
+                const int nrep = (int)meta_nrep(m);
+                if (base + j >= a.shard_end || !meta_elig(m) || nrep == 0) continue;
+                uint32_t reps[RC];
+#pragma unroll
+                for (int k = 0; k < RC; k++) reps[k] = P.r[k][j];
+                int nelig;
+                const int tb = first_target<RC, LSETS>(a, s_set, m, reps, nrep, &nelig);
+                if (tb < 0) continue;
+                const double delta = P.w[j] * inv_avg;
+                const double dt = dtgt(s_r[tb], delta);
+                if (hasL && a.allow_leader && dsrc(s_r[reps[0]], delta) + dt <= tL + 8.0 * eps)
+                    todo |= 1u << (j * 16);
+#pragma unroll
+                for (int k = 1; k < RC; k++)
+                    if (hasN && k < nrep && dsrc(s_r[reps[k]], delta) + dt <= tN + 8.0 * eps)
+                        todo |= 1u << (j * 16 + k);
+            }
+            // one walk call site (a compact, rarely executed code path)
+            while (todo) {
+                const int bit = __ffs(todo) - 1;
+                todo &= todo - 1;
+                const int j = bit >> 4, k = bit & 15;
+                const uint32_t m = j ? P.m[1] : P.m[0];
+                const double w = j ? P.w[1] : P.w[0];
+                uint32_t reps[RC];
+#pragma unroll
+                for (int q = 0; q < RC; q++) reps[q] = j ? P.r[q][1] : P.r[q][0];
+                uint32_t src = reps[0];
+#pragma unroll
+                for (int q = 1; q < RC; q++) src = k == q ? reps[q] : src;
+                const int nrep = (int)meta_nrep(m), set = (int)meta_set(m);
+                const uint16_t* rec16 = LSETS ? (const uint16_t*)(s_set + (size_t)set * U)
+                                              : (const uint16_t*)(a.setrec + (size_t)set * U);
+                const double ds = dsrc(s_r[src], w * inv_avg);
+                walk_targets<RC>(a, T, s_r, s_pos, s_blm, rec16, k ? 1 : 0, base + j, k, (int)src, reps, nrep, set, w, ds,
+                                 k ? tN : tL, eps, inv_avg, nblm);
+            }
         }
-        __syncthreads();
-        // near-tie census against the tile minimum (usually one slot per tile)
-        const bool wl = tL < HUGE_VAL && lL <= tL + 8.0 * eps;
-        const bool wn = tN < HUGE_VAL && lN <= tN + 8.0 * eps;
-        if (wl || wn) census<RC, LSETS>(a, T, s_r, s_set, base, wl, wn, tL, tN, eps, inv_avg, nblm);
         wgL = tL < wgL ? tL : wgL;
         wgN = tN < wgN ? tN : wgN;
+        if (more) P = Pn;
     }
     // workgroup record: counts, first-index predicates, minima, near-tie keys
     cL = wave_sum(cL);
     cN = wave_sum(cN);
 #pragma unroll
     for (int f = 0; f < NF; f++) fst[f] = wave_min(fst[f]);
+    __shared__ double s_wm[2][NW];
     if (lane == 0) {
         s_c[0][wid] = cL; s_c[1][wid] = cN;
+        s_wm[0][wid] = wgL; s_wm[1][wid] = wgN;
 #pragma unroll
         for (int f = 0; f < NF; f++) s_f[f][wid] = fst[f];
     }
     __syncthreads();   // also orders every census insert before the flush
+#pragma unroll
+    for (int x = 0; x < NW; x++) {
+        wgL = s_wm[0][x] < wgL ? s_wm[0][x] : wgL;
+        wgN = s_wm[1][x] < wgN ? s_wm[1][x] : wgN;
+    }
     RecHdr* hdr = (RecHdr*)(a.recs + (size_t)blockIdx.x * WGREC_BYTES);
     Contender* keys = (Contender*)(hdr + 1);
     for (int h = tid; h < DEDUP_SCAN; h += SCAN_THREADS) {
@@ -585,10 +607,24 @@ struct Decision {
     int32_t exact, err, err_broker, pad;
 };
 
+// broker flags (bfl / s_fl)
+constexpr uint8_t BF_PRESENT = 1, BF_INCFG = 2, BF_DIRTY = 4, BF_TOUCHED = 8;
+
+// the relative load the prep wrote to r[] for a bl_move broker, recomputed
+// bit-identically from the load (same operands, same fused operation)
+__device__ __forceinline__ double rel_ld(const double* s_ld, int b, double inv_avg) {
+    return __fma_rn(s_ld[b], inv_avg, -1.0);
+}
+__device__ __forceinline__ double cont_delta_ld(const double* s_ld, const Contender& c, double inv_avg) {
+    const double delta = c.w * inv_avg;
+    return dsrc(rel_ld(s_ld, c.s, inv_avg), delta) + dtgt(rel_ld(s_ld, c.t, inv_avg), delta);
+}
+
 // every near-tie contender of `kind` within 4*eps of g: the keys of the
 // records whose minimum is within 8*eps, then the raw spill buffer
 template <typename F>
-__device__ void for_each_contender(const StepArgs& a, int kind, double g, double eps, double inv_avg, F f) {
+__device__ void for_each_contender(const StepArgs& a, const double* s_ld, int kind, double g, double eps,
+                                   double inv_avg, F f) {
     const int nt = blockDim.x;
     for (int i = threadIdx.x; i < a.nrec; i += nt) {
         const RecHdr* h = (const RecHdr*)(a.recs + (size_t)i * a.rec_stride);
@@ -598,7 +634,7 @@ __device__ void for_each_contender(const StepArgs& a, int kind, double g, double
         for (int k = 0; k < nk; k++) {
             const Contender c = keys[k];
             if (c.kind != kind) continue;
-            if (cont_delta(a.r, c, inv_avg) <= g + 4.0 * eps) f(c);
+            if (cont_delta_ld(s_ld, c, inv_avg) <= g + 4.0 * eps) f(c);
         }
     }
     if (a.use_spill) {
@@ -606,20 +642,19 @@ __device__ void for_each_contender(const StepArgs& a, int kind, double g, double
         for (uint32_t i = threadIdx.x; i < n; i += nt) {
             const Contender c = a.cont[i];
             if (c.kind != kind) continue;
-            if (cont_delta(a.r, c, inv_avg) <= g + 4.0 * eps) f(c);
+            if (cont_delta_ld(s_ld, c, inv_avg) <= g + 4.0 * eps) f(c);
         }
     }
 }
 
 __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
     DevCtl* ctl = a.ctl;
-    if (ctl->halted != H_RUN) return;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     constexpr int NW = STEP_THREADS / 64;
     __shared__ Decision D;
     __shared__ int s_done, s_i, s_fail, s_ndist, s_exact_need, s_nT, s_unc, s_nblm;
     __shared__ unsigned long long s_u[NW];
-    __shared__ double s_dv[NW], s_dv2[NW], s_dv3[NW];
+    __shared__ double s_dv[NW];
     __shared__ int s_bs[NW], s_bt[NW];
     __shared__ double s_bw[NW];
     __shared__ double s_g[2];
@@ -629,68 +664,89 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
     __shared__ double s_sux;
     __shared__ uint32_t s_key[DEDUP_STEP];
     __shared__ unsigned long long s_wb[DEDUP_STEP], s_it[DEDUP_STEP];
-    __shared__ double s_ld[MAXB];                    // loads (by id) / exact loads in bl order
-    __shared__ unsigned long long s_k64[MAXB];       // sort keys
-    __shared__ int32_t s_ord[MAXB];                  // universe order
-    __shared__ int32_t s_ord2[MAXB];
-    __shared__ uint8_t s_tm[MAXB];                   // touched-broker marks
-    __shared__ int s_T[TMAX];
-    __shared__ int s_cntT[TMAX], s_posT[TMAX];
+    __shared__ double s_ld[MAXB];                    // loads by broker id
+    __shared__ double s_e[MAXB];                     // load error bounds; zero whenever every load is
+                                                     // exact, so then also sort keys / exact bl loads
+    __shared__ int32_t s_ord[MAXB];                  // universe order by (load, id)
+    __shared__ uint8_t s_fl[MAXB];                   // BF_* flags
+    __shared__ int s_T[TMAX], s_posT[TMAX];
+    __shared__ int s_cntT[TMAX];
     __shared__ uint64_t s_blmb[MAXB / 64], s_presb[MAXB / 64];
     __shared__ uint32_t s_smark[MAX_SETS / 32];
     Dedup T{s_key, s_wb, s_it, DEDUP_STEP};
-    const double eps = ctl->eps, inv_avg = ctl->inv_avg, U0h = ctl->U0;
-    const int nblm0 = ctl->nblm;
+    const int B = a.B;
     KB_STAMP_BEGIN();
 
-    if (tid == 0) { s_nT = 0; s_done = 0; s_exact_need = 0; }
+    // ---- one memory round trip: the broker state, the scan records, the control block
+    for (int b = tid; b < B; b += STEP_THREADS) {
+        s_ld[b] = a.load[b];
+        s_e[b] = a.eb[b];
+        s_fl[b] = a.bfl[b];
+        s_ord[b] = a.order[b];
+    }
+    double d0 = HUGE_VAL, d1 = HUGE_VAL;
+    unsigned long long c0 = 0, c1 = 0;
+    uint32_t f[NF];
+#pragma unroll
+    for (int q = 0; q < NF; q++) f[q] = NONE32;
+    uint32_t flg = 0;
+    for (int i = tid; i < a.nrec; i += STEP_THREADS) {
+        const RecHdr* h = (const RecHdr*)(a.recs + (size_t)i * a.rec_stride);
+        d0 = h->dmin[0] < d0 ? h->dmin[0] : d0;
+        d1 = h->dmin[1] < d1 ? h->dmin[1] : d1;
+        c0 += h->cand[0]; c1 += h->cand[1];
+#pragma unroll
+        for (int q = 0; q < NF; q++) f[q] = min(f[q], h->first[q]);
+        flg |= h->flags;
+    }
+    const int halted = ctl->halted;
     const bool do_res = ctl->prepped && ctl->steps < ctl->budget;
+    const double eps = ctl->eps, inv_avg = ctl->inv_avg, U0h = ctl->U0;
+    const int nblm0 = ctl->nblm, ndirty0 = ctl->ndirty;
+    const bool pend = ctl->pending_list != 0;
+    __shared__ long long s_moved;
+    if (tid == 0) { s_nT = 0; s_done = 0; s_exact_need = 0; s_moved = -1; }
+    if (halted != H_RUN) return;
     __syncthreads();
 
     // ================================================================ resolve
     if (do_res) {
-        if (ctl->pending_list) do_list_op(ctl, a.L, &s_i);   // not consumed by a scan: do it here
-        // ---- combine the scan records (or the gathered rank summaries)
-        double d0 = HUGE_VAL, d1 = HUGE_VAL;
-        unsigned long long c0 = 0, c1 = 0;
-        uint32_t f[NF];
-#pragma unroll
-        for (int q = 0; q < NF; q++) f[q] = NONE32;
-        uint32_t flg = 0;
-        for (int i = tid; i < a.nrec; i += STEP_THREADS) {
-            const RecHdr* h = (const RecHdr*)(a.recs + (size_t)i * a.rec_stride);
-            d0 = h->dmin[0] < d0 ? h->dmin[0] : d0;
-            d1 = h->dmin[1] < d1 ? h->dmin[1] : d1;
-            c0 += h->cand[0]; c1 += h->cand[1];
-#pragma unroll
-            for (int q = 0; q < NF; q++) f[q] = min(f[q], h->first[q]);
-            flg |= h->flags;
-        }
+        if (pend) do_list_op(ctl, a.L, &s_i);   // not consumed by a scan: do it here
+        // ---- combine the scan records (or the gathered rank summaries): every value
+        // reduced across the wave at once, then across the waves by wave 0
         d0 = wave_min(d0); d1 = wave_min(d1); c0 = wave_sum(c0); c1 = wave_sum(c1);
 #pragma unroll
         for (int q = 0; q < NF; q++) f[q] = wave_min(f[q]);
-        for (int o = 32; o > 0; o >>= 1) flg |= __shfl_xor(flg, o);
-        if (lane == 0) { s_dv[wid] = d0; s_dv2[wid] = d1; s_u[wid] = c0; s_bw[wid] = 0; s_bs[wid] = (int)flg; }
-        if (lane == 0) s_bt[wid] = 0;
-        __shared__ unsigned long long s_c1w[NW];
-        __shared__ uint32_t s_fw[NF][NW];
-        if (lane == 0) {
-            s_c1w[wid] = c1;
 #pragma unroll
-            for (int q = 0; q < NF; q++) s_fw[q][wid] = f[q];
+        for (int o = 32; o > 0; o >>= 1) flg |= __shfl_xor(flg, o);
+        __shared__ double s_pd[2][NW];
+        __shared__ unsigned long long s_pc[2][NW];
+        __shared__ uint32_t s_pf[NF + 1][NW];
+        if (lane == 0) {
+            s_pd[0][wid] = d0; s_pd[1][wid] = d1; s_pc[0][wid] = c0; s_pc[1][wid] = c1;
+#pragma unroll
+            for (int q = 0; q < NF; q++) s_pf[q][wid] = f[q];
+            s_pf[NF][wid] = flg;
         }
         __syncthreads();
-        if (tid == 0) {
-            for (int x = 1; x < NW; x++) {
-                d0 = s_dv[x] < d0 ? s_dv[x] : d0;
-                d1 = s_dv2[x] < d1 ? s_dv2[x] : d1;
-                c0 += s_u[x]; c1 += s_c1w[x];
-                flg |= (uint32_t)s_bs[x];
-                for (int q = 0; q < NF; q++) f[q] = min(f[q], s_fw[q][x]);
+        if (wid == 0) {
+            const bool in = lane < NW;
+            d0 = in ? s_pd[0][lane] : HUGE_VAL; d1 = in ? s_pd[1][lane] : HUGE_VAL;
+            c0 = in ? s_pc[0][lane] : 0ull; c1 = in ? s_pc[1][lane] : 0ull;
+#pragma unroll
+            for (int q = 0; q < NF; q++) f[q] = in ? s_pf[q][lane] : NONE32;
+            flg = in ? s_pf[NF][lane] : 0u;
+            d0 = wave_min(d0); d1 = wave_min(d1); c0 = wave_sum(c0); c1 = wave_sum(c1);
+#pragma unroll
+            for (int q = 0; q < NF; q++) f[q] = wave_min(f[q]);
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) flg |= __shfl_xor(flg, o);
+            if (lane == 0) {
+                s_g[0] = d0; s_g[1] = d1; s_cand[0] = c0; s_cand[1] = c1;
+#pragma unroll
+                for (int q = 0; q < NF; q++) s_first[q] = f[q];
+                s_flags = flg | (a.use_spill && ctl->cont_overflow ? 1u : 0u);
             }
-            s_g[0] = d0; s_g[1] = d1; s_cand[0] = c0; s_cand[1] = c1;
-            for (int q = 0; q < NF; q++) s_first[q] = f[q];
-            s_flags = flg | (a.use_spill && ctl->cont_overflow ? 1u : 0u);
         }
         __syncthreads();
         KB_STAMP(ctl, 0);
@@ -764,49 +820,47 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
                 else { D.status = 1; D.kind = 1; D.to = t; }
                 s_done = 1;
             } else if (a.rebalance) {                                 // steps.go:234-282
-                // su < MinUnbalance decides; certify it against eps or ask for exact loads
+                // su < MinUnbalance decides; certify it against eps or use the exact su
                 const bool lo = su + 2.0 * eps < a.min_unbalance, hi = su - 2.0 * eps >= a.min_unbalance;
                 if (!lo && !hi) {
-                    if (!a.integral && ctl->ndirty > 0) s_exact_need = 1;
-                    else s_exact_need = 2;       // exact su decides (below)
+                    s_exact_need = (!a.integral && ndirty0 > 0) ? 1 : 2;
                 } else if (hi) {
-                    if (F[F_EMPTY] != NONE32 || nblm0 == 0) {
-                        D.status = -1; D.step = 6; D.err = E_PANIC; D.part = F[F_EMPTY]; s_done = 1;
-                    } else if (F[F_LEAD] != NONE32) {
-                        const uint32_t p = F[F_LEAD];
-                        const int nrep = (int)meta_nrep(a.meta[p]);
-                        const int light = ctl->light;
-                        int ex = -1;
-                        for (int k = 0; k < nrep && ex < 0; k++) if (rd(p, k) == light) ex = k;
-                        D.status = 1; D.step = 6; D.part = p; D.slot = 0; D.from = rd(p, 0); D.to = light;
-                        D.kind = ex >= 0 ? 4 : 1;       // swap when bl[0] is already a replica
-                        s_done = 1;
-                    }
+                    s_exact_need = 3;                                 // leader pick below
                 }
             }
         }
         __syncthreads();
-        // exact su (sequential folds in bl order) when a decision needs it
+        // exact su (sequential folds in bl order); s_e doubles as the bl-ordered loads
+        // (every load is exact here, so every error bound is zero)
+        double* s_Lm = s_e;
         auto exact_su = [&]() {
-            for (int k = tid; k < nblm0; k += STEP_THREADS) s_ld[k] = a.load[a.blm[k]];
+            for (int k = tid; k < nblm0; k += STEP_THREADS) s_Lm[k] = s_ld[a.blm[k]];
             __syncthreads();
             if (tid == 0) {
-                const double S = fold_lds(s_ld, nblm0);
+                const double S = fold_lds(s_Lm, nblm0);
                 const double avg = S / (double)nblm0;
                 double U = 0.0;
-                for (int k = 0; k < nblm0; k++) U += term_x(s_ld[k], avg);
+                for (int k = 0; k < nblm0; k++) U += term_x(s_Lm[k], avg);
                 s_sux = U;
                 atomicAdd(&ctl->total_folds, 1ull);
             }
             __syncthreads();
         };
-        if (s_exact_need == 2) {
-            // ReassignLeaders on the exact su (utils-folds, integral or clean loads)
-            exact_su();
+        auto unstage = [&]() {
+            for (int b = tid; b < B; b += STEP_THREADS) s_e[b] = 0.0;
+            __syncthreads();
+        };
+        if (s_exact_need >= 2) {
+            bool take = s_exact_need == 3;
+            if (s_exact_need == 2) {
+                exact_su();
+                unstage();
+                take = !(s_sux < a.min_unbalance);
+            }
             if (tid == 0) {
                 s_exact_need = 0;
                 const uint32_t* F = s_first;
-                if (!(s_sux < a.min_unbalance)) {
+                if (take) {
                     auto rd = [&](uint32_t p, int k) -> int { return (int)a.rep[(long long)k * a.Ppad + p]; };
                     if (F[F_EMPTY] != NONE32 || nblm0 == 0) {
                         D.status = -1; D.step = 6; D.err = E_PANIC; D.part = F[F_EMPTY]; s_done = 1;
@@ -817,7 +871,7 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
                         int ex = -1;
                         for (int k = 0; k < nrep && ex < 0; k++) if (rd(p, k) == light) ex = k;
                         D.status = 1; D.step = 6; D.part = p; D.slot = 0; D.from = rd(p, 0); D.to = light;
-                        D.kind = ex >= 0 ? 4 : 1;
+                        D.kind = ex >= 0 ? 4 : 1;       // swap when bl[0] is already a replica
                         s_done = 1;
                     }
                 }
@@ -844,7 +898,7 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
             if (s_done) break;
             // (1) distinct keys of this kind (earliest iteration index per key)
             if (g < HUGE_VAL)
-                for_each_contender(a, kind, g, eps, inv_avg, [&](const Contender& c) {
+                for_each_contender(a, s_ld, kind, g, eps, inv_avg, [&](const Contender& c) {
                     if (dedup_insert(T, c.kind, c.s, c.t, c.w, c.iter) < 0) s_fail = 1;
                 });
             __syncthreads();
@@ -867,7 +921,7 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
                 for (int h = tid; h < DEDUP_STEP; h += STEP_THREADS) if (s_key[h] != NONE32) s_i = h;
                 __syncthreads();
                 cw = dedup_entry(T, s_i);
-                Ua = U0h + cont_delta(a.r, cw, inv_avg);
+                Ua = U0h + cont_delta_ld(s_ld, cw, inv_avg);
                 // |Ua - U'| <= eps and |U0h - su| <= eps; margins of 3*eps on both decisions
                 const double thr = U0h - a.min_unbalance;
                 const double rel = 4.0 * DBL_EPSILON * fabs(thr);
@@ -877,14 +931,15 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
                 c_improved = imp_t;
                 c_take = take_t;
             } else if (!have) {
-                // no candidate: cu = su; the decision is su < su - MinUnbalance
-                const bool t_t = a.min_unbalance < 0.0, t_f = a.min_unbalance >= 0.0;
+                // no candidate: cu = su; the decision is su < fl(su - MinUnbalance)
+                const bool t_t = -a.min_unbalance > 4.0 * DBL_EPSILON * (fabs(U0h) + eps);
+                const bool t_f = a.min_unbalance >= 0.0;
                 certain = (t_t || t_f) && !a.exact_unb;
                 c_improved = false;
                 c_take = t_t;
             }
-            if (!certain && !a.integral && ctl->ndirty > 0) {
-                if (tid == 0) { s_exact_need = 1; }
+            if (!certain && !a.integral && ndirty0 > 0) {
+                if (tid == 0) s_exact_need = 1;
                 __syncthreads();
                 break;
             }
@@ -903,8 +958,8 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
                 sux = s_sux;
                 if (!fail && ndist == 1) {
                     if (tid == 0) {
-                        s_dv[0] = exact_unbalance_lds(s_ld, nblm0, a.posm[cw.s], a.posm[cw.t],
-                                                      a.load[cw.s] - cw.w, a.load[cw.t] + cw.w);
+                        s_dv[0] = exact_unbalance_lds(s_Lm, nblm0, a.posm[cw.s], a.posm[cw.t],
+                                                      s_ld[cw.s] - cw.w, s_ld[cw.t] + cw.w);
                         atomicAdd(&ctl->total_folds, 1ull);
                     }
                     __syncthreads();
@@ -918,8 +973,8 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
                     double bw = 0.0;
                     unsigned long long nf = 0;
                     auto consider = [&](const Contender& c) {
-                        const double u = exact_unbalance_lds(s_ld, nblm0, a.posm[c.s], a.posm[c.t],
-                                                             a.load[c.s] - c.w, a.load[c.t] + c.w);
+                        const double u = exact_unbalance_lds(s_Lm, nblm0, a.posm[c.s], a.posm[c.t],
+                                                             s_ld[c.s] - c.w, s_ld[c.t] + c.w);
                         nf++;
                         if (u < bu || (u == bu && c.iter < bi)) { bu = u; bi = c.iter; bs = c.s; bt = c.t; bw = c.w; }
                     };
@@ -927,7 +982,7 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
                         for (int h = tid; h < DEDUP_STEP; h += STEP_THREADS)
                             if (s_key[h] != NONE32) consider(dedup_entry(T, h));
                     } else {
-                        for_each_contender(a, kind, g, eps, inv_avg, consider);
+                        for_each_contender(a, s_ld, kind, g, eps, inv_avg, consider);
                     }
                     nf = wave_sum(nf);
                     if (lane == 0 && nf) atomicAdd(&ctl->total_folds, nf);
@@ -951,6 +1006,7 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
                     Ustar = s_dv[0]; witer = s_u[0];
                     cw.s = s_bs[0]; cw.t = s_bt[0]; cw.w = s_bw[0]; cw.iter = witer;
                 }
+                unstage();
                 // cu starts at su and only a strictly smaller u replaces it (steps.go:163,211)
                 improved = have && Ustar < sux;
                 const double cu = improved ? Ustar : sux;
@@ -987,24 +1043,21 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
         }
 
         // ---------------------------------------------------------- apply
-        __shared__ int s_aff[2 * MAXR + 2];
-        __shared__ double s_oldc[2 * MAXR + 2];
-        __shared__ int s_naff;
+        // (thread 0; its small arrays live in LDS, not in scratch memory)
+        __shared__ int rold[MAXR + 1], r[MAXR + 1];
+        __shared__ int tb[2 * MAXR + 2], dcnt[2 * MAXR + 2], cv[2 * MAXR + 2];
+        __shared__ double oc[2 * MAXR + 2], nc2[2 * MAXR + 2], av[2 * MAXR + 2];
         if (tid == 0) {
-            s_naff = 0;
+            int nT = 0;
             if (D.status == 1) {
                 const long long p = D.part;
+                // the partition (one round trip)
                 const uint32_t m = a.meta[p];
-                const int nrep = (int)meta_nrep(m);
-                int r[MAXR + 1];
-                for (int k = 0; k < nrep; k++) r[k] = (int)a.rep[(long long)k * a.Ppad + p];
+                for (int k = 0; k < a.RC; k++) rold[k] = (int)a.rep[(long long)k * a.Ppad + p];
                 const double wv = a.w[p];
                 const int ncp = a.nc[p];
-                for (int k = 0; k < nrep; k++) {             // old contributions of p's brokers
-                    s_aff[s_naff] = r[k];
-                    s_oldc[s_naff] = k == 0 ? wv * (double)(nrep + ncp) : wv;
-                    s_naff++;
-                }
+                const int nrep = (int)meta_nrep(m);
+                for (int k = 0; k < nrep; k++) r[k] = rold[k];
                 int nn = nrep;
                 bool state_changed = true;
                 if (D.kind == 1) {                           // replace at slot (utils.go:186-190)
@@ -1023,7 +1076,6 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
                     if (a.sem_go) state_changed = false;     // the append is not visible through pl
                     else { r[nrep] = D.to; nn = nrep + 1; }
                 }
-                // the meta bits that depend on the replicas (Disallowed trigger, in-set count)
                 const uint64_t* sb = a.setbits + (size_t)meta_set(m) * a.W64;
                 auto remeta = [&](int n) {
                     uint32_t dis = 0, nin = 0;
@@ -1036,64 +1088,69 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
                         for (int k = 0; k < nrep; k++) a.rep[(long long)k * a.Ppad + p] = (uint16_t)r[k];
                         a.meta[p] = remeta(nrep);
                     }
-                    s_naff = 0;
                 } else if (state_changed) {
                     for (int k = 0; k < nn; k++) a.rep[(long long)k * a.Ppad + p] = (uint16_t)r[k];
                     a.meta[p] = remeta(nn);
-                    if (D.kind == 1) { a.cnt[D.from]--; a.cnt[D.to]++; }
-                    if (D.kind == 2) { a.cnt[D.from]--; }
-                    if (D.kind == 3) { a.cnt[D.to]++; }
-                    // new contributions: exact +- in integral mode, bounded increments otherwise
-                    const double u = DBL_EPSILON / 2;
-                    auto upd = [&](int b, double oldc, double newc) {
-                        const double L = a.load[b];
-                        if (a.integral) { a.load[b] = (L - oldc) + newc; return; }
-                        const double x1 = L - oldc;
-                        double x2 = x1 + newc;
-                        double e = a.lerr[b] + 1.01 * u * (fabs(x1) + fabs(x2));
-                        if (!(x2 > 0.0)) x2 = 0.0;           // loads are sums of non-negative terms
-                        if (a.cnt[b] == 0) { x2 = 0.0; e = 0.0; }   // empty fold: exactly 0
-                        a.load[b] = x2;
-                        a.lerr[b] = e;
-                        const uint8_t dn = a.cnt[b] > 0 ? 1 : 0;
-                        if (dn != a.dirty[b]) ctl->ndirty += dn ? 1 : -1;
-                        a.dirty[b] = dn;
+                    // brokers whose contribution changed: old vs new (getBrokerLoad, utils.go:92-105)
+                    int na = 0;
+                    auto slot_of = [&](int b) {
+                        for (int x = 0; x < na; x++) if (tb[x] == b) return x;
+                        tb[na] = b; oc[na] = 0.0; nc2[na] = 0.0; dcnt[na] = 0;
+                        return na++;
                     };
-                    const int base_aff = s_naff;
+                    for (int k = 0; k < nrep; k++) {
+                        const int x = slot_of(rold[k]);
+                        oc[x] = k == 0 ? wv * (double)(nrep + ncp) : wv;
+                        dcnt[x]--;
+                    }
                     for (int k = 0; k < nn; k++) {
-                        const int b = r[k];
-                        const double cc = k == 0 ? wv * (double)(nn + ncp) : wv;
-                        int f2 = -1;
-                        for (int x = 0; x < base_aff; x++) if (s_aff[x] == b) f2 = x;
-                        if (f2 >= 0) {
-                            if (s_oldc[f2] == cc) { s_aff[f2] = -1 - s_aff[f2]; }  // unchanged contribution
-                            else upd(b, s_oldc[f2], cc);
+                        const int x = slot_of(r[k]);
+                        nc2[x] = k == 0 ? wv * (double)(nn + ncp) : wv;
+                        dcnt[x]++;
+                    }
+                    // their counts and error terms (one round trip)
+                    for (int x = 0; x < na; x++) { cv[x] = a.cnt[tb[x]]; if (!a.integral) av[x] = a.lerr[tb[x]]; }
+                    const double u = DBL_EPSILON / 2;
+                    int dd = 0;
+                    for (int x = 0; x < na; x++) {
+                        const int b = tb[x];
+                        const int cnew = cv[x] + dcnt[x];
+                        if (dcnt[x]) a.cnt[b] = cnew;
+                        if (oc[x] == nc2[x]) continue;               // unchanged contribution
+                        const double L = s_ld[b];
+                        uint8_t fl = s_fl[b] & ~BF_PRESENT;
+                        if (cnew > 0) fl |= BF_PRESENT;
+                        double Ln, eb = 0.0;
+                        if (a.integral) {
+                            Ln = (L - oc[x]) + nc2[x];
                         } else {
-                            upd(b, 0.0, cc);
-                            s_aff[s_naff] = b; s_oldc[s_naff] = 0.0; s_naff++;
+                            // bounded incremental update; the exact fold comes with k_refresh
+                            const double x1 = L - oc[x];
+                            Ln = x1 + nc2[x];
+                            double ae = av[x] + 1.01 * u * (fabs(x1) + fabs(Ln));
+                            if (!(Ln > 0.0)) Ln = 0.0;               // loads are sums of non-negative terms
+                            if (cnew == 0) { Ln = 0.0; ae = 0.0; }  // empty fold: exactly 0
+                            a.lerr[b] = ae;
+                            const bool dirty = cnew > 0;
+                            if (dirty != ((fl & BF_DIRTY) != 0)) dd += dirty ? 1 : -1;
+                            fl = dirty ? (uint8_t)(fl | BF_DIRTY) : (uint8_t)(fl & ~BF_DIRTY);
+                            eb = dirty ? ae + gamma_n(cnew) * (Ln + ae) : 0.0;
                         }
+                        a.load[b] = Ln; s_ld[b] = Ln;
+                        a.eb[b] = eb; s_e[b] = eb;
+                        a.bfl[b] = fl; s_fl[b] = fl;
+                        if (nT < TMAX) s_T[nT++] = b;
                     }
-                    for (int x = 0; x < base_aff; x++) {
-                        const int b = s_aff[x];
-                        if (b < 0) continue;
-                        bool still = false;
-                        for (int k = 0; k < nn; k++) still |= r[k] == b;
-                        if (!still) upd(b, s_oldc[x], 0.0);
-                    }
-                    int n2 = 0;                              // brokers whose contribution changed
-                    for (int x = 0; x < s_naff; x++) if (s_aff[x] >= 0) s_aff[n2++] = s_aff[x];
-                    s_naff = n2;
+                    if (dd) ctl->ndirty += dd;
                     // the per-broker partition lists follow in the next scan (k_scan's list workgroup)
                     if (!a.integral && (D.kind == 1 || D.kind == 2 || D.kind == 3)) {
                         ctl->pl_kind = D.kind; ctl->pl_from = D.from; ctl->pl_to = D.to; ctl->pl_part = p;
                         ctl->pending_list = 1;
                     }
-                } else {
-                    s_naff = 0;
                 }
             }
-            for (int x = 0; x < s_naff && x < TMAX; x++) s_T[x] = s_aff[x];
-            s_nT = s_naff < TMAX ? s_naff : TMAX;
+            s_nT = nT;
+            if (D.status == 1) s_moved = D.part;
             // log the step
             ChangeDev ch;
             ch.status = D.status; ch.step = D.step; ch.kind = D.kind; ch.slot = D.slot;
@@ -1110,24 +1167,23 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
             }
             ctl->total_cand += add;
             ctl->total_cont += (unsigned long long)s_ndist;
-            ctl->ncont = 0;
-            ctl->cont_overflow = 0;
             if (D.status != 1) { ctl->halted = H_DONE; ctl->prepped = 0; }
         }
         __syncthreads();
-        if (ctl->halted != H_RUN) return;
+        if (D.status != 1) return;
         KB_STAMP(ctl, 3);
     }
 
     // ================================================================== prep
     // (next step): getBL's (load, id) order, bl_move, relative loads, eps, sets
-    const int B = a.B;
     const bool full = ctl->full_prep != 0;
-    for (int b = tid; b < B; b += STEP_THREADS) s_ld[b] = a.load[b];
+    const int nT = s_nT;
     if (full) {
+        // every load is exact here (fresh state or after k_refresh): s_e holds the sort keys
+        unsigned long long* s_k64 = (unsigned long long*)s_e;
         const int NP2 = a.NP2;
         for (int i = tid; i < NP2; i += STEP_THREADS) {
-            s_k64[i] = i < B ? d2u(a.load[i]) : NONE64;
+            s_k64[i] = i < B ? d2u(s_ld[i]) : NONE64;
             s_ord[i] = i < B ? i : 0x7FFFFFFF;
         }
         __syncthreads();
@@ -1148,57 +1204,61 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
                 __syncthreads();
             }
         }
-    } else {
+        for (int b = tid; b < B; b += STEP_THREADS) s_e[b] = 0.0;
+    } else if (nT > 0) {
         // incremental: only the touched brokers moved (their loads changed)
-        const int nT = s_nT;
-        for (int b = tid; b < B; b += STEP_THREADS) s_tm[b] = 0;
-        if (tid < TMAX) s_cntT[tid] = 0;
+        if (tid < nT) { s_fl[s_T[tid]] |= BF_TOUCHED; s_cntT[tid] = 0; }
         __syncthreads();
-        if (tid < nT) { s_tm[s_T[tid]] = 1; s_posT[tid] = a.posu[s_T[tid]]; }
-        for (int i = tid; i < B; i += STEP_THREADS) s_ord2[i] = a.order[i];
+        for (int i = tid; i < B; i += STEP_THREADS) {
+            const int b = s_ord[i];
+            if (s_fl[b] & BF_TOUCHED)
+                for (int x = 0; x < nT; x++) if (s_T[x] == b) s_posT[x] = i;
+        }
         __syncthreads();
-        if (nT == 0) {
-            for (int i = tid; i < B; i += STEP_THREADS) s_ord[i] = s_ord2[i];
-        } else {
-            // per untouched element: new position = old - (touched before it) + (touched keys below it)
-            for (int i0 = 0; i0 < B; i0 += STEP_THREADS) {
-                const int i = i0 + tid;
-                const bool in = i < B;
-                const int b = in ? s_ord2[i] : 0;
-                const bool untouched = in && !s_tm[b];
-                const double Lb = in ? s_ld[b] : 0.0;
-                int below = 0, before = 0;
-                for (int x = 0; x < nT; x++) {
-                    const int t = s_T[x];
-                    const double Lt = s_ld[t];
-                    const bool t_lt_b = (Lt < Lb) || (Lt == Lb && t < b);
-                    below += t_lt_b ? 1 : 0;
-                    before += s_posT[x] < i ? 1 : 0;
-                    // count, for touched t, the untouched brokers below it
-                    const bool b_lt_t = untouched && ((Lb < Lt) || (Lb == Lt && b < t));
-                    const unsigned long long bal = __ballot(b_lt_t);
-                    if (lane == 0 && bal) atomicAdd(&s_cntT[x], (int)__popcll(bal));
-                }
-                if (untouched) s_ord[i - before + below] = b;
-            }
-            __syncthreads();
-            if (tid < nT) {
-                const int t = s_T[tid];
+        // per untouched element: new position = old - (touched before it) + (touched keys below it)
+        int nb[(MAXB + STEP_THREADS - 1) / STEP_THREADS], np[(MAXB + STEP_THREADS - 1) / STEP_THREADS];
+#pragma unroll
+        for (int q = 0; q < (MAXB + STEP_THREADS - 1) / STEP_THREADS; q++) {
+            const int i = q * STEP_THREADS + tid;
+            const bool in = i < B;
+            const int b = in ? s_ord[i] : 0;
+            const bool untouched = in && !(s_fl[b] & BF_TOUCHED);
+            const double Lb = s_ld[b];
+            int below = 0, before = 0;
+            for (int x = 0; x < nT; x++) {
+                const int t = s_T[x];
                 const double Lt = s_ld[t];
-                int rank = 0;
-                for (int x = 0; x < nT; x++) {
-                    const int t2 = s_T[x];
-                    const double L2 = s_ld[t2];
-                    rank += ((L2 < Lt) || (L2 == Lt && t2 < t)) ? 1 : 0;
-                }
-                s_ord[s_cntT[tid] + rank] = t;
+                below += ((Lt < Lb) || (Lt == Lb && t < b)) ? 1 : 0;
+                before += s_posT[x] < i ? 1 : 0;
+                // count, for touched t, the untouched brokers below it
+                const bool b_lt_t = untouched && ((Lb < Lt) || (Lb == Lt && b < t));
+                const unsigned long long bal = __ballot(b_lt_t);
+                if (lane == 0 && bal) atomicAdd(&s_cntT[x], (int)__popcll(bal));
             }
+            nb[q] = untouched ? b : -1;
+            np[q] = i - before + below;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < (MAXB + STEP_THREADS - 1) / STEP_THREADS; q++)
+            if (nb[q] >= 0) s_ord[np[q]] = nb[q];
+        if (tid < nT) {
+            const int t = s_T[tid];
+            const double Lt = s_ld[t];
+            int rank = 0;
+            for (int x = 0; x < nT; x++) {
+                const int t2 = s_T[x];
+                const double L2 = s_ld[t2];
+                rank += ((L2 < Lt) || (L2 == Lt && t2 < t)) ? 1 : 0;
+            }
+            s_ord[s_cntT[tid] + rank] = t;
         }
     }
     __syncthreads();
-    for (int i = tid; i < B; i += STEP_THREADS) { const int b = s_ord[i]; a.order[i] = b; a.posu[b] = i; }
+    KB_STAMP(ctl, 4);
     // bl_move = brokers present in the load map or listed in -broker-ids (steps.go:150-157)
     for (int w = tid; w < MAXB / 64; w += STEP_THREADS) { s_blmb[w] = 0; s_presb[w] = 0; }
+    if (tid == 0) s_unc = 0;
     __syncthreads();
     {
         int flag[4], c = 0;
@@ -1209,11 +1269,21 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
             flag[q] = 0;
             if (i < B) {
                 const int b = s_ord[i];
-                const bool pres = a.cnt[b] > 0;
-                flag[q] = (pres || a.incfg[b]) ? 1 : 0;
+                const uint8_t fl = s_fl[b];
+                const bool pres = (fl & BF_PRESENT) != 0;
+                flag[q] = (fl & (BF_PRESENT | BF_INCFG)) ? 1 : 0;
                 if (flag[q]) atomicOr((unsigned long long*)&s_blmb[b >> 6], 1ull << (b & 63));
                 if (pres) atomicOr((unsigned long long*)&s_presb[b >> 6], 1ull << (b & 63));
                 c += flag[q];
+                a.order[i] = b;
+                a.posu[b] = i;
+                // order certification: with approximate loads, neighbours must be
+                // separated by more than their error bounds (else the exact order is unknown)
+                if (i + 1 < B) {
+                    const int b2 = s_ord[i + 1];
+                    const double e = s_e[b] + s_e[b2];
+                    if (e > 0.0 && !(s_ld[b2] - s_ld[b] > e)) s_unc = 1;
+                }
             }
         }
         int incl = c;
@@ -1238,43 +1308,28 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
     }
     __syncthreads();
     const int nblm = s_nblm;
-    KB_STAMP(ctl, 4);
-    // order certification: with approximate loads, neighbours must be separated
-    // by more than their error bounds (else the exact order is unknown)
-    if (tid == 0) s_unc = 0;
-    __syncthreads();
-    if (!a.integral && ctl->ndirty > 0) {
-        for (int i = tid; i + 1 < B; i += STEP_THREADS) {
-            const int b1 = s_ord[i], b2 = s_ord[i + 1];
-            const double e = load_err(a.load, a.lerr, a.dirty, a.cnt, b1) + load_err(a.load, a.lerr, a.dirty, a.cnt, b2);
-            if (e > 0.0 && !(s_ld[b2] - s_ld[b1] > e)) s_unc = 1;
-        }
-    }
-    __syncthreads();
     if (s_unc) {
         if (tid == 0) { ctl->halted = H_NEED_EXACT; ctl->prepped = 0; ctl->total_exact_halts++; }
         return;
     }
     // approximate S (exact in integral mode: integers below 2^52), total load error E
     double sS = 0.0, sE = 0.0;
-    for (int k = tid; k < nblm; k += STEP_THREADS) {
-        const int b = a.blm[k];
-        sS += s_ld[b];
-        if (!a.integral) sE += load_err(a.load, a.lerr, a.dirty, a.cnt, b);
-    }
+    for (int b = tid; b < B; b += STEP_THREADS)
+        if (s_fl[b] & (BF_PRESENT | BF_INCFG)) { sS += s_ld[b]; sE += s_e[b]; }
+    __shared__ double s_q[3][NW];
     sS = wave_sum(sS); sE = wave_sum(sE);
-    if (lane == 0) { s_dv[wid] = sS; s_dv2[wid] = sE; }
+    if (lane == 0) { s_q[0][wid] = sS; s_q[1][wid] = sE; }
     __syncthreads();
     double S = 0.0, E = 0.0;
-    for (int x = 0; x < NW; x++) { S += s_dv[x]; E += s_dv2[x]; }
-    __syncthreads();
+#pragma unroll
+    for (int x = 0; x < NW; x++) { S += s_q[0][x]; E += s_q[1][x]; }
     const double avg = S / (double)nblm;
     const double iav = 1.0 / avg;
     double su = 0.0, v = 0.0, rm = 0.0;
     for (int b = tid; b < B; b += STEP_THREADS) {
         double r = 0.0;
-        if (a.posm[b] >= 0) {
-            r = __fma_rn(s_ld[b], iav, -1.0);
+        if (s_fl[b] & (BF_PRESENT | BF_INCFG)) {
+            r = rel_ld(s_ld, b, iav);
             su += fsq(r);
             const double ar = fabs(r);
             v += ar * (1.0 + ar);
@@ -1283,11 +1338,40 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
         a.r[b] = r;
     }
     su = wave_sum(su); v = wave_sum(v); rm = wave_max(rm);
-    if (lane == 0) { s_dv[wid] = su; s_dv2[wid] = v; s_dv3[wid] = rm; }
+    // upper bound of the next step's minimum per kind: the near-tie keys of the scan
+    // just resolved whose partition and brokers the applied move did not touch are
+    // still candidates; re-scored on the new loads they bound the new minimum
+    double ub0 = HUGE_VAL, ub1 = HUGE_VAL;
+    if (do_res && !full) {
+        const long long pm = s_moved;
+        for (int i = tid; i < a.nrec; i += STEP_THREADS) {
+            const RecHdr* h = (const RecHdr*)(a.recs + (size_t)i * a.rec_stride);
+            const Contender* keys = (const Contender*)(h + 1);
+            const int nk = (int)min(h->nkeys, (uint32_t)a.rec_keys);
+            for (int k = 0; k < nk; k++) {
+                const Contender c = keys[k];
+                if ((long long)(c.iter >> 21) == pm) continue;
+                if ((s_fl[c.s] | s_fl[c.t]) & BF_TOUCHED) continue;
+                const double d = cont_delta_ld(s_ld, c, iav);
+                if (c.kind == 0) ub0 = d < ub0 ? d : ub0;
+                else ub1 = d < ub1 ? d : ub1;
+            }
+        }
+    }
+    ub0 = wave_min(ub0); ub1 = wave_min(ub1);
+    __shared__ double s_ubw[2][NW];
     __syncthreads();
+    if (lane == 0) { s_q[0][wid] = su; s_q[1][wid] = v; s_q[2][wid] = rm; s_ubw[0][wid] = ub0; s_ubw[1][wid] = ub1; }
+    __syncthreads();
+    double U0 = 0.0, V = 0.0, Rm = 0.0;
+    if (tid == 0)
+#pragma unroll
+        for (int x = 0; x < NW; x++) {
+            U0 += s_q[0][x]; V += s_q[1][x]; Rm = s_q[2][x] > Rm ? s_q[2][x] : Rm;
+            ub0 = s_ubw[0][x] < ub0 ? s_ubw[0][x] : ub0;
+            ub1 = s_ubw[1][x] < ub1 ? s_ubw[1][x] : ub1;
+        }
     if (tid == 0) {
-        double U0 = 0.0, V = 0.0, Rm = 0.0;
-        for (int x = 0; x < NW; x++) { U0 += s_dv[x]; V += s_dv2[x]; Rm = s_dv3[x] > Rm ? s_dv3[x] : Rm; }
         const double u = DBL_EPSILON / 2;
         const double n = (double)nblm;
         const double R = Rm + a.wmax * iav;
@@ -1298,16 +1382,31 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
         if (!(ep > 1e-300)) ep = 1e-300;
         ctl->S = S; ctl->avg = avg; ctl->inv_avg = iav; ctl->U0 = U0;
         ctl->V = V; ctl->eps = ep; ctl->E = E; ctl->nblm = nblm;
-        ctl->heavy = nblm > 0 ? a.blm[nblm - 1] : -1;
-        ctl->light = nblm > 0 ? a.blm[0] : -1;
+        ctl->ub[0] = ub0; ctl->ub[1] = ub1;
         ctl->want_refresh = (epsl > epsf || ctl->ndirty >= 256) ? 1 : 0;
+        ctl->ncont = 0;
+        ctl->cont_overflow = 0;
+    }
+    if (wid == 0) {
+        // first / last bl_move broker in universe order (scan the order from both ends)
+        int lo = 0x7FFFFFFF, hi = -1;
+        for (int i = lane; i < B; i += 64) {
+            const int b = s_ord[i];
+            if (s_fl[b] & (BF_PRESENT | BF_INCFG)) { lo = i < lo ? i : lo; hi = i > hi ? i : hi; }
+        }
+        lo = wave_min(lo);
+        hi = wave_max(hi);
+        if (lane == 0) {
+            ctl->light = lo < 0x7FFFFFFF ? s_ord[lo] : -1;
+            ctl->heavy = hi >= 0 ? s_ord[hi] : -1;
+        }
     }
     KB_STAMP(ctl, 5);
     // ---- set records: full, or the sets containing a touched broker
     for (int w = tid; w < (a.nsets + 31) / 32; w += STEP_THREADS) s_smark[w] = full ? 0xFFFFFFFFu : 0u;
     __syncthreads();
     if (!full) {
-        for (int x = 0; x < s_nT; x++) {
+        for (int x = 0; x < nT; x++) {
             const int t = s_T[x];
             for (int j = a.bset_off[t] + tid; j < a.bset_off[t + 1]; j += STEP_THREADS) {
                 const int s = a.bset_ids[j];
@@ -1321,7 +1420,7 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
         const int K = a.K, KR = a.KR;
         for (int set = wid; set < a.nsets; set += NW) {
             if (!((s_smark[set >> 5] >> (set & 31)) & 1u)) continue;
-            const uint64_t sbw = lane < a.W64 ? a.setbits[(size_t)set * a.W64 + lane] : 0ull;
+            const unsigned long long sbw = lane < a.W64 ? (unsigned long long)a.setbits[(size_t)set * a.W64 + lane] : 0ull;
             auto inset = [&](int b) -> bool {
                 const unsigned long long wv = __shfl(sbw, b >> 6);
                 return (wv >> (b & 63)) & 1ull;
@@ -1379,7 +1478,7 @@ constexpr int REFRESH_CHUNK = 4096;
 
 __global__ __launch_bounds__(REFRESH_THREADS) void k_refresh(RefreshArgs a) {
     const int b = blockIdx.x;
-    if (b >= a.B || !a.dirty[b]) return;
+    if (b >= a.B || !(a.bfl[b] & BF_DIRTY)) return;
     __shared__ double s_c[REFRESH_CHUNK];
     const uint32_t st = a.L.lstart[b], n = a.L.llen[b];
     double acc = 0.0;
@@ -1399,7 +1498,8 @@ __global__ __launch_bounds__(REFRESH_THREADS) void k_refresh(RefreshArgs a) {
     if (threadIdx.x == 0) {
         a.load[b] = acc;
         a.lerr[b] = gamma_n((int)n) * acc;
-        a.dirty[b] = 0;
+        a.eb[b] = 0.0;
+        a.bfl[b] = a.bfl[b] & ~BF_DIRTY;
     }
 }
 

@@ -33,6 +33,7 @@ struct ScanArgs {
     Contender* cont;          // spill buffer
     uint32_t cont_cap;
     int listwg;               // 1: the last workgroup applies the pending list op
+    int dbg;                  // diagnostic only (KB_DEBUG_SCAN): 1 = skip the census
     Lists L;
 };
 
@@ -53,10 +54,10 @@ struct StepArgs {
     int32_t* posm;            // [B] position in bl_move or -1
     double* r;                // [B] approximate relative loads
     double* load;             // [B] loads (exact in integral mode / when clean)
-    double* lerr;             // [B] bound |load - real sum of contributions| (dirty brokers)
-    uint8_t* dirty;           // [B] 1: load is an incremental approximation
+    double* lerr;             // [B] bound |load - real sum of contributions| (non-integral)
+    double* eb;               // [B] bound |load - reference fold| (0 when exact)
+    uint8_t* bfl;             // [B] BF_PRESENT | BF_INCFG | BF_DIRTY
     int32_t* cnt;             // [B] replicas held
-    const uint8_t* incfg;     // [B] listed in -broker-ids
     const int32_t* bset_off;  // [B+1] sets containing each broker
     const int32_t* bset_ids;
     const unsigned char* recs;   // scan records or gathered rank summaries
@@ -79,8 +80,8 @@ struct RefreshArgs {
     const int32_t* nc;
     double* load;
     double* lerr;
-    uint8_t* dirty;
-    const int32_t* cnt;
+    double* eb;
+    uint8_t* bfl;
     int B;
     Lists L;
 };
