@@ -127,9 +127,10 @@ def main():
     if args.stamps:
         st = eng.stamps()
         n = max(1, st1["steps"])
-        names = ["res.reduce", "res.pred", "res.move", "res.apply", "prep.sort+blm", "prep.loads+eps",
-                 "prep.sets", None, "scan0.prologue", "scan0.tile", "scan0.reduce", "scan0.census", "scan0.final"]
-        counts = {"spills": 7, "walks": 13, "walk_iters": 14, "emits": 15}
+        names = [None, "step.loads", "res.reduce", "res.pred", "res.move", "res.apply(tail)", "prep.sort", None,
+                 "prep.blm+cert", "prep.S+r+eps+ub", "prep.sets", "res.move->apply", "apply.load_p",
+                 "apply.decide+sbw+remeta", "apply.load_cnt"]
+        counts = {"spills": 7, "emits": 15}
         print(json.dumps({"stamps_us_per_step": {k: st[i] / 100.0 / n for i, k in enumerate(names) if k},
                           "counts_per_step": {k: st[i] / n for k, i in counts.items()},
                           "stats": eng.stats()}))

@@ -72,7 +72,6 @@ struct kb_engine {
     uint8_t* bfl = nullptr;
     int32_t* cnt = nullptr;
     uint64_t* setbits = nullptr;
-    int32_t* lists = nullptr;
     uint4* setrec = nullptr;
     int32_t* order = nullptr;
     int32_t* posu = nullptr;
@@ -448,7 +447,6 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
     HIPCHK(dalloc(&e->bfl, e->B));
     HIPCHK(dalloc(&e->cnt, e->B));
     HIPCHK(dalloc(&e->setbits, (size_t)e->nsets * e->W64));
-    HIPCHK(dalloc(&e->lists, (size_t)e->nsets * 2 * e->K));
     HIPCHK(dalloc(&e->setrec, (size_t)e->nsets * e->units));
     HIPCHK(dalloc(&e->order, e->B));
     HIPCHK(dalloc(&e->posu, e->B));
@@ -525,7 +523,7 @@ static void fill_step_args(kb_engine* e, StepArgs& a, const unsigned char* recs,
     a.ctl = e->ctl; a.w = e->w; a.rep = e->rep; a.meta = e->meta; a.nc = e->nc; a.Ppad = e->Ppad;
     a.RC = e->rc_dev; a.KR = e->KR; a.K = e->K; a.units = e->units; a.W64 = e->W64; a.B = (int)e->B;
     a.nsets = (int)e->nsets; a.NP2 = e->NP2;
-    a.setbits = e->setbits; a.setrec = e->setrec; a.lists = e->lists;
+    a.setbits = e->setbits; a.setrec = e->setrec;
     a.order = e->order; a.posu = e->posu; a.blm = e->blm; a.posm = e->posm; a.r = e->r;
     a.load = e->load; a.lerr = e->lerr; a.eb = e->eb; a.bfl = e->bfl; a.cnt = e->cnt;
     a.bset_off = e->bset_off; a.bset_ids = e->bset_ids;
@@ -885,7 +883,7 @@ extern "C" int kb_engine_last_error(kb_engine* e, char* buf, size_t n) {
 extern "C" void kb_engine_destroy(kb_engine* e) {
     if (!e) return;
     void* ptrs[] = {e->w, e->rep, e->meta, e->nc, e->load, e->lerr, e->eb, e->bfl, e->cnt,
-                    e->setbits, e->lists, e->setrec, e->order, e->posu, e->blm, e->posm, e->r,
+                    e->setbits, e->setrec, e->order, e->posu, e->blm, e->posm, e->r,
                     e->bset_off, e->bset_ids, e->recs, e->cont, e->ctl, e->log,
                     e->L.lstart, e->L.llen, e->L.lcap, e->L.lent};
     for (void* p : ptrs) if (p) hipFree(p);

@@ -31,9 +31,11 @@
 // binary64, no FMA: the file is built with -ffp-contract=off; true division).
 #include <hip/hip_runtime.h>
 #include <cfloat>
+#include <cstddef>
 #include <cstdint>
 #include "engine_dev.h"
 #include "kernels_api.h"
+#include "wave_ops.h"
 
 namespace kbe {
 
@@ -62,24 +64,13 @@ __device__ __forceinline__ bool setbit(const uint64_t* sb, int b) {
     return (sb[b >> 6] >> (b & 63)) & 1ull;
 }
 
+// wave-wide reductions (full waves only): DPP row operations, no LDS traffic
 template <typename T>
-__device__ __forceinline__ T wave_min(T v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) { T x = __shfl_xor(v, o); v = x < v ? x : v; }
-    return v;
-}
+__device__ __forceinline__ T wave_min(T v) { return wave_red_min(v); }
 template <typename T>
-__device__ __forceinline__ T wave_max(T v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) { T x = __shfl_xor(v, o); v = x > v ? x : v; }
-    return v;
-}
+__device__ __forceinline__ T wave_max(T v) { return wave_red_max(v); }
 template <typename T>
-__device__ __forceinline__ T wave_sum(T v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    return v;
-}
+__device__ __forceinline__ T wave_sum(T v) { return wave_red_sum(v); }
 
 // u16 field idx of a set record held in registers / memory as 16-B units
 __device__ __forceinline__ uint32_t rec_u16(const uint4* v, int idx) {
@@ -149,6 +140,8 @@ struct Dedup {
     unsigned long long* wb;
     unsigned long long* it;
     int cap;
+    int* n = nullptr;               // optional: count of distinct keys, per kind
+    int* last = nullptr;            // optional: slot of a claimed key per kind (the one when n == 1)
 };
 
 __device__ __forceinline__ uint32_t ckey(int kind, int s, int t) {
@@ -166,6 +159,7 @@ __device__ int dedup_insert(const Dedup& T, int kind, int s, int t, double w, un
     int probe = 0;
     for (; probe < T.cap; probe++) {
         uint32_t old = atomicCAS(&T.key[h], NONE32, k);
+        if (old == NONE32 && T.n) { atomicAdd(&T.n[kind], 1); T.last[kind] = (int)h; }
         if (old == NONE32 || old == k) break;
         h = (h + 1) & (uint32_t)(T.cap - 1);
     }
@@ -273,26 +267,26 @@ __device__ void do_list_op(DevCtl* ctl, const Lists& L, int* s_i) {
 
 static_assert(PER_LANE == 2, "the scan's register layout assumes two partitions per lane");
 
+// one tile's data of one lane, as loaded (packed: unpacked where used, so the
+// loads of a prefetched tile stay in flight until its scoring starts)
 template <int RC>
-struct PartRegs {
-    double w[PER_LANE];
-    uint32_t m[PER_LANE];
-    uint32_t r[RC][PER_LANE];
+struct PartRaw {
+    double2 w;                      // weights of the lane's two partitions
+    uint2 m;                        // their meta words
+    uint32_t r[RC];                 // slot k: two u16 dense broker ids
+    __device__ __forceinline__ double wt(int j) const { return j ? w.y : w.x; }
+    __device__ __forceinline__ uint32_t mt(int j) const { return j ? m.y : m.x; }
+    __device__ __forceinline__ uint32_t rp(int k, int j) const { return j ? (r[k] >> 16) : (r[k] & 0xFFFFu); }
 };
 
 // two consecutive partitions per lane: one 16-B weight load, one 8-B meta load
 // and one 4-B load per replica slot (coalesced across the wave)
 template <int RC>
-__device__ __forceinline__ void load_parts(const ScanArgs& a, long long base, PartRegs<RC>& P) {
-    const double2 w2 = *(const double2*)(a.w + base);
-    P.w[0] = w2.x; P.w[1] = w2.y;
-    const uint2 m2 = *(const uint2*)(a.meta + base);
-    P.m[0] = m2.x; P.m[1] = m2.y;
+__device__ __forceinline__ void load_parts(const ScanArgs& a, long long base, PartRaw<RC>& P) {
+    P.w = *(const double2*)(a.w + base);
+    P.m = *(const uint2*)(a.meta + base);
 #pragma unroll
-    for (int k = 0; k < RC; k++) {
-        const uint32_t r2 = *(const uint32_t*)(a.rep + (long long)k * a.Ppad + base);
-        P.r[k][0] = r2 & 0xFFFFu; P.r[k][1] = r2 >> 16;
-    }
+    for (int k = 0; k < RC; k++) P.r[k] = *(const uint32_t*)(a.rep + (long long)k * a.Ppad + base);
 }
 
 __device__ __forceinline__ void emit_global(DevCtl* ctl, Contender* cont, uint32_t cap, const Contender& c) {
@@ -417,8 +411,8 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
     // every load that does not depend on the control block goes out first: the
     // first tile's stream, then the lookup tables (one memory round trip)
     int tile = blockIdx.x;
-    PartRegs<RC> P;
-    if (tile < a.ntiles) load_parts<RC>(a, a.shard_begin + (long long)tile * TILE + (long long)tid * PER_LANE, P);
+    PartRaw<RC> A, Bq;
+    if (tile < a.ntiles) load_parts<RC>(a, a.shard_begin + (long long)tile * TILE + (long long)tid * PER_LANE, A);
     for (int i = tid; i < a.B; i += SCAN_THREADS) {
         s_r[i] = a.r[i];
         s_pos[i] = (int16_t)a.posm[i];
@@ -440,28 +434,26 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
     for (int f = 0; f < NF; f++) fst[f] = NONE32;
     unsigned long long cL = 0, cN = 0;
 
-    for (int it = 0; tile < a.ntiles; tile += a.nscan, it++) {
-        const long long base = a.shard_begin + (long long)tile * TILE + (long long)tid * PER_LANE;
-        // prefetch the next tile: its loads stay in flight while this one is scored
-        PartRegs<RC> Pn;
-        const bool more = tile + a.nscan < a.ntiles;
-        if (more) load_parts<RC>(a, base + (long long)a.nscan * TILE, Pn);
-        // lane minima of the leader / non-leader slot scores
+    // score one tile held in P (partitions base, base + 1 of this lane)
+    auto score = [&](const PartRaw<RC>& P, long long base) {
         double lL = HUGE_VAL, lN = HUGE_VAL;
 #pragma unroll
         for (int j = 0; j < PER_LANE; j++) {
             const long long p = base + j;
             const bool valid = p < a.shard_end;
-            const uint32_t m = P.m[j];
+            const uint32_t m = P.mt(j);
             const int nrep = (int)meta_nrep(m), want = (int)meta_want(m);
             const bool elig = valid && meta_elig(m);
             const uint32_t pi = valid ? (uint32_t)p : NONE32;
+            uint32_t reps[RC];
+#pragma unroll
+            for (int k = 0; k < RC; k++) reps[k] = P.rp(k, j);
             if (a.sem_go) {
                 bool dup = false;
 #pragma unroll
                 for (int x = 0; x < RC; x++)
 #pragma unroll
-                    for (int y = x + 1; y < RC; y++) dup |= (y < nrep) && P.r[x][j] == P.r[y][j];
+                    for (int y = x + 1; y < RC; y++) dup |= (y < nrep) && reps[x] == reps[y];
                 if (dup) fst[F_DUP] = min(fst[F_DUP], pi);
             }
             if (want < nrep) fst[F_REMOVE] = min(fst[F_REMOVE], pi);
@@ -471,15 +463,12 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
                 if (elig) fst[F_EMPTY_ELIG] = min(fst[F_EMPTY_ELIG], pi);
             }
             if (meta_dis(m)) fst[F_DIS] = min(fst[F_DIS], pi);
-            if (a.rebalance && elig && nrep > 0 && (int)P.r[0][j] == heavy) fst[F_LEAD] = min(fst[F_LEAD], pi);
+            if (a.rebalance && elig && nrep > 0 && (int)reps[0] == heavy) fst[F_LEAD] = min(fst[F_LEAD], pi);
             if (!elig || nrep == 0) continue;
-            uint32_t reps[RC];
-#pragma unroll
-            for (int k = 0; k < RC; k++) reps[k] = P.r[k][j];
             int nelig;
             const int tb = first_target<RC, LSETS>(a, s_set, m, reps, nrep, &nelig);
             if (tb < 0) continue;
-            const double delta = P.w[j] * inv_avg;
+            const double delta = P.wt(j) * inv_avg;
             const double dt = dtgt(s_r[tb], delta);
             const unsigned long long ne = (unsigned long long)(nelig - (int)meta_nin(m));
             if (a.allow_leader) {
@@ -497,25 +486,25 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
         }
         // wave minima; the census runs only where a wave minimum can be within 8*eps
         // of the step's global minimum, which is at most ub (k_step's upper bound)
-        const double tL = wave_min(lL), tN = wave_min(lN);
         // (g <= ub + 2*eps: the first-target score is monotone in the target up to 2*eps)
+        const double tL = wave_min(lL), tN = wave_min(lN);
         const bool hasL = tL < HUGE_VAL && tL <= ubL + 12.0 * eps;
         const bool hasN = tN < HUGE_VAL && tN <= ubN + 12.0 * eps;
         if (!(a.dbg & 1) && ((hasL && lL <= tL + 8.0 * eps) || (hasN && lN <= tN + 8.0 * eps))) {
-            // the (partition, slot) pairs within 8*eps of the tile minimum, as bits j*16 + slot
+            // the (partition, slot) pairs within 8*eps of the wave minimum, as bits j*16 + slot
             uint32_t todo = 0;
 #pragma unroll
             for (int j = 0; j < PER_LANE; j++) {
-                const uint32_t m = P.m[j];
+                const uint32_t m = P.mt(j);
                 const int nrep = (int)meta_nrep(m);
                 if (base + j >= a.shard_end || !meta_elig(m) || nrep == 0) continue;
                 uint32_t reps[RC];
 #pragma unroll
-                for (int k = 0; k < RC; k++) reps[k] = P.r[k][j];
+                for (int k = 0; k < RC; k++) reps[k] = P.rp(k, j);
                 int nelig;
                 const int tb = first_target<RC, LSETS>(a, s_set, m, reps, nrep, &nelig);
                 if (tb < 0) continue;
-                const double delta = P.w[j] * inv_avg;
+                const double delta = P.wt(j) * inv_avg;
                 const double dt = dtgt(s_r[tb], delta);
                 if (hasL && a.allow_leader && dsrc(s_r[reps[0]], delta) + dt <= tL + 8.0 * eps)
                     todo |= 1u << (j * 16);
@@ -529,11 +518,11 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
                 const int bit = __ffs(todo) - 1;
                 todo &= todo - 1;
                 const int j = bit >> 4, k = bit & 15;
-                const uint32_t m = j ? P.m[1] : P.m[0];
-                const double w = j ? P.w[1] : P.w[0];
+                const uint32_t m = P.mt(j);
+                const double w = P.wt(j);
                 uint32_t reps[RC];
 #pragma unroll
-                for (int q = 0; q < RC; q++) reps[q] = j ? P.r[q][1] : P.r[q][0];
+                for (int q = 0; q < RC; q++) reps[q] = P.rp(q, j);
                 uint32_t src = reps[0];
 #pragma unroll
                 for (int q = 1; q < RC; q++) src = k == q ? reps[q] : src;
@@ -541,13 +530,27 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
                 const uint16_t* rec16 = LSETS ? (const uint16_t*)(s_set + (size_t)set * U)
                                               : (const uint16_t*)(a.setrec + (size_t)set * U);
                 const double ds = dsrc(s_r[src], w * inv_avg);
-                walk_targets<RC>(a, T, s_r, s_pos, s_blm, rec16, k ? 1 : 0, base + j, k, (int)src, reps, nrep, set, w, ds,
-                                 k ? tN : tL, eps, inv_avg, nblm);
+                walk_targets<RC>(a, T, s_r, s_pos, s_blm, rec16, k ? 1 : 0, base + j, k, (int)src, reps, nrep, set, w,
+                                 ds, k ? tN : tL, eps, inv_avg, nblm);
             }
         }
         wgL = tL < wgL ? tL : wgL;
         wgN = tN < wgN ? tN : wgN;
-        if (more) P = Pn;
+    };
+
+    // ping-pong between two register sets: the next tile's loads are in flight
+    // while the current one is scored
+    const long long lane_off = a.shard_begin + (long long)tid * PER_LANE;
+    // (the prefetch is unconditional -- a last tile re-loads itself -- so that the
+    // compiler waits for exactly the older tile's loads: vmcnt(N), not vmcnt(0))
+    for (; tile < a.ntiles; tile += 2 * a.nscan) {
+        const int t1 = tile + a.nscan;
+        load_parts<RC>(a, lane_off + (long long)(t1 < a.ntiles ? t1 : tile) * TILE, Bq);
+        score(A, lane_off + (long long)tile * TILE);
+        if (t1 >= a.ntiles) break;
+        const int t2 = t1 + a.nscan;
+        load_parts<RC>(a, lane_off + (long long)(t2 < a.ntiles ? t2 : t1) * TILE, A);
+        score(Bq, lane_off + (long long)t1 * TILE);
     }
     // workgroup record: counts, first-index predicates, minima, near-tie keys
     cL = wave_sum(cL);
@@ -647,10 +650,20 @@ __device__ void for_each_contender(const StepArgs& a, const double* s_ld, int ki
     }
 }
 
+// the control block lives in LDS for the whole k_step (one load round trip at the
+// start, stores only at the end): the serial code never waits on a global RMW
+constexpr int CTL_WORDS = (int)(offsetof(DevCtl, stamps) / 4);
+
 __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
     DevCtl* ctl = a.ctl;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     constexpr int NW = STEP_THREADS / 64;
+    __shared__ DevCtl C;
+    if (tid < CTL_WORDS) ((uint32_t*)&C)[tid] = ((const uint32_t*)ctl)[tid];
+    auto write_back = [&]() {
+        __syncthreads();
+        if (tid < CTL_WORDS) ((uint32_t*)ctl)[tid] = ((const uint32_t*)&C)[tid];
+    };
     __shared__ Decision D;
     __shared__ int s_done, s_i, s_fail, s_ndist, s_exact_need, s_nT, s_unc, s_nblm;
     __shared__ unsigned long long s_u[NW];
@@ -673,7 +686,8 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
     __shared__ int s_cntT[TMAX];
     __shared__ uint64_t s_blmb[MAXB / 64], s_presb[MAXB / 64];
     __shared__ uint32_t s_smark[MAX_SETS / 32];
-    Dedup T{s_key, s_wb, s_it, DEDUP_STEP};
+    __shared__ int s_nd[2], s_li[2], s_kfail[2];
+    Dedup T{s_key, s_wb, s_it, DEDUP_STEP, s_nd, s_li};
     const int B = a.B;
     KB_STAMP_BEGIN();
 
@@ -684,41 +698,46 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
         s_fl[b] = a.bfl[b];
         s_ord[b] = a.order[b];
     }
-    double d0 = HUGE_VAL, d1 = HUGE_VAL;
-    unsigned long long c0 = 0, c1 = 0;
-    uint32_t f[NF];
-#pragma unroll
-    for (int q = 0; q < NF; q++) f[q] = NONE32;
-    uint32_t flg = 0;
-    for (int i = tid; i < a.nrec; i += STEP_THREADS) {
-        const RecHdr* h = (const RecHdr*)(a.recs + (size_t)i * a.rec_stride);
-        d0 = h->dmin[0] < d0 ? h->dmin[0] : d0;
-        d1 = h->dmin[1] < d1 ? h->dmin[1] : d1;
-        c0 += h->cand[0]; c1 += h->cand[1];
-#pragma unroll
-        for (int q = 0; q < NF; q++) f[q] = min(f[q], h->first[q]);
-        flg |= h->flags;
-    }
-    const int halted = ctl->halted;
-    const bool do_res = ctl->prepped && ctl->steps < ctl->budget;
-    const double eps = ctl->eps, inv_avg = ctl->inv_avg, U0h = ctl->U0;
-    const int nblm0 = ctl->nblm, ndirty0 = ctl->ndirty;
-    const bool pend = ctl->pending_list != 0;
+    dedup_clear(T);
+    if (tid < 2) { s_nd[tid] = 0; s_li[tid] = -1; s_kfail[tid] = 0; }
+    __syncthreads();                               // the control block copy
+    const int halted = C.halted;
+    const bool do_res = C.prepped && C.steps < C.budget;
+    const double eps = C.eps, inv_avg = C.inv_avg, U0h = C.U0;
+    const int nblm0 = C.nblm, ndirty0 = C.ndirty;
+    const bool pend = C.pending_list != 0;
     __shared__ long long s_moved;
-    if (tid == 0) { s_nT = 0; s_done = 0; s_exact_need = 0; s_moved = -1; }
+    __shared__ int s_lkind, s_lpick;
+    __shared__ uint32_t s_lpart;
+    __shared__ int s_lrep[MAXR + 1];
+    __shared__ unsigned long long s_lsb[64];
+    if (tid == 0) { s_nT = 0; s_done = 0; s_exact_need = 0; s_moved = -1; s_lkind = 0; }
     if (halted != H_RUN) return;
     __syncthreads();
-
-    // ================================================================ resolve
+    // ---- the scan records (or the gathered rank summaries): one per thread, reduced
+    // per wave with DPP and across the waves by wave 0; then every thread collects
+    // its record's near-tie keys of both kinds within 4*eps of the minima (distinct
+    // keys, earliest iteration index per key)
     if (do_res) {
-        if (pend) do_list_op(ctl, a.L, &s_i);   // not consumed by a scan: do it here
-        // ---- combine the scan records (or the gathered rank summaries): every value
-        // reduced across the wave at once, then across the waves by wave 0
+        double d0 = HUGE_VAL, d1 = HUGE_VAL;
+        unsigned long long c0 = 0, c1 = 0;
+        uint32_t f[NF];
+#pragma unroll
+        for (int q = 0; q < NF; q++) f[q] = NONE32;
+        uint32_t flg = 0;
+        for (int i = tid; i < a.nrec; i += STEP_THREADS) {
+            const RecHdr* h = (const RecHdr*)(a.recs + (size_t)i * a.rec_stride);
+            d0 = h->dmin[0] < d0 ? h->dmin[0] : d0;
+            d1 = h->dmin[1] < d1 ? h->dmin[1] : d1;
+            c0 += h->cand[0]; c1 += h->cand[1];
+#pragma unroll
+            for (int q = 0; q < NF; q++) f[q] = min(f[q], h->first[q]);
+            flg |= h->flags;
+        }
         d0 = wave_min(d0); d1 = wave_min(d1); c0 = wave_sum(c0); c1 = wave_sum(c1);
 #pragma unroll
         for (int q = 0; q < NF; q++) f[q] = wave_min(f[q]);
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) flg |= __shfl_xor(flg, o);
+        flg = wave_red_or(flg);
         __shared__ double s_pd[2][NW];
         __shared__ unsigned long long s_pc[2][NW];
         __shared__ uint32_t s_pf[NF + 1][NW];
@@ -739,17 +758,53 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
             d0 = wave_min(d0); d1 = wave_min(d1); c0 = wave_sum(c0); c1 = wave_sum(c1);
 #pragma unroll
             for (int q = 0; q < NF; q++) f[q] = wave_min(f[q]);
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) flg |= __shfl_xor(flg, o);
+            flg = wave_red_or(flg);
             if (lane == 0) {
                 s_g[0] = d0; s_g[1] = d1; s_cand[0] = c0; s_cand[1] = c1;
 #pragma unroll
                 for (int q = 0; q < NF; q++) s_first[q] = f[q];
-                s_flags = flg | (a.use_spill && ctl->cont_overflow ? 1u : 0u);
+                s_flags = flg | (a.use_spill && C.cont_overflow ? 1u : 0u);
             }
         }
         __syncthreads();
-        KB_STAMP(ctl, 0);
+        const double g0 = s_g[0], g1 = s_g[1];
+        for (int i = tid; i < a.nrec; i += STEP_THREADS) {
+            const RecHdr* h = (const RecHdr*)(a.recs + (size_t)i * a.rec_stride);
+            const bool q0 = h->dmin[0] <= g0 + 8.0 * eps, q1 = h->dmin[1] <= g1 + 8.0 * eps;
+            if (!q0 && !q1) continue;
+            const Contender* keys = (const Contender*)(h + 1);
+            const int nk = (int)min(h->nkeys, (uint32_t)a.rec_keys);
+            for (int k = 0; k < nk; k++) {
+                const Contender c = keys[k];
+                if (!(c.kind ? q1 : q0)) continue;
+                if (cont_delta_ld(s_ld, c, inv_avg) <= (c.kind ? g1 : g0) + 4.0 * eps &&
+                    dedup_insert(T, c.kind, c.s, c.t, c.w, c.iter) < 0)
+                    s_kfail[c.kind] = 1;
+            }
+        }
+    }
+    __syncthreads();
+    if (do_res && a.use_spill && C.ncont > 0) {
+        // raw spills of the scan (rare): every thread
+        const uint32_t n = min(C.ncont, a.cont_cap);
+        for (uint32_t i = tid; i < n; i += STEP_THREADS) {
+            const Contender c = a.cont[i];
+            if (cont_delta_ld(s_ld, c, inv_avg) <= s_g[c.kind] + 4.0 * eps &&
+                dedup_insert(T, c.kind, c.s, c.t, c.w, c.iter) < 0)
+                s_kfail[c.kind] = 1;
+        }
+        __syncthreads();
+    }
+    KB_STAMP(ctl, 1);
+
+    // ================================================================ resolve
+    if (do_res) {
+        if (pend) {                              // not consumed by a scan: do it here
+            do_list_op(ctl, a.L, &s_i);
+            if (tid == 0) { C.pending_list = 0; C.list_overflow = ctl->list_overflow; }
+            __syncthreads();
+        }
+        KB_STAMP(ctl, 2);
 
         // ---- Validate(dup) / RemoveExtra / AddMissing / MoveDisallowed / ReassignLeaders
         if (tid == 0) {
@@ -758,7 +813,7 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
             D.from = -1; D.to = -1; D.su = su; D.cu = su; D.exact = 0; D.err = E_NONE; D.err_broker = -1;
             const uint32_t* F = s_first;
             auto rd = [&](uint32_t p, int k) -> int { return (int)a.rep[(long long)k * a.Ppad + p]; };
-            if (ctl->list_overflow) {
+            if (C.list_overflow) {
                 D.status = -1; D.step = 8; D.err = E_LIST_OVERFLOW; s_done = 1;
             } else if (a.sem_go && F[F_DUP] != NONE32) {
                 D.status = -1; D.step = 1; D.err = E_DUP; D.part = F[F_DUP]; s_done = 1;
@@ -783,42 +838,9 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
                 }
                 s_done = 1;
             } else if (F[F_ADD] != NONE32) {                         // steps.go:93-113
-                const uint32_t p = F[F_ADD];
-                const uint32_t m = a.meta[p];
-                const int nrep = (int)meta_nrep(m), set = (int)meta_set(m);
-                const int32_t* dl = a.lists + ((size_t)set * 2 + 1) * a.K;
-                int t = -1;
-                for (int i = 0; i < a.K && t < 0; i++) {
-                    const int b = dl[i];
-                    if (b < 0) break;
-                    bool isrep = false;
-                    for (int k = 0; k < nrep; k++) isrep |= rd(p, k) == b;
-                    if (!isrep) t = b;
-                }
-                D.step = 4; D.part = p;
-                if (t < 0) { D.status = -1; D.err = E_ADD; }
-                else { D.status = 1; D.kind = 3; D.slot = nrep; D.from = -1; D.to = t; }
-                s_done = 1;
+                s_lkind = 2; s_lpart = F[F_ADD];                      // pick list below
             } else if (F[F_DIS] != NONE32) {                         // steps.go:117-143
-                const uint32_t p = F[F_DIS];
-                const uint32_t m = a.meta[p];
-                const int nrep = (int)meta_nrep(m), set = (int)meta_set(m);
-                const uint64_t* sb = a.setbits + (size_t)set * a.W64;
-                int vslot = -1;
-                for (int k = 0; k < nrep && vslot < 0; k++) if (!setbit(sb, rd(p, k))) vslot = k;
-                const int32_t* dl = a.lists + ((size_t)set * 2 + 0) * a.K;
-                int t = -1;
-                for (int i = 0; i < a.K && t < 0; i++) {
-                    const int b = dl[i];
-                    if (b < 0) break;
-                    bool isrep = false;
-                    for (int k = 0; k < nrep; k++) isrep |= rd(p, k) == b;
-                    if (!isrep) t = b;
-                }
-                D.step = 5; D.part = p; D.slot = vslot; D.from = rd(p, vslot);
-                if (t < 0) { D.status = -1; D.err = E_DIS; D.err_broker = D.from; }
-                else { D.status = 1; D.kind = 1; D.to = t; }
-                s_done = 1;
+                s_lkind = 1; s_lpart = F[F_DIS];
             } else if (a.rebalance) {                                 // steps.go:234-282
                 // su < MinUnbalance decides; certify it against eps or use the exact su
                 const bool lo = su + 2.0 * eps < a.min_unbalance, hi = su - 2.0 * eps >= a.min_unbalance;
@@ -830,6 +852,55 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
             }
         }
         __syncthreads();
+        if (s_lkind) {
+            // AddMissingReplicas / MoveDisallowedReplicas pick from the allowed brokers in
+            // (load, id) order from the heaviest down: getBrokerListByLoad over the load
+            // map with absent brokers at 0 (Add, utils.go:66-79), getBrokerListByLoadBL
+            // over the brokers holding replicas (Disallowed, utils.go:81-90)
+            const uint32_t p = s_lpart;
+            const uint32_t m = a.meta[p];
+            const int nrep = (int)meta_nrep(m), set = (int)meta_set(m);
+            if (wid == 0) {
+                if (lane < nrep) s_lrep[lane] = (int)a.rep[(long long)lane * a.Ppad + p];
+                const unsigned long long sbw = lane < a.W64 ? (unsigned long long)a.setbits[(size_t)set * a.W64 + lane] : 0ull;
+                s_lsb[lane] = sbw;
+                if (lane == 0) s_lpick = -1;
+                const unsigned long long lt = (1ull << lane) - 1ull;
+                bool done = false;
+                for (int base = 0; base < B && !done; base += 64) {
+                    const int k = base + lane;
+                    const int b = k < B ? s_ord[B - 1 - k] : 0;
+                    bool mem = k < B && ((s_lsb[b >> 6] >> (b & 63)) & 1ull);
+                    if (s_lkind == 1) mem = mem && (s_fl[b] & BF_PRESENT);
+                    bool isrep = false;
+                    for (int q = 0; q < nrep; q++) isrep |= s_lrep[q] == b;
+                    const bool ok = mem && !isrep;
+                    const unsigned long long bal = __ballot(ok);
+                    if (bal) {
+                        if (ok && (bal & lt) == 0) s_lpick = b;      // first eligible from the heavy end
+                        done = true;
+                    }
+                }
+            }
+            __syncthreads();
+            if (tid == 0) {
+                const int t = s_lpick;
+                if (s_lkind == 2) {
+                    D.step = 4; D.part = p;
+                    if (t < 0) { D.status = -1; D.err = E_ADD; }
+                    else { D.status = 1; D.kind = 3; D.slot = nrep; D.from = -1; D.to = t; }
+                } else {
+                    int vslot = -1;
+                    for (int k = 0; k < nrep && vslot < 0; k++)
+                        if (!((s_lsb[s_lrep[k] >> 6] >> (s_lrep[k] & 63)) & 1ull)) vslot = k;
+                    D.step = 5; D.part = p; D.slot = vslot; D.from = s_lrep[vslot];
+                    if (t < 0) { D.status = -1; D.err = E_DIS; D.err_broker = D.from; }
+                    else { D.status = 1; D.kind = 1; D.to = t; }
+                }
+                s_done = 1;
+            }
+            __syncthreads();
+        }
         // exact su (sequential folds in bl order); s_e doubles as the bl-ordered loads
         // (every load is exact here, so every error bound is zero)
         double* s_Lm = s_e;
@@ -842,7 +913,7 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
                 double U = 0.0;
                 for (int k = 0; k < nblm0; k++) U += term_x(s_Lm[k], avg);
                 s_sux = U;
-                atomicAdd(&ctl->total_folds, 1ull);
+                atomicAdd(&C.total_folds, 1ull);
             }
             __syncthreads();
         };
@@ -867,7 +938,7 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
                     } else if (F[F_LEAD] != NONE32) {
                         const uint32_t p = F[F_LEAD];
                         const int nrep = (int)meta_nrep(a.meta[p]);
-                        const int light = ctl->light;
+                        const int light = C.light;
                         int ex = -1;
                         for (int k = 0; k < nrep && ex < 0; k++) if (rd(p, k) == light) ex = k;
                         D.status = 1; D.step = 6; D.part = p; D.slot = 0; D.from = rd(p, 0); D.to = light;
@@ -878,7 +949,7 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
             }
             __syncthreads();
         }
-        KB_STAMP(ctl, 1);
+        KB_STAMP(ctl, 3);
 
         // ---- move(): leader step (if allowed), then non-leader step (steps.go:284-298)
         for (int kind = a.allow_leader ? 0 : 1; kind < 2 && !s_done && !s_exact_need; kind++) {
@@ -890,25 +961,12 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
                 } else if (s_flags & 1u) {
                     D.status = -1; D.step = step; D.err = E_CONT_OVERFLOW; s_done = 1;
                 }
-                s_fail = 0;
-                s_ndist = 0;
             }
-            dedup_clear(T);
             __syncthreads();
             if (s_done) break;
-            // (1) distinct keys of this kind (earliest iteration index per key)
-            if (g < HUGE_VAL)
-                for_each_contender(a, s_ld, kind, g, eps, inv_avg, [&](const Contender& c) {
-                    if (dedup_insert(T, c.kind, c.s, c.t, c.w, c.iter) < 0) s_fail = 1;
-                });
-            __syncthreads();
-            int nd = 0;
-            for (int h = tid; h < DEDUP_STEP; h += STEP_THREADS) nd += s_key[h] != NONE32 ? 1 : 0;
-            nd = wave_sum(nd);
-            if (lane == 0 && nd) atomicAdd(&s_ndist, nd);
-            __syncthreads();
-            const int ndist = s_ndist;
-            const bool fail = s_fail != 0;
+            // (1) the distinct keys of this kind were collected with the records
+            const int ndist = s_nd[kind];
+            const bool fail = s_kfail[kind] != 0;
             const bool have = ndist > 0 || fail;
             // (2) certified decision for one key; exact folds otherwise
             double Ua = 0.0;
@@ -916,11 +974,7 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
             cw.s = cw.t = -1; cw.w = 0; cw.iter = NONE64; cw.kind = kind; cw.pad = 0;
             bool certain = false, c_improved = false, c_take = false;
             if (!fail && ndist == 1) {
-                if (tid == 0) s_i = -1;
-                __syncthreads();
-                for (int h = tid; h < DEDUP_STEP; h += STEP_THREADS) if (s_key[h] != NONE32) s_i = h;
-                __syncthreads();
-                cw = dedup_entry(T, s_i);
+                cw = dedup_entry(T, s_li[kind]);    // the one claimed slot
                 Ua = U0h + cont_delta_ld(s_ld, cw, inv_avg);
                 // |Ua - U'| <= eps and |U0h - su| <= eps; margins of 3*eps on both decisions
                 const double thr = U0h - a.min_unbalance;
@@ -960,7 +1014,7 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
                     if (tid == 0) {
                         s_dv[0] = exact_unbalance_lds(s_Lm, nblm0, a.posm[cw.s], a.posm[cw.t],
                                                       s_ld[cw.s] - cw.w, s_ld[cw.t] + cw.w);
-                        atomicAdd(&ctl->total_folds, 1ull);
+                        atomicAdd(&C.total_folds, 1ull);
                     }
                     __syncthreads();
                     Ustar = s_dv[0];
@@ -980,12 +1034,12 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
                     };
                     if (!fail) {
                         for (int h = tid; h < DEDUP_STEP; h += STEP_THREADS)
-                            if (s_key[h] != NONE32) consider(dedup_entry(T, h));
+                            if (s_key[h] != NONE32 && (int)(s_key[h] >> 30) == kind) consider(dedup_entry(T, h));
                     } else {
                         for_each_contender(a, s_ld, kind, g, eps, inv_avg, consider);
                     }
                     nf = wave_sum(nf);
-                    if (lane == 0 && nf) atomicAdd(&ctl->total_folds, nf);
+                    if (lane == 0 && nf) atomicAdd(&C.total_folds, nf);
                     for (int o = 32; o > 0; o >>= 1) {
                         const double ou = __shfl_xor(bu, o);
                         const unsigned long long oi = __shfl_xor(bi, o);
@@ -1030,32 +1084,44 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
             }
             __syncthreads();
         }
-        KB_STAMP(ctl, 2);
+        KB_STAMP(ctl, 4);
 
         if (s_exact_need) {
             // the bounds cannot decide and some loads are approximate: refold first
             if (tid == 0) {
-                ctl->halted = H_NEED_EXACT;
-                ctl->prepped = 0;
-                ctl->total_exact_halts++;
+                C.halted = H_NEED_EXACT;
+                C.prepped = 0;
+                C.total_exact_halts++;
             }
+            write_back();
             return;
         }
 
         // ---------------------------------------------------------- apply
-        // (thread 0; its small arrays live in LDS, not in scratch memory)
+        // thread 0 decides; the loads it needs are issued by several lanes at once
+        // (three memory round trips); its small arrays live in LDS, not scratch
         __shared__ int rold[MAXR + 1], r[MAXR + 1];
         __shared__ int tb[2 * MAXR + 2], dcnt[2 * MAXR + 2], cv[2 * MAXR + 2];
         __shared__ double oc[2 * MAXR + 2], nc2[2 * MAXR + 2], av[2 * MAXR + 2];
+        __shared__ uint64_t s_sbw[MAXR + 1];
+        __shared__ uint32_t s_am;
+        __shared__ double s_aw;
+        __shared__ int s_anc, s_nn, s_na, s_mode;
+        const bool chg = D.status == 1;
+        const long long p = D.part;
+        KB_STAMP(ctl, 11);
+        if (chg) {
+            if (tid < a.RC) rold[tid] = (int)a.rep[(long long)tid * a.Ppad + p];
+            if (tid == 32) s_am = a.meta[p];
+            if (tid == 33) s_aw = a.w[p];
+            if (tid == 34) s_anc = a.nc[p];
+        }
+        __syncthreads();
+        KB_STAMP(ctl, 12);
         if (tid == 0) {
-            int nT = 0;
-            if (D.status == 1) {
-                const long long p = D.part;
-                // the partition (one round trip)
-                const uint32_t m = a.meta[p];
-                for (int k = 0; k < a.RC; k++) rold[k] = (int)a.rep[(long long)k * a.Ppad + p];
-                const double wv = a.w[p];
-                const int ncp = a.nc[p];
+            s_mode = 0;
+            if (chg) {
+                const uint32_t m = s_am;
                 const int nrep = (int)meta_nrep(m);
                 for (int k = 0; k < nrep; k++) r[k] = rold[k];
                 int nn = nrep;
@@ -1076,77 +1142,103 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
                     if (a.sem_go) state_changed = false;     // the append is not visible through pl
                     else { r[nrep] = D.to; nn = nrep + 1; }
                 }
-                const uint64_t* sb = a.setbits + (size_t)meta_set(m) * a.W64;
-                auto remeta = [&](int n) {
-                    uint32_t dis = 0, nin = 0;
-                    for (int k = 0; k < n; k++) { const bool in = setbit(sb, r[k]); dis |= in ? 0u : 1u; nin += in ? 1u : 0u; }
-                    return make_meta((uint32_t)n, meta_want(m), meta_elig(m), dis, nin, meta_set(m));
-                };
                 if (a.sem_go && (D.kind == 2 || D.kind == 3)) {
-                    // Go aliasing: the remove shifted the shared backing array in place
-                    if (D.kind == 2) {
-                        for (int k = 0; k < nrep; k++) a.rep[(long long)k * a.Ppad + p] = (uint16_t)r[k];
-                        a.meta[p] = remeta(nrep);
-                    }
+                    s_mode = D.kind == 2 ? 1 : 0;            // Go aliasing: the remove shifted the array in place
+                    s_nn = nrep;
                 } else if (state_changed) {
-                    for (int k = 0; k < nn; k++) a.rep[(long long)k * a.Ppad + p] = (uint16_t)r[k];
-                    a.meta[p] = remeta(nn);
-                    // brokers whose contribution changed: old vs new (getBrokerLoad, utils.go:92-105)
-                    int na = 0;
-                    auto slot_of = [&](int b) {
-                        for (int x = 0; x < na; x++) if (tb[x] == b) return x;
-                        tb[na] = b; oc[na] = 0.0; nc2[na] = 0.0; dcnt[na] = 0;
-                        return na++;
-                    };
-                    for (int k = 0; k < nrep; k++) {
-                        const int x = slot_of(rold[k]);
-                        oc[x] = k == 0 ? wv * (double)(nrep + ncp) : wv;
-                        dcnt[x]--;
+                    s_mode = 2;
+                    s_nn = nn;
+                }
+            }
+        }
+        __syncthreads();
+        const int mode = s_mode;
+        if (mode) {
+            // the allowed-set words of the new replicas (Disallowed trigger, in-set count)
+            if (tid < s_nn) s_sbw[tid] = a.setbits[(size_t)meta_set(s_am) * a.W64 + (r[tid] >> 6)];
+        }
+        __syncthreads();
+        if (tid == 0 && mode) {
+            const uint32_t m = s_am;
+            const int n = s_nn;
+            uint32_t dis = 0, nin = 0;
+            for (int k = 0; k < n; k++) {
+                const bool in = (s_sbw[k] >> (r[k] & 63)) & 1ull;
+                dis |= in ? 0u : 1u;
+                nin += in ? 1u : 0u;
+            }
+            for (int k = 0; k < n; k++) a.rep[(long long)k * a.Ppad + p] = (uint16_t)r[k];
+            a.meta[p] = make_meta((uint32_t)n, meta_want(m), meta_elig(m), dis, nin, meta_set(m));
+            // brokers whose contribution changed: old vs new (getBrokerLoad, utils.go:92-105)
+            int na = 0;
+            if (mode == 2) {
+                const int nrep = (int)meta_nrep(m);
+                const double wv = s_aw;
+                const int ncp = s_anc;
+                auto slot_of = [&](int b) {
+                    for (int x = 0; x < na; x++) if (tb[x] == b) return x;
+                    tb[na] = b; oc[na] = 0.0; nc2[na] = 0.0; dcnt[na] = 0;
+                    return na++;
+                };
+                for (int k = 0; k < nrep; k++) {
+                    const int x = slot_of(rold[k]);
+                    oc[x] = k == 0 ? wv * (double)(nrep + ncp) : wv;
+                    dcnt[x]--;
+                }
+                for (int k = 0; k < n; k++) {
+                    const int x = slot_of(r[k]);
+                    nc2[x] = k == 0 ? wv * (double)(n + ncp) : wv;
+                    dcnt[x]++;
+                }
+            }
+            s_na = na;
+        }
+        __syncthreads();
+        KB_STAMP(ctl, 13);
+        // their counts and error terms
+        if (mode == 2 && tid < s_na) { cv[tid] = a.cnt[tb[tid]]; av[tid] = a.integral ? 0.0 : a.lerr[tb[tid]]; }
+        __syncthreads();
+        KB_STAMP(ctl, 14);
+        if (tid == 0) {
+            int nT = 0;
+            if (mode == 2) {
+                const int na = s_na;
+                const double u = DBL_EPSILON / 2;
+                int dd = 0;
+                for (int x = 0; x < na; x++) {
+                    const int b = tb[x];
+                    const int cnew = cv[x] + dcnt[x];
+                    if (dcnt[x]) a.cnt[b] = cnew;
+                    if (oc[x] == nc2[x]) continue;               // unchanged contribution
+                    const double L = s_ld[b];
+                    uint8_t fl = s_fl[b] & ~BF_PRESENT;
+                    if (cnew > 0) fl |= BF_PRESENT;
+                    double Ln, eb = 0.0;
+                    if (a.integral) {
+                        Ln = (L - oc[x]) + nc2[x];
+                    } else {
+                        // bounded incremental update; the exact fold comes with k_refresh
+                        const double x1 = L - oc[x];
+                        Ln = x1 + nc2[x];
+                        double ae = av[x] + 1.01 * u * (fabs(x1) + fabs(Ln));
+                        if (!(Ln > 0.0)) Ln = 0.0;               // loads are sums of non-negative terms
+                        if (cnew == 0) { Ln = 0.0; ae = 0.0; }  // empty fold: exactly 0
+                        a.lerr[b] = ae;
+                        const bool dirty = cnew > 0;
+                        if (dirty != ((fl & BF_DIRTY) != 0)) dd += dirty ? 1 : -1;
+                        fl = dirty ? (uint8_t)(fl | BF_DIRTY) : (uint8_t)(fl & ~BF_DIRTY);
+                        eb = dirty ? ae + gamma_n(cnew) * (Ln + ae) : 0.0;
                     }
-                    for (int k = 0; k < nn; k++) {
-                        const int x = slot_of(r[k]);
-                        nc2[x] = k == 0 ? wv * (double)(nn + ncp) : wv;
-                        dcnt[x]++;
-                    }
-                    // their counts and error terms (one round trip)
-                    for (int x = 0; x < na; x++) { cv[x] = a.cnt[tb[x]]; if (!a.integral) av[x] = a.lerr[tb[x]]; }
-                    const double u = DBL_EPSILON / 2;
-                    int dd = 0;
-                    for (int x = 0; x < na; x++) {
-                        const int b = tb[x];
-                        const int cnew = cv[x] + dcnt[x];
-                        if (dcnt[x]) a.cnt[b] = cnew;
-                        if (oc[x] == nc2[x]) continue;               // unchanged contribution
-                        const double L = s_ld[b];
-                        uint8_t fl = s_fl[b] & ~BF_PRESENT;
-                        if (cnew > 0) fl |= BF_PRESENT;
-                        double Ln, eb = 0.0;
-                        if (a.integral) {
-                            Ln = (L - oc[x]) + nc2[x];
-                        } else {
-                            // bounded incremental update; the exact fold comes with k_refresh
-                            const double x1 = L - oc[x];
-                            Ln = x1 + nc2[x];
-                            double ae = av[x] + 1.01 * u * (fabs(x1) + fabs(Ln));
-                            if (!(Ln > 0.0)) Ln = 0.0;               // loads are sums of non-negative terms
-                            if (cnew == 0) { Ln = 0.0; ae = 0.0; }  // empty fold: exactly 0
-                            a.lerr[b] = ae;
-                            const bool dirty = cnew > 0;
-                            if (dirty != ((fl & BF_DIRTY) != 0)) dd += dirty ? 1 : -1;
-                            fl = dirty ? (uint8_t)(fl | BF_DIRTY) : (uint8_t)(fl & ~BF_DIRTY);
-                            eb = dirty ? ae + gamma_n(cnew) * (Ln + ae) : 0.0;
-                        }
-                        a.load[b] = Ln; s_ld[b] = Ln;
-                        a.eb[b] = eb; s_e[b] = eb;
-                        a.bfl[b] = fl; s_fl[b] = fl;
-                        if (nT < TMAX) s_T[nT++] = b;
-                    }
-                    if (dd) ctl->ndirty += dd;
-                    // the per-broker partition lists follow in the next scan (k_scan's list workgroup)
-                    if (!a.integral && (D.kind == 1 || D.kind == 2 || D.kind == 3)) {
-                        ctl->pl_kind = D.kind; ctl->pl_from = D.from; ctl->pl_to = D.to; ctl->pl_part = p;
-                        ctl->pending_list = 1;
-                    }
+                    a.load[b] = Ln; s_ld[b] = Ln;
+                    a.eb[b] = eb; s_e[b] = eb;
+                    a.bfl[b] = fl; s_fl[b] = fl;
+                    if (nT < TMAX) s_T[nT++] = b;
+                }
+                if (dd) C.ndirty += dd;
+                // the per-broker partition lists follow in the next scan (k_scan's list workgroup)
+                if (!a.integral && (D.kind == 1 || D.kind == 2 || D.kind == 3)) {
+                    C.pl_kind = D.kind; C.pl_from = D.from; C.pl_to = D.to; C.pl_part = p;
+                    C.pending_list = 1;
                 }
             }
             s_nT = nT;
@@ -1156,27 +1248,27 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
             ch.status = D.status; ch.step = D.step; ch.kind = D.kind; ch.slot = D.slot;
             ch.part = D.part; ch.from = D.from; ch.to = D.to; ch.su = D.su; ch.cu = D.cu;
             ch.exact = D.exact; ch.err_code = D.err; ch.err_broker = D.err_broker; ch.pad = 0;
-            if (ctl->logpos < ctl->logcap) a.log[ctl->logpos] = ch;
-            ctl->logpos++;
-            ctl->steps++;
+            if (C.logpos < C.logcap) a.log[C.logpos] = ch;
+            C.logpos++;
+            C.steps++;
             // reference candidate count of the steps that actually ran this iteration
             unsigned long long add = 0;
             if (D.step < 0 || D.step >= 7) {
                 if (a.allow_leader) add += s_cand[0];
                 if (D.step != 7) add += s_cand[1];
             }
-            ctl->total_cand += add;
-            ctl->total_cont += (unsigned long long)s_ndist;
-            if (D.status != 1) { ctl->halted = H_DONE; ctl->prepped = 0; }
+            C.total_cand += add;
+            C.total_cont += (unsigned long long)(s_nd[0] + s_nd[1]);
+            if (D.status != 1) { C.halted = H_DONE; C.prepped = 0; }
         }
         __syncthreads();
-        if (D.status != 1) return;
-        KB_STAMP(ctl, 3);
+        if (D.status != 1) { write_back(); return; }
+        KB_STAMP(ctl, 5);
     }
 
     // ================================================================== prep
     // (next step): getBL's (load, id) order, bl_move, relative loads, eps, sets
-    const bool full = ctl->full_prep != 0;
+    const bool full = C.full_prep != 0;
     const int nT = s_nT;
     if (full) {
         // every load is exact here (fresh state or after k_refresh): s_e holds the sort keys
@@ -1255,7 +1347,7 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
         }
     }
     __syncthreads();
-    KB_STAMP(ctl, 4);
+    KB_STAMP(ctl, 6);
     // bl_move = brokers present in the load map or listed in -broker-ids (steps.go:150-157)
     for (int w = tid; w < MAXB / 64; w += STEP_THREADS) { s_blmb[w] = 0; s_presb[w] = 0; }
     if (tid == 0) s_unc = 0;
@@ -1309,9 +1401,11 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
     __syncthreads();
     const int nblm = s_nblm;
     if (s_unc) {
-        if (tid == 0) { ctl->halted = H_NEED_EXACT; ctl->prepped = 0; ctl->total_exact_halts++; }
+        if (tid == 0) { C.halted = H_NEED_EXACT; C.prepped = 0; C.total_exact_halts++; }
+        write_back();
         return;
     }
+    KB_STAMP(ctl, 8);
     // approximate S (exact in integral mode: integers below 2^52), total load error E
     double sS = 0.0, sE = 0.0;
     for (int b = tid; b < B; b += STEP_THREADS)
@@ -1380,12 +1474,12 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
         double epsl = 16.0 * Ea * (V / (n > 0 ? n : 1.0) + R + 1.0) + 4.0 * Ea * Ea;
         double ep = epsf + epsl;
         if (!(ep > 1e-300)) ep = 1e-300;
-        ctl->S = S; ctl->avg = avg; ctl->inv_avg = iav; ctl->U0 = U0;
-        ctl->V = V; ctl->eps = ep; ctl->E = E; ctl->nblm = nblm;
-        ctl->ub[0] = ub0; ctl->ub[1] = ub1;
-        ctl->want_refresh = (epsl > epsf || ctl->ndirty >= 256) ? 1 : 0;
-        ctl->ncont = 0;
-        ctl->cont_overflow = 0;
+        C.S = S; C.avg = avg; C.inv_avg = iav; C.U0 = U0;
+        C.V = V; C.eps = ep; C.E = E; C.nblm = nblm;
+        C.ub[0] = ub0; C.ub[1] = ub1;
+        C.want_refresh = (epsl > epsf || C.ndirty >= 256) ? 1 : 0;
+        C.ncont = 0;
+        C.cont_overflow = 0;
     }
     if (wid == 0) {
         // first / last bl_move broker in universe order (scan the order from both ends)
@@ -1397,11 +1491,11 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
         lo = wave_min(lo);
         hi = wave_max(hi);
         if (lane == 0) {
-            ctl->light = lo < 0x7FFFFFFF ? s_ord[lo] : -1;
-            ctl->heavy = hi >= 0 ? s_ord[hi] : -1;
+            C.light = lo < 0x7FFFFFFF ? s_ord[lo] : -1;
+            C.heavy = hi >= 0 ? s_ord[hi] : -1;
         }
     }
-    KB_STAMP(ctl, 5);
+    KB_STAMP(ctl, 9);
     // ---- set records: full, or the sets containing a touched broker
     for (int w = tid; w < (a.nsets + 31) / 32; w += STEP_THREADS) s_smark[w] = full ? 0xFFFFFFFFu : 0u;
     __syncthreads();
@@ -1416,49 +1510,42 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
     }
     __syncthreads();
     {
+        __shared__ unsigned long long s_wsb[NW][64];
         const unsigned long long lt = (1ull << lane) - 1ull;
-        const int K = a.K, KR = a.KR;
+        const int KR = a.KR;
         for (int set = wid; set < a.nsets; set += NW) {
             if (!((s_smark[set >> 5] >> (set & 31)) & 1u)) continue;
             const unsigned long long sbw = lane < a.W64 ? (unsigned long long)a.setbits[(size_t)set * a.W64 + lane] : 0ull;
-            auto inset = [&](int b) -> bool {
-                const unsigned long long wv = __shfl(sbw, b >> 6);
-                return (wv >> (b & 63)) & 1ull;
-            };
+            s_wsb[wid][lane] = sbw;
+            auto inset = [&](int b) -> bool { return (s_wsb[wid][b >> 6] >> (b & 63)) & 1ull; };
             uint16_t* rec16 = (uint16_t*)(a.setrec + (size_t)set * a.units);
-            // kind 0: first KR of set ∩ bl_move ascending; 1: last K of set ∩ present; 2: last K of set
-            for (int kind = 0; kind < 3; kind++) {
-                const int cap = kind == 0 ? KR : K;
+            // the first KR brokers of set ∩ bl_move in bl order (move targets, steps.go:192-201)
+            {
+                const int cap = KR;
                 int found = 0;
                 for (int base = 0; base < B && found < cap; base += 64) {
                     const int k = base + lane;
-                    const int b = k < B ? s_ord[kind == 0 ? k : B - 1 - k] : 0;
+                    const int b = k < B ? s_ord[k] : 0;
                     bool mem = inset(b) && k < B;
-                    if (kind == 0) mem = mem && ((s_blmb[b >> 6] >> (b & 63)) & 1ull);
-                    else if (kind == 1) mem = mem && ((s_presb[b >> 6] >> (b & 63)) & 1ull);
+                    mem = mem && ((s_blmb[b >> 6] >> (b & 63)) & 1ull);
                     const unsigned long long m = __ballot(mem);
                     if (mem) {
                         const int rk = found + (int)__popcll(m & lt);
-                        if (rk < cap) {
-                            if (kind == 0) rec16[2 + rk] = (uint16_t)b;
-                            else a.lists[((size_t)set * 2 + (kind - 1)) * K + rk] = b;
-                        }
+                        if (rk < cap) rec16[2 + rk] = (uint16_t)b;
                     }
                     found += (int)__popcll(m);
                 }
-                for (int rk = found + lane; rk < cap; rk += 64) {
-                    if (kind == 0) rec16[2 + rk] = NONE16;
-                    else a.lists[((size_t)set * 2 + (kind - 1)) * K + rk] = -1;
-                }
-                if (kind == 0 && lane == 0) rec16[1] = (uint16_t)(found < cap ? found : cap);
+                for (int rk = found + lane; rk < cap; rk += 64) rec16[2 + rk] = NONE16;
+                if (lane == 0) rec16[1] = (uint16_t)(found < cap ? found : cap);
             }
             int n = lane < a.W64 ? (int)__popcll(sbw & s_blmb[lane]) : 0;
             n = wave_sum(n);
             if (lane == 0) rec16[0] = (uint16_t)n;
         }
     }
-    if (tid == 0) { ctl->prepped = 1; ctl->full_prep = 0; }
-    KB_STAMP(ctl, 6);
+    if (tid == 0) { C.prepped = 1; C.full_prep = 0; }
+    KB_STAMP(ctl, 10);
+    write_back();
 }
 
 // ------------------------------------------------------------- k_listop

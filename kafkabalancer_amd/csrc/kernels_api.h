@@ -47,7 +47,6 @@ struct StepArgs {
     int RC, KR, K, units, W64, B, nsets, NP2;
     const uint64_t* setbits;
     uint4* setrec;
-    int32_t* lists;           // [nsets][2][K]: desc present (Disallowed), desc universe (Add)
     int32_t* order;           // [B] universe sorted by (load, id)
     int32_t* posu;            // [B] position in order
     int32_t* blm;             // [B] bl_move order

@@ -3,4 +3,4 @@ for s in 5 200; do
   KB_PROBE_STEPS=$s timeout -k 10 120 python -u tools/scan_probe.py >> gpurun_out/exp.log 2>&1 || exit 1
   KB_PROBE_STEPS=$s KB_DEBUG_SCAN=1 timeout -k 10 120 python -u tools/scan_probe.py >> gpurun_out/exp.log 2>&1 || exit 1
 done
-KB_PROBE_STEPS=5 KB_ENGINE_LIB=$PWD/kafkabalancer_amd/lib/libkbengine_stamps.so timeout -k 10 120 python -u tools/scan_probe.py >> gpurun_out/exp.log 2>&1 || exit 1
+for n in 256 1024; do KB_NSCAN=$n timeout -k 10 120 python -u tools/scan_probe.py >> gpurun_out/exp.log 2>&1 || exit 1; done
