@@ -128,8 +128,7 @@ def main():
         st = eng.stamps()
         n = max(1, st1["steps"])
         names = [None, "step.loads", "res.reduce", "res.pred", "res.move", "res.apply(tail)", "prep.sort", None,
-                 "prep.blm+cert", "prep.S+r+eps+ub", "prep.sets", "res.move->apply", "apply.load_p",
-                 "apply.decide+sbw+remeta", "apply.load_cnt"]
+                 "prep.blm+cert", "prep.S+r+eps+ub", "prep.sets", "res.move->apply"]
         counts = {"spills": 7, "emits": 15}
         print(json.dumps({"stamps_us_per_step": {k: st[i] / 100.0 / n for i, k in enumerate(names) if k},
                           "counts_per_step": {k: st[i] / n for k, i in counts.items()},

@@ -665,7 +665,7 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
         if (tid < CTL_WORDS) ((uint32_t*)ctl)[tid] = ((const uint32_t*)&C)[tid];
     };
     __shared__ Decision D;
-    __shared__ int s_done, s_i, s_fail, s_ndist, s_exact_need, s_nT, s_unc, s_nblm;
+    __shared__ int s_done, s_i, s_exact_need, s_nT, s_unc, s_nblm;
     __shared__ unsigned long long s_u[NW];
     __shared__ double s_dv[NW];
     __shared__ int s_bs[NW], s_bt[NW];
@@ -1098,149 +1098,138 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
         }
 
         // ---------------------------------------------------------- apply
-        // thread 0 decides; the loads it needs are issued by several lanes at once
-        // (three memory round trips); its small arrays live in LDS, not scratch
-        __shared__ int rold[MAXR + 1], r[MAXR + 1];
-        __shared__ int tb[2 * MAXR + 2], dcnt[2 * MAXR + 2], cv[2 * MAXR + 2];
-        __shared__ double oc[2 * MAXR + 2], nc2[2 * MAXR + 2], av[2 * MAXR + 2];
-        __shared__ uint64_t s_sbw[MAXR + 1];
-        __shared__ uint32_t s_am;
-        __shared__ double s_aw;
-        __shared__ int s_anc, s_nn, s_na, s_mode;
-        const bool chg = D.status == 1;
-        const long long p = D.part;
+        // wave 0, one lane per replica slot (lanes 0..15 the old replicas, 16..31 the
+        // new ones); cross-lane work by ballot / readlane, three memory round trips
         KB_STAMP(ctl, 11);
-        if (chg) {
-            if (tid < a.RC) rold[tid] = (int)a.rep[(long long)tid * a.Ppad + p];
-            if (tid == 32) s_am = a.meta[p];
-            if (tid == 33) s_aw = a.w[p];
-            if (tid == 34) s_anc = a.nc[p];
-        }
-        __syncthreads();
-        KB_STAMP(ctl, 12);
-        if (tid == 0) {
-            s_mode = 0;
-            if (chg) {
-                const uint32_t m = s_am;
-                const int nrep = (int)meta_nrep(m);
-                for (int k = 0; k < nrep; k++) r[k] = rold[k];
-                int nn = nrep;
-                bool state_changed = true;
-                if (D.kind == 1) {                           // replace at slot (utils.go:186-190)
-                    r[D.slot] = D.to;
-                } else if (D.kind == 4) {                    // swap with the existing replica (utils.go:179-185)
-                    int ex = 0;
-                    for (int k = 0; k < nrep; k++) if (r[k] == D.to) { ex = k; break; }
-                    const int old = r[D.slot];
-                    r[D.slot] = D.to;
-                    r[ex] = old;
-                } else if (D.kind == 2) {                    // remove (utils.go:176-178)
-                    for (int k = D.slot; k + 1 < nrep; k++) r[k] = r[k + 1];
-                    if (a.sem_go) state_changed = false;     // pl keeps its length: duplicates
-                    else nn = nrep - 1;
-                } else if (D.kind == 3) {                    // add (utils.go:199-202)
-                    if (a.sem_go) state_changed = false;     // the append is not visible through pl
-                    else { r[nrep] = D.to; nn = nrep + 1; }
-                }
-                if (a.sem_go && (D.kind == 2 || D.kind == 3)) {
-                    s_mode = D.kind == 2 ? 1 : 0;            // Go aliasing: the remove shifted the array in place
-                    s_nn = nrep;
-                } else if (state_changed) {
-                    s_mode = 2;
-                    s_nn = nn;
-                }
-            }
-        }
-        __syncthreads();
-        const int mode = s_mode;
-        if (mode) {
-            // the allowed-set words of the new replicas (Disallowed trigger, in-set count)
-            if (tid < s_nn) s_sbw[tid] = a.setbits[(size_t)meta_set(s_am) * a.W64 + (r[tid] >> 6)];
-        }
-        __syncthreads();
-        if (tid == 0 && mode) {
-            const uint32_t m = s_am;
-            const int n = s_nn;
-            uint32_t dis = 0, nin = 0;
-            for (int k = 0; k < n; k++) {
-                const bool in = (s_sbw[k] >> (r[k] & 63)) & 1ull;
-                dis |= in ? 0u : 1u;
-                nin += in ? 1u : 0u;
-            }
-            for (int k = 0; k < n; k++) a.rep[(long long)k * a.Ppad + p] = (uint16_t)r[k];
-            a.meta[p] = make_meta((uint32_t)n, meta_want(m), meta_elig(m), dis, nin, meta_set(m));
-            // brokers whose contribution changed: old vs new (getBrokerLoad, utils.go:92-105)
-            int na = 0;
-            if (mode == 2) {
-                const int nrep = (int)meta_nrep(m);
-                const double wv = s_aw;
-                const int ncp = s_anc;
-                auto slot_of = [&](int b) {
-                    for (int x = 0; x < na; x++) if (tb[x] == b) return x;
-                    tb[na] = b; oc[na] = 0.0; nc2[na] = 0.0; dcnt[na] = 0;
-                    return na++;
-                };
-                for (int k = 0; k < nrep; k++) {
-                    const int x = slot_of(rold[k]);
-                    oc[x] = k == 0 ? wv * (double)(nrep + ncp) : wv;
-                    dcnt[x]--;
-                }
-                for (int k = 0; k < n; k++) {
-                    const int x = slot_of(r[k]);
-                    nc2[x] = k == 0 ? wv * (double)(n + ncp) : wv;
-                    dcnt[x]++;
-                }
-            }
-            s_na = na;
-        }
-        __syncthreads();
-        KB_STAMP(ctl, 13);
-        // their counts and error terms
-        if (mode == 2 && tid < s_na) { cv[tid] = a.cnt[tb[tid]]; av[tid] = a.integral ? 0.0 : a.lerr[tb[tid]]; }
-        __syncthreads();
-        KB_STAMP(ctl, 14);
-        if (tid == 0) {
+        if (wid == 0) {
             int nT = 0;
-            if (mode == 2) {
-                const int na = s_na;
-                const double u = DBL_EPSILON / 2;
-                int dd = 0;
-                for (int x = 0; x < na; x++) {
-                    const int b = tb[x];
-                    const int cnew = cv[x] + dcnt[x];
-                    if (dcnt[x]) a.cnt[b] = cnew;
-                    if (oc[x] == nc2[x]) continue;               // unchanged contribution
-                    const double L = s_ld[b];
-                    uint8_t fl = s_fl[b] & ~BF_PRESENT;
-                    if (cnew > 0) fl |= BF_PRESENT;
-                    double Ln, eb = 0.0;
-                    if (a.integral) {
-                        Ln = (L - oc[x]) + nc2[x];
-                    } else {
-                        // bounded incremental update; the exact fold comes with k_refresh
-                        const double x1 = L - oc[x];
-                        Ln = x1 + nc2[x];
-                        double ae = av[x] + 1.01 * u * (fabs(x1) + fabs(Ln));
-                        if (!(Ln > 0.0)) Ln = 0.0;               // loads are sums of non-negative terms
-                        if (cnew == 0) { Ln = 0.0; ae = 0.0; }  // empty fold: exactly 0
-                        a.lerr[b] = ae;
-                        const bool dirty = cnew > 0;
-                        if (dirty != ((fl & BF_DIRTY) != 0)) dd += dirty ? 1 : -1;
-                        fl = dirty ? (uint8_t)(fl | BF_DIRTY) : (uint8_t)(fl & ~BF_DIRTY);
-                        eb = dirty ? ae + gamma_n(cnew) * (Ln + ae) : 0.0;
-                    }
-                    a.load[b] = Ln; s_ld[b] = Ln;
-                    a.eb[b] = eb; s_e[b] = eb;
-                    a.bfl[b] = fl; s_fl[b] = fl;
-                    if (nT < TMAX) s_T[nT++] = b;
+            const bool chg = D.status == 1;
+            const long long p = D.part;
+            const int kind = D.kind, slot = D.slot, to = D.to;
+            int ro = -1;                                 // old replica at slot `lane`
+            uint32_t m = 0;
+            double wv = 0.0;
+            int ncp = 0;
+            if (chg) {
+                if (lane < a.RC) ro = (int)a.rep[(long long)lane * a.Ppad + p];
+                m = a.meta[p];
+                wv = a.w[p];
+                ncp = a.nc[p];
+            }
+            const int nrep = (int)meta_nrep(m);
+            if (lane >= nrep) ro = -1;
+            // the new replica list (replacepl / addpl, utils.go:166-202)
+            int rn = ro, nn = nrep;
+            bool state_changed = chg;
+            const unsigned long long ball_to = __ballot(ro == to && lane < 16);
+            if (kind == 1) {                             // replace at slot (utils.go:186-190)
+                if (lane == slot) rn = to;
+            } else if (kind == 4) {                      // swap with the existing replica (utils.go:179-185)
+                const int ex = ball_to ? (int)__ffsll((long long)ball_to) - 1 : 0;
+                const int ro_slot = __shfl(ro, slot);
+                if (lane == slot) rn = to;
+                else if (lane == ex) rn = ro_slot;
+            } else if (kind == 2) {                      // remove (utils.go:176-178)
+                const int nxt = __shfl(ro, (lane + 1) & 63);
+                if (lane >= slot && lane + 1 < nrep) rn = nxt;
+                if (a.sem_go) state_changed = false;     // pl keeps its length: duplicates
+                else { nn = nrep - 1; if (lane == nn) rn = -1; }
+            } else if (kind == 3) {                      // add (utils.go:199-202)
+                if (a.sem_go) state_changed = false;     // the append is not visible through pl
+                else { nn = nrep + 1; if (lane == nrep) rn = to; }
+            }
+            const bool go_remove = chg && a.sem_go && kind == 2;
+            const int nw = go_remove ? nrep : nn;        // the replica slots written
+            if (state_changed || go_remove) {
+                // the allowed-set words of the new replicas (Disallowed trigger, in-set count)
+                bool in = false;
+                if (lane < nw) in = (a.setbits[(size_t)meta_set(m) * a.W64 + (rn >> 6)] >> (rn & 63)) & 1ull;
+                const unsigned long long bin = __ballot(in && lane < nw), bout = __ballot(!in && lane < nw);
+                if (lane < nw) a.rep[(long long)lane * a.Ppad + p] = (uint16_t)rn;
+                if (lane == 0)
+                    a.meta[p] = make_meta((uint32_t)nw, meta_want(m), meta_elig(m), bout ? 1u : 0u,
+                                          (uint32_t)__popcll(bin), meta_set(m));
+            }
+            if (state_changed) {
+                // contributions of getBrokerLoad (utils.go:92-105): the leader slot carries
+                // W * (len(R) + NumConsumers); lanes 0..15 hold the old replicas, 16..31 the new
+                const int j = lane & 15;
+                const bool old_lane = lane < 16 && j < nrep, new_lane = lane >= 16 && lane < 32 && j < nn;
+                const int rnew_j = __shfl(rn, j);
+                const int b = old_lane ? ro : (new_lane ? rnew_j : -1);
+                const double oc = old_lane ? (j == 0 ? wv * (double)(nrep + ncp) : wv) : 0.0;
+                const double nc_here = new_lane ? (j == 0 ? wv * (double)(nn + ncp) : wv) : 0.0;
+                // pair an old replica with the same broker among the new ones
+                double cn_other = 0.0;
+                bool matched = false;
+                for (int q = 0; q < 16; q++) {
+                    const int bq = __shfl(rn, q);           // new replica q
+                    const int bo = __shfl(ro, q);           // old replica q
+                    const double ncq = q < nn ? (q == 0 ? wv * (double)(nn + ncp) : wv) : 0.0;
+                    if (old_lane && q < nn && bq == b) { cn_other = ncq; matched = true; }
+                    if (new_lane && q < nrep && bo == b) matched = true;
                 }
-                if (dd) C.ndirty += dd;
-                // the per-broker partition lists follow in the next scan (k_scan's list workgroup)
-                if (!a.integral && (D.kind == 1 || D.kind == 2 || D.kind == 3)) {
-                    C.pl_kind = D.kind; C.pl_from = D.from; C.pl_to = D.to; C.pl_part = p;
-                    C.pending_list = 1;
+                // per broker: (old, new) contribution; new-only brokers from the new lanes
+                const bool rep_lane = old_lane || (new_lane && !matched);
+                const double oldc = old_lane ? oc : 0.0;
+                const double newc = old_lane ? cn_other : nc_here;
+                const int dcnt = old_lane ? (matched ? 0 : -1) : 1;
+                const bool touched = rep_lane && oldc != newc;
+                const bool cnt_changes = rep_lane && dcnt != 0;
+                int cv = 0;
+                double av = 0.0;
+                if (touched || cnt_changes) {               // their counts and error terms
+                    cv = a.cnt[b];
+                    if (!a.integral) av = a.lerr[b];
+                }
+                int dd = 0;
+                if (touched || cnt_changes) {
+                    const int cnew = cv + dcnt;
+                    if (dcnt) a.cnt[b] = cnew;
+                    if (touched) {
+                        const double L = s_ld[b];
+                        uint8_t fl = s_fl[b] & ~BF_PRESENT;
+                        if (cnew > 0) fl |= BF_PRESENT;
+                        double Ln, eb = 0.0;
+                        if (a.integral) {
+                            Ln = (L - oldc) + newc;
+                        } else {
+                            // bounded incremental update; the exact fold comes with k_refresh
+                            const double u = DBL_EPSILON / 2;
+                            const double x1 = L - oldc;
+                            Ln = x1 + newc;
+                            double ae = av + 1.01 * u * (fabs(x1) + fabs(Ln));
+                            if (!(Ln > 0.0)) Ln = 0.0;               // loads are sums of non-negative terms
+                            if (cnew == 0) { Ln = 0.0; ae = 0.0; }  // empty fold: exactly 0
+                            a.lerr[b] = ae;
+                            const bool dirty = cnew > 0;
+                            if (dirty != ((fl & BF_DIRTY) != 0)) dd = dirty ? 1 : -1;
+                            fl = dirty ? (uint8_t)(fl | BF_DIRTY) : (uint8_t)(fl & ~BF_DIRTY);
+                            eb = dirty ? ae + gamma_n(cnew) * (Ln + ae) : 0.0;
+                        }
+                        a.load[b] = Ln; s_ld[b] = Ln;
+                        a.eb[b] = eb; s_e[b] = eb;
+                        a.bfl[b] = fl; s_fl[b] = fl;
+                    }
+                }
+                dd = wave_sum(dd);
+                const unsigned long long bt = __ballot(touched);
+                if (touched) {
+                    const int k = (int)__popcll(bt & ((1ull << lane) - 1ull));
+                    if (k < TMAX) s_T[k] = b;
+                }
+                nT = (int)__popcll(bt);
+                if (nT > TMAX) nT = TMAX;
+                if (lane == 0) {
+                    if (dd) C.ndirty += dd;
+                    // the per-broker partition lists follow in the next scan (k_scan's list workgroup)
+                    if (!a.integral && (kind == 1 || kind == 2 || kind == 3)) {
+                        C.pl_kind = kind; C.pl_from = D.from; C.pl_to = to; C.pl_part = p;
+                        C.pending_list = 1;
+                    }
                 }
             }
+            if (lane == 0) {
             s_nT = nT;
             if (D.status == 1) s_moved = D.part;
             // log the step
@@ -1260,6 +1249,7 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
             C.total_cand += add;
             C.total_cont += (unsigned long long)(s_nd[0] + s_nd[1]);
             if (D.status != 1) { C.halted = H_DONE; C.prepped = 0; }
+            }
         }
         __syncthreads();
         if (D.status != 1) { write_back(); return; }
