@@ -127,9 +127,9 @@ def main():
     if args.stamps:
         st = eng.stamps()
         n = max(1, st1["steps"])
-        names = [None, "step.loads", "res.reduce", "res.pred", "res.move", "res.apply(tail)", "prep.sort", None,
-                 "prep.blm+cert", "prep.S+r+eps+ub", "prep.sets", "res.move->apply"]
-        counts = {"spills": 7, "emits": 15}
+        names = ["prep.S+r+ubloop", "step.loads", "res.reduce", "res.pred", "res.move", "res.apply(tail)", "prep.sort", None,
+                 "prep.blm+cert", "prep.reduce+eps", "prep.sets", "res.move->apply", "loads.bro+ctl", "loads.rec_reduce", "loads.keys", None, "sets.mark"]
+        counts = {"emits": 31, "spills": 30, "walks": 29, "walk_steps": 28, "walk_global": 27}
         print(json.dumps({"stamps_us_per_step": {k: st[i] / 100.0 / n for i, k in enumerate(names) if k},
                           "counts_per_step": {k: st[i] / n for k, i in counts.items()},
                           "stats": eng.stats()}))

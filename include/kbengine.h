@@ -174,7 +174,8 @@ int kb_engine_stats(kb_engine *e, kb_stats *out);
 int kb_engine_timings(kb_engine *e, double *ms, int64_t *launches, int n);
 
 /* Diagnostic: accumulated in-kernel phase stamps (100 MHz ticks) of k_step
- * phases [0..6]; non-zero only in a -DKB_STAMPS build. */
+ * phases and scan event counts (up to 32 slots, returns the slot count);
+ * non-zero only in a -DKB_STAMPS build. */
 int kb_engine_stamps(kb_engine *e, uint64_t *out, int n);
 
 /* Diagnostic: average device time (us) of the scan kernel over `iters`

@@ -423,7 +423,7 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
     int ncu = 256;
     hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, e->dev);
     if (ncu <= 0) ncu = 256;
-    const size_t rbytes = ((size_t)e->B * 8 + 15) & ~(size_t)15;
+    const size_t rbytes = (size_t)e->B * 16;          // (r, f(r)) pairs
     const size_t setbytes = (size_t)e->nsets * e->units * 16;
     const size_t dedup = (size_t)DEDUP_SCAN * (4 + 8 + 8);
     e->lds_sets = setbytes <= (size_t)LDS_SETS_MAX;
@@ -841,8 +841,8 @@ extern "C" int kb_engine_stamps(kb_engine* e, uint64_t* out, int n) {
     if (!e || !out) return KB_ERR_INVALID;
     DevCtl c;
     HIPCHK(hipMemcpy(&c, e->ctl, sizeof c, hipMemcpyDeviceToHost));
-    for (int k = 0; k < 16 && k < n; k++) out[k] = c.stamps[k];
-    return 16;
+    for (int k = 0; k < 32 && k < n; k++) out[k] = c.stamps[k];
+    return 32;
 }
 
 // Diagnostic: average device time of k_scan over `iters` back-to-back launches on

@@ -104,7 +104,7 @@ struct DevCtl {
     unsigned long long total_cand, total_cont, total_folds, total_exact_halts;
     // diagnostic phase stamps (builds with -DKB_STAMPS): accumulated
     // wall_clock64 ticks (100 MHz) per phase of k_step
-    unsigned long long stamps[16];
+    unsigned long long stamps[32];
 };
 
 #ifdef KB_STAMPS

@@ -53,12 +53,15 @@ __device__ __forceinline__ double term_x(double L, double avg) {
 
 // scoring (approximate; error covered by eps): f(r) and the O(1) move delta
 __device__ __forceinline__ double fsq(double r) {
-    double q = r * r;
-    return r > 0 ? q : 0.5 * q;
+    const double q = r * r;
+    return __builtin_amdgcn_ldexp(q, r > 0 ? 0 : -1);   // q or q/2, exactly (power-of-two scaling)
 }
 // U(after) - U(before) for moving weight w (delta = w/avg) from source s to target t
 __device__ __forceinline__ double dsrc(double rs, double delta) { return fsq(rs - delta) - fsq(rs); }
 __device__ __forceinline__ double dtgt(double rt, double delta) { return fsq(rt + delta) - fsq(rt); }
+// the same with f(r) from a (r, f(r)) table entry (bit-identical results)
+__device__ __forceinline__ double dsrc_f(double2 rf, double delta) { return fsq(rf.x - delta) - rf.y; }
+__device__ __forceinline__ double dtgt_f(double2 rf, double delta) { return fsq(rf.x + delta) - rf.y; }
 
 __device__ __forceinline__ bool setbit(const uint64_t* sb, int b) {
     return (sb[b >> 6] >> (b & 63)) & 1ull;
@@ -297,9 +300,9 @@ __device__ __forceinline__ void emit_global(DevCtl* ctl, Contender* cont, uint32
 
 __device__ __forceinline__ void emit(const ScanArgs& a, const Dedup& T, int kind, int s, int t, double w,
                                      unsigned long long iter) {
-    KB_COUNT(a.ctl, 15, 1);
+    KB_COUNT(a.ctl, 31, 1);
     if (dedup_insert(T, kind, s, t, w, iter) < 0) {   // table full or weight conflict: spill it raw
-        KB_COUNT(a.ctl, 7, 1);
+        KB_COUNT(a.ctl, 30, 1);
         Contender c;
         c.s = s; c.t = t; c.w = w; c.iter = iter; c.kind = kind; c.pad = 0;
         emit_global(a.ctl, a.cont, a.cont_cap, c);
@@ -310,7 +313,7 @@ __device__ __forceinline__ void emit(const ScanArgs& a, const Dedup& T, int kind
 // and emit the ones within 4*eps of the tile minimum g; stop once 8*eps is
 // exceeded (the approximate delta is monotone in the target load up to 2*eps).
 template <int RC>
-__device__ void walk_targets(const ScanArgs& a, const Dedup& T, const double* s_r, const int16_t* s_pos,
+__device__ void walk_targets(const ScanArgs& a, const Dedup& T, const double2* s_rf, const int16_t* s_pos,
                              const uint16_t* s_blm, const uint16_t* rec16, int kind, long long p, int slot, int src,
                              const uint32_t (&reps)[RC], int nrep, int set, double w, double ds, double g,
                              double eps, double inv_avg, int nblm) {
@@ -319,30 +322,30 @@ __device__ void walk_targets(const ScanArgs& a, const Dedup& T, const double* s_
     const double delta = w * inv_avg;
     const int nl = rec16[1];
     int last = -1;
-    KB_COUNT(a.ctl, 13, 1);
+    KB_COUNT(a.ctl, 29, 1);
     for (int i = 0; i < nl; i++) {                // the set's first KR eligible brokers
         const int b = rec16[2 + i];
-        KB_COUNT(a.ctl, 14, 1);
+        KB_COUNT(a.ctl, 28, 1);
         last = b;
         bool isrep = false;
 #pragma unroll
         for (int q = 0; q < RC; q++) isrep |= (q < nrep) && ((int)reps[q] == b);
         if (isrep) continue;
-        const double d = ds + dtgt(s_r[b], delta);
+        const double d = ds + dtgt_f(s_rf[b], delta);
         if (d <= g + 4.0 * eps) emit(a, T, kind, src, b, w, ib | (unsigned long long)s_pos[b]);
         if (d > g + 8.0 * eps) return;
     }
     if (nl < KR || last < 0) return;              // the set is exhausted
     const uint64_t* sb = a.setbits + (size_t)set * a.W64;
     for (int k = s_pos[last] + 1; k < nblm; k++) {   // rare: more than KR near-tied targets
-        KB_COUNT(a.ctl, 0, 1);
+        KB_COUNT(a.ctl, 27, 1);
         const int b = s_blm[k];
         if (!setbit(sb, b)) continue;
         bool isrep = false;
 #pragma unroll
         for (int q = 0; q < RC; q++) isrep |= (q < nrep) && ((int)reps[q] == b);
         if (isrep) continue;
-        const double d = ds + dtgt(s_r[b], delta);
+        const double d = ds + dtgt_f(s_rf[b], delta);
         if (d <= g + 4.0 * eps) emit(a, T, kind, src, b, w, ib | (unsigned long long)k);
         if (d > g + 8.0 * eps) return;
     }
@@ -360,16 +363,21 @@ __device__ __forceinline__ int first_target(const ScanArgs& a, const uint4* s_se
 #pragma unroll
     for (int u = 0; u < U; u++) R[u] = LSETS ? s_set[set * U + u] : a.setrec[(size_t)set * U + u];
     *nelig = (int)rec_u16(R, 0);
-    int tb = -1;
+    // slots past nrep compare against an id no record holds (ids < MAXB, NONE16 = padding);
+    // padding is never a replica, so it is picked only when no valid target precedes it
+    uint32_t rq[RC];
+#pragma unroll
+    for (int k = 0; k < RC; k++) rq[k] = k < nrep ? reps[k] : 0xFFFEu;
+    uint32_t tb = NONE16;
 #pragma unroll
     for (int i = KT - 1; i >= 0; i--) {
-        const int b = (int)rec_u16(R, 2 + i);
+        const uint32_t b = rec_u16(R, 2 + i);
         bool isrep = false;
 #pragma unroll
-        for (int k = 0; k < RC; k++) isrep |= (k < nrep) && ((int)reps[k] == b);
-        if (b != (int)NONE16 && !isrep) tb = b;
+        for (int k = 0; k < RC; k++) isrep |= rq[k] == b;
+        tb = isrep ? tb : b;
     }
-    return tb;
+    return tb == NONE16 ? -1 : (int)tb;
 }
 
 // order-preserving encoding of a double into u64 (LDS atomicMin of a minimum)
@@ -393,8 +401,8 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     KB_STAMP_BEGIN();
 
-    double* s_r = (double*)smem;
-    const size_t rbytes = ((size_t)a.B * 8 + 15) & ~(size_t)15;
+    double2* s_rf = (double2*)smem;                 // (r, f(r)) per broker
+    const size_t rbytes = (size_t)a.B * 16;
     int16_t* s_pos = (int16_t*)(smem + rbytes);
     const size_t pbytes = ((size_t)a.B * 2 + 15) & ~(size_t)15;
     uint16_t* s_blm = (uint16_t*)(smem + rbytes + pbytes);
@@ -414,7 +422,8 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
     PartRaw<RC> A, Bq;
     if (tile < a.ntiles) load_parts<RC>(a, a.shard_begin + (long long)tile * TILE + (long long)tid * PER_LANE, A);
     for (int i = tid; i < a.B; i += SCAN_THREADS) {
-        s_r[i] = a.r[i];
+        const double r = a.r[i];
+        s_rf[i] = make_double2(r, fsq(r));
         s_pos[i] = (int16_t)a.posm[i];
         s_blm[i] = (uint16_t)a.blm[i];
     }
@@ -426,7 +435,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
     const double ubL = ctl->ub[0], ubN = ctl->ub[1];
     const int heavy = ctl->heavy, nblm = ctl->nblm;
     __syncthreads();
-    if (!run) return;
+    if (!run || (a.dbg & 4)) return;
 
     double wgL = HUGE_VAL, wgN = HUGE_VAL;
     uint32_t fst[NF];
@@ -436,54 +445,90 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
 
     // score one tile held in P (partitions base, base + 1 of this lane)
     auto score = [&](const PartRaw<RC>& P, long long base) {
+        if (a.dbg & 2) {                          // diagnostic: stream only
+            uint32_t x = P.m.x ^ P.m.y ^ (uint32_t)__double2hiint(P.w.x) ^ (uint32_t)__double2hiint(P.w.y);
+#pragma unroll
+            for (int k = 0; k < RC; k++) x ^= P.r[k];
+            fst[F_DUP] = min(fst[F_DUP], x | 0x80000000u);
+            return;
+        }
         double lL = HUGE_VAL, lN = HUGE_VAL;
+        uint32_t cl = 0, cn = 0;                  // candidate counts of this tile (flushed to u64 below)
+        // the first-index predicates are rare once the plan is in shape: one cheap
+        // test per partition, the detailed path only for waves where one holds
+        bool spec = false;
 #pragma unroll
         for (int j = 0; j < PER_LANE; j++) {
-            const long long p = base + j;
-            const bool valid = p < a.shard_end;
             const uint32_t m = P.mt(j);
-            const int nrep = (int)meta_nrep(m), want = (int)meta_want(m);
-            const bool elig = valid && meta_elig(m);
-            const uint32_t pi = valid ? (uint32_t)p : NONE32;
+            uint32_t x = ((m ^ (m >> 5)) & 31u) | (m & 0x800u);      // want != nrep, Disallowed
+            bool sp = x != 0 || (m & 31u) == 0;                         // ..., empty
+            if (a.rebalance) sp |= P.rp(0, j) == (uint32_t)heavy;
+            if (a.sem_go) {
+                const int nrep = (int)meta_nrep(m);
+#pragma unroll
+                for (int q = 0; q < RC; q++)
+#pragma unroll
+                    for (int y = q + 1; y < RC; y++) sp |= (y < nrep) && P.rp(q, j) == P.rp(y, j);
+            }
+            spec |= sp && base + j < a.shard_end;
+        }
+        if (__ballot(spec)) {
+#pragma unroll
+            for (int j = 0; j < PER_LANE; j++) {
+                const long long p = base + j;
+                const bool valid = p < a.shard_end;
+                const uint32_t m = P.mt(j);
+                const int nrep = (int)meta_nrep(m), want = (int)meta_want(m);
+                const bool elig = valid && meta_elig(m);
+                const uint32_t pi = valid ? (uint32_t)p : NONE32;
+                if (a.sem_go) {
+                    bool dup = false;
+#pragma unroll
+                    for (int x = 0; x < RC; x++)
+#pragma unroll
+                        for (int y = x + 1; y < RC; y++) dup |= (y < nrep) && P.rp(x, j) == P.rp(y, j);
+                    if (dup) fst[F_DUP] = min(fst[F_DUP], pi);
+                }
+                if (want < nrep) fst[F_REMOVE] = min(fst[F_REMOVE], pi);
+                if (want > nrep) fst[F_ADD] = min(fst[F_ADD], pi);
+                if (nrep == 0) {
+                    fst[F_EMPTY] = min(fst[F_EMPTY], pi);
+                    if (elig) fst[F_EMPTY_ELIG] = min(fst[F_EMPTY_ELIG], pi);
+                }
+                if (meta_dis(m)) fst[F_DIS] = min(fst[F_DIS], pi);
+                if (a.rebalance && elig && nrep > 0 && (int)P.rp(0, j) == heavy) fst[F_LEAD] = min(fst[F_LEAD], pi);
+            }
+        }
+        // branch-free: every lane scores both partitions; invalid ones are masked
+        const uint32_t bmax = (uint32_t)(a.B - 1);
+#pragma unroll
+        for (int j = 0; j < PER_LANE; j++) {
+            const uint32_t m = P.mt(j);
+            const int nrep = (int)meta_nrep(m);
             uint32_t reps[RC];
 #pragma unroll
             for (int k = 0; k < RC; k++) reps[k] = P.rp(k, j);
-            if (a.sem_go) {
-                bool dup = false;
-#pragma unroll
-                for (int x = 0; x < RC; x++)
-#pragma unroll
-                    for (int y = x + 1; y < RC; y++) dup |= (y < nrep) && reps[x] == reps[y];
-                if (dup) fst[F_DUP] = min(fst[F_DUP], pi);
-            }
-            if (want < nrep) fst[F_REMOVE] = min(fst[F_REMOVE], pi);
-            if (want > nrep) fst[F_ADD] = min(fst[F_ADD], pi);
-            if (nrep == 0) {
-                fst[F_EMPTY] = min(fst[F_EMPTY], pi);
-                if (elig) fst[F_EMPTY_ELIG] = min(fst[F_EMPTY_ELIG], pi);
-            }
-            if (meta_dis(m)) fst[F_DIS] = min(fst[F_DIS], pi);
-            if (a.rebalance && elig && nrep > 0 && (int)reps[0] == heavy) fst[F_LEAD] = min(fst[F_LEAD], pi);
-            if (!elig || nrep == 0) continue;
             int nelig;
-            const int tb = first_target<RC, LSETS>(a, s_set, m, reps, nrep, &nelig);
-            if (tb < 0) continue;
+            const int tb0 = first_target<RC, LSETS>(a, s_set, m, reps, nrep, &nelig);
+            const bool ok = base + j < a.shard_end && meta_elig(m) && nrep > 0 && tb0 >= 0;
             const double delta = P.wt(j) * inv_avg;
-            const double dt = dtgt(s_r[tb], delta);
-            const unsigned long long ne = (unsigned long long)(nelig - (int)meta_nin(m));
+            const double dt = dtgt_f(s_rf[tb0 >= 0 ? tb0 : 0], delta);
+            const uint32_t ne = ok ? (uint32_t)(nelig - (int)meta_nin(m)) : 0u;
+            const uint32_t r0 = min(reps[0], bmax);   // table index even where the slot is unused
             if (a.allow_leader) {
-                const double d = dsrc(s_r[reps[0]], delta) + dt;
-                lL = d < lL ? d : lL;
-                cL += ne;
+                const double d = dsrc_f(s_rf[r0], delta) + dt;
+                lL = ok && d < lL ? d : lL;
+                cl += ne;
             }
 #pragma unroll
-            for (int k = 1; k < RC; k++)
-                if (k < nrep) {
-                    const double d = dsrc(s_r[reps[k]], delta) + dt;
-                    lN = d < lN ? d : lN;
-                }
-            cN += ne * (unsigned long long)(nrep - 1);
+            for (int k = 1; k < RC; k++) {
+                const double d = dsrc_f(s_rf[k < nrep ? reps[k] : r0], delta) + dt;
+                lN = ok && k < nrep && d < lN ? d : lN;
+            }
+            cn += ne * (uint32_t)(nrep - 1);
         }
+        cL += cl;
+        cN += cn;
         // wave minima; the census runs only where a wave minimum can be within 8*eps
         // of the step's global minimum, which is at most ub (k_step's upper bound)
         // (g <= ub + 2*eps: the first-target score is monotone in the target up to 2*eps)
@@ -505,12 +550,12 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
                 const int tb = first_target<RC, LSETS>(a, s_set, m, reps, nrep, &nelig);
                 if (tb < 0) continue;
                 const double delta = P.wt(j) * inv_avg;
-                const double dt = dtgt(s_r[tb], delta);
-                if (hasL && a.allow_leader && dsrc(s_r[reps[0]], delta) + dt <= tL + 8.0 * eps)
+                const double dt = dtgt_f(s_rf[tb], delta);
+                if (hasL && a.allow_leader && dsrc_f(s_rf[reps[0]], delta) + dt <= tL + 8.0 * eps)
                     todo |= 1u << (j * 16);
 #pragma unroll
                 for (int k = 1; k < RC; k++)
-                    if (hasN && k < nrep && dsrc(s_r[reps[k]], delta) + dt <= tN + 8.0 * eps)
+                    if (hasN && k < nrep && dsrc_f(s_rf[reps[k]], delta) + dt <= tN + 8.0 * eps)
                         todo |= 1u << (j * 16 + k);
             }
             // one walk call site (a compact, rarely executed code path)
@@ -529,8 +574,8 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
                 const int nrep = (int)meta_nrep(m), set = (int)meta_set(m);
                 const uint16_t* rec16 = LSETS ? (const uint16_t*)(s_set + (size_t)set * U)
                                               : (const uint16_t*)(a.setrec + (size_t)set * U);
-                const double ds = dsrc(s_r[src], w * inv_avg);
-                walk_targets<RC>(a, T, s_r, s_pos, s_blm, rec16, k ? 1 : 0, base + j, k, (int)src, reps, nrep, set, w,
+                const double ds = dsrc_f(s_rf[src], w * inv_avg);
+                walk_targets<RC>(a, T, s_rf, s_pos, s_blm, rec16, k ? 1 : 0, base + j, k, (int)src, reps, nrep, set, w,
                                  ds, k ? tN : tL, eps, inv_avg, nblm);
             }
         }
@@ -576,7 +621,8 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
         if (s_key[h] == NONE32 || s_wb[h] == NONE64) continue;
         const Contender c = dedup_entry(T, h);
         const double g = c.kind == 0 ? wgL : wgN;
-        if (!(cont_delta(s_r, c, inv_avg) <= g + 4.0 * eps)) continue;
+        const double dl = c.w * inv_avg;
+        if (!(dsrc_f(s_rf[c.s], dl) + dtgt_f(s_rf[c.t], dl) <= g + 4.0 * eps)) continue;
         const uint32_t k = atomicAdd(&s_nk, 1u);
         if (k < (uint32_t)TILE_KEYS) keys[k] = c;
         else emit_global(ctl, a.cont, a.cont_cap, c);
@@ -714,6 +760,7 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
     if (tid == 0) { s_nT = 0; s_done = 0; s_exact_need = 0; s_moved = -1; s_lkind = 0; }
     if (halted != H_RUN) return;
     __syncthreads();
+    KB_STAMP(ctl, 12);
     // ---- the scan records (or the gathered rank summaries): one per thread, reduced
     // per wave with DPP and across the waves by wave 0; then every thread collects
     // its record's near-tie keys of both kinds within 4*eps of the minima (distinct
@@ -767,6 +814,7 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
             }
         }
         __syncthreads();
+        KB_STAMP(ctl, 13);
         const double g0 = s_g[0], g1 = s_g[1];
         for (int i = tid; i < a.nrec; i += STEP_THREADS) {
             const RecHdr* h = (const RecHdr*)(a.recs + (size_t)i * a.rec_stride);
@@ -784,6 +832,7 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
         }
     }
     __syncthreads();
+    KB_STAMP(ctl, 14);
     if (do_res && a.use_spill && C.ncont > 0) {
         // raw spills of the scan (rare): every thread
         const uint32_t n = min(C.ncont, a.cont_cap);
@@ -1382,11 +1431,18 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
             const int i = base + q;
             if (i < B) {
                 const int b = s_ord[i];
-                if (flag[q]) { a.blm[pos] = b; a.posm[b] = pos; pos++; }
-                else a.posm[b] = -1;
+                if (flag[q]) {
+                    // the first / last bl_move broker: getBL's lightest / heaviest
+                    if (pos == 0) C.light = b;
+                    if (pos == total - 1) C.heavy = b;
+                    a.blm[pos] = b; a.posm[b] = pos; pos++;
+                } else a.posm[b] = -1;
             }
         }
-        if (tid == 0) s_nblm = total;
+        if (tid == 0) {
+            s_nblm = total;
+            if (total == 0) { C.light = -1; C.heavy = -1; }
+        }
     }
     __syncthreads();
     const int nblm = s_nblm;
@@ -1442,6 +1498,7 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
             }
         }
     }
+    KB_STAMP(ctl, 0);
     ub0 = wave_min(ub0); ub1 = wave_min(ub1);
     __shared__ double s_ubw[2][NW];
     __syncthreads();
@@ -1471,20 +1528,6 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
         C.ncont = 0;
         C.cont_overflow = 0;
     }
-    if (wid == 0) {
-        // first / last bl_move broker in universe order (scan the order from both ends)
-        int lo = 0x7FFFFFFF, hi = -1;
-        for (int i = lane; i < B; i += 64) {
-            const int b = s_ord[i];
-            if (s_fl[b] & (BF_PRESENT | BF_INCFG)) { lo = i < lo ? i : lo; hi = i > hi ? i : hi; }
-        }
-        lo = wave_min(lo);
-        hi = wave_max(hi);
-        if (lane == 0) {
-            C.light = lo < 0x7FFFFFFF ? s_ord[lo] : -1;
-            C.heavy = hi >= 0 ? s_ord[hi] : -1;
-        }
-    }
     KB_STAMP(ctl, 9);
     // ---- set records: full, or the sets containing a touched broker
     for (int w = tid; w < (a.nsets + 31) / 32; w += STEP_THREADS) s_smark[w] = full ? 0xFFFFFFFFu : 0u;
@@ -1499,6 +1542,7 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
         }
     }
     __syncthreads();
+    KB_STAMP(ctl, 16);
     {
         __shared__ unsigned long long s_wsb[NW][64];
         const unsigned long long lt = (1ull << lane) - 1ull;

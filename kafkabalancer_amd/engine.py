@@ -306,8 +306,8 @@ class Engine:
 
     def stamps(self):
         """Diagnostic build only: accumulated phase ticks (100 MHz) of the k_step phases."""
-        out = np.zeros(16, np.int64)
-        lib().kb_engine_stamps(self.h, out.ctypes.data_as(P64), 16)
+        out = np.zeros(32, np.int64)
+        lib().kb_engine_stamps(self.h, out.ctypes.data_as(P64), 32)
         return out.tolist()
 
     def bench_scan(self, iters=100):

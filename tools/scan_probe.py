@@ -19,7 +19,5 @@ st1 = eng.stamps()
 out = {"dbg": os.environ.get("KB_DEBUG_SCAN", "0"), "nscan": eng.stats()["scan_workgroups"], "scan_us": us}
 if "stamps" in os.environ.get("KB_ENGINE_LIB", ""):
     d = [(b - a) / (iters + 1) for a, b in zip(st0, st1)]
-    out["per_scan"] = {"beyond_iters": d[0], "spills": d[7], "walks": d[13], "walk_iters": d[14], "emits": d[15],
-                       "scan0_us": {k: d[i] / 100.0 for k, i in
-                                    [("prologue", 8), ("score", 9), ("reduce", 10), ("census", 11), ("final", 12)]}}
+    out["per_scan"] = {"beyond_iters": d[27], "spills": d[30], "walks": d[29], "walk_iters": d[28], "emits": d[31]}
 print(json.dumps(out))
