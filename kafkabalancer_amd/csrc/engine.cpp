@@ -512,14 +512,13 @@ static void fill_scan_args(kb_engine* e, ScanArgs& s) {
     s.B = (int)e->B; s.nsets = (int)e->nsets; s.W64 = e->W64; s.units = e->units;
     s.setbits = e->setbits; s.setrec = e->setrec; s.r = e->r; s.blm = e->blm; s.posm = e->posm;
     s.allow_leader = e->allow_leader; s.rebalance = e->rebalance; s.sem_go = e->sem == KB_SEM_GO;
-    s.recs = e->recs; s.cont = e->cont; s.cont_cap = e->cont_cap;
+    s.R = scan_recs(e->recs, (int)e->nscan); s.cont = e->cont; s.cont_cap = e->cont_cap;
     s.listwg = e->integral ? 0 : 1;
     s.dbg = e->dbg_scan;
     s.L = e->L;
 }
 
-static void fill_step_args(kb_engine* e, StepArgs& a, const unsigned char* recs, int nrec, int stride,
-                           int keys, int use_spill) {
+static void fill_step_args(kb_engine* e, StepArgs& a, const Recs& R, int use_spill) {
     a.ctl = e->ctl; a.w = e->w; a.rep = e->rep; a.meta = e->meta; a.nc = e->nc; a.Ppad = e->Ppad;
     a.RC = e->rc_dev; a.KR = e->KR; a.K = e->K; a.units = e->units; a.W64 = e->W64; a.B = (int)e->B;
     a.nsets = (int)e->nsets; a.NP2 = e->NP2;
@@ -527,7 +526,7 @@ static void fill_step_args(kb_engine* e, StepArgs& a, const unsigned char* recs,
     a.order = e->order; a.posu = e->posu; a.blm = e->blm; a.posm = e->posm; a.r = e->r;
     a.load = e->load; a.lerr = e->lerr; a.eb = e->eb; a.bfl = e->bfl; a.cnt = e->cnt;
     a.bset_off = e->bset_off; a.bset_ids = e->bset_ids;
-    a.recs = recs; a.nrec = nrec; a.rec_stride = stride; a.rec_keys = keys;
+    a.R = R;
     a.cont = e->cont; a.cont_cap = e->cont_cap; a.use_spill = use_spill;
     a.allow_leader = e->allow_leader; a.rebalance = e->rebalance; a.sem_go = e->sem == KB_SEM_GO;
     a.integral = e->integral ? 1 : 0; a.exact_unb = e->exact_unb;
@@ -576,7 +575,7 @@ static void enqueue_scan(kb_engine* e) {
 
 static void enqueue_step(kb_engine* e) {
     StepArgs a;
-    fill_step_args(e, a, e->recs, (int)e->nscan, WGREC_BYTES, TILE_KEYS, 1);
+    fill_step_args(e, a, scan_recs(e->recs, (int)e->nscan), 1);
     launch_step(a, e->st);
 }
 
@@ -914,8 +913,8 @@ extern "C" int kb_engine_step_begin(kb_engine* e, void* summary_dev) {
     if (!e->h_ctl->prepped) enqueue_step(e);       // prep only (nothing to resolve yet)
     enqueue_scan(e);
     SumArgs s;
-    s.ctl = e->ctl; s.recs = e->recs; s.nrec = (int)e->nscan; s.cont = e->cont; s.cont_cap = e->cont_cap;
-    s.r = e->r; s.out = (unsigned char*)summary_dev;
+    s.ctl = e->ctl; s.R = scan_recs(e->recs, (int)e->nscan); s.cont = e->cont; s.cont_cap = e->cont_cap;
+    s.r = e->r; s.out = summary_recs((unsigned char*)summary_dev, 1);
     launch_summary(s, e->st);
     HIPCHK(hipGetLastError());
     return KB_OK;
@@ -925,7 +924,7 @@ extern "C" int kb_engine_step_finish(kb_engine* e, const void* gathered_dev, int
     if (!e || !gathered_dev || n_ranks < 1 || !out) return KB_ERR_INVALID;
     if (e->pending) return pending_result(e, out);
     StepArgs a;
-    fill_step_args(e, a, (const unsigned char*)gathered_dev, n_ranks, SUMMARY_BYTES, SUMMARY_KEYS, 0);
+    fill_step_args(e, a, summary_recs((unsigned char*)gathered_dev, n_ranks), 0);
     launch_step(a, e->st);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(e->h_ctl, e->ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, e->st));

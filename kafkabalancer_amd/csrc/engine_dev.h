@@ -66,18 +66,53 @@ struct Contender {                  // a near-tie candidate move (32 B)
     int32_t pad;
 };
 
-// header of a scan-workgroup record and of a rank summary (multi-GPU); the
-// near-tie keys follow it (TILE_KEYS resp. SUMMARY_KEYS slots)
-struct RecHdr {
+// header of a scan-workgroup record and of a rank summary (multi-GPU)
+struct RecHdr {                     // 112 B
     double dmin[2];                 // min score delta {leader, non-leader}
     unsigned long long cand[2];     // reference candidate counts
-    uint32_t first[NF];             // first-index predicates
-    uint32_t nkeys;                 // keys stored after the header
+    uint32_t nkeys;                 // near-tie keys stored for this record
     uint32_t flags;                 // bit0: keys spilled / overflowed (see k_step)
-    uint32_t pad[2];
+    uint32_t fmask;                 // bit q: first[q] != NONE32 (first-index predicates)
+    uint32_t ran;                   // summaries: the rank's scan ran
+    Contender best[2];              // the record's minimum-score key per kind (s < 0: none);
+                                    // k_step re-scores them for the next step's upper bound
 };
-constexpr int WGREC_BYTES = (int)sizeof(RecHdr) + TILE_KEYS * (int)sizeof(Contender);
-constexpr int SUMMARY_BYTES = (int)sizeof(RecHdr) + SUMMARY_KEYS * (int)sizeof(Contender);
+static_assert(sizeof(RecHdr) == 112, "record header layout");
+
+// a set of records: headers, first-index predicate words and near-tie keys, each
+// with its own byte stride (scan records: three dense arrays; rank summaries: one
+// self-contained block per rank)
+struct Recs {
+    unsigned char* hdr;
+    unsigned char* first;           // uint32_t[NF] per record
+    unsigned char* keys;            // Contender[cap] per record
+    int hdr_stride, first_stride, key_stride;
+    int n, cap;
+    __host__ __device__ RecHdr* h(int i) const { return (RecHdr*)(hdr + (size_t)i * hdr_stride); }
+    __host__ __device__ uint32_t* f(int i) const { return (uint32_t*)(first + (size_t)i * first_stride); }
+    __host__ __device__ Contender* k(int i) const { return (Contender*)(keys + (size_t)i * key_stride); }
+};
+constexpr int FIRST_BYTES = NF * 4;
+constexpr int WGREC_BYTES = (int)sizeof(RecHdr) + FIRST_BYTES + TILE_KEYS * (int)sizeof(Contender);
+constexpr int SUMMARY_BYTES = (int)sizeof(RecHdr) + FIRST_BYTES + SUMMARY_KEYS * (int)sizeof(Contender);
+inline Recs scan_recs(unsigned char* base, int nscan) {
+    Recs r;
+    r.hdr = base;
+    r.first = base + (size_t)nscan * sizeof(RecHdr);
+    r.keys = r.first + (size_t)nscan * FIRST_BYTES;
+    r.hdr_stride = (int)sizeof(RecHdr); r.first_stride = FIRST_BYTES; r.key_stride = TILE_KEYS * (int)sizeof(Contender);
+    r.n = nscan; r.cap = TILE_KEYS;
+    return r;
+}
+inline Recs summary_recs(unsigned char* base, int n) {
+    Recs r;
+    r.hdr = base;
+    r.first = base + sizeof(RecHdr);
+    r.keys = r.first + FIRST_BYTES;
+    r.hdr_stride = r.first_stride = r.key_stride = SUMMARY_BYTES;
+    r.n = n; r.cap = SUMMARY_KEYS;
+    return r;
+}
 
 struct ChangeDev {
     int32_t status, step, kind, slot;
@@ -108,20 +143,32 @@ struct DevCtl {
 };
 
 #ifdef KB_STAMPS
-#define KB_STAMP_BEGIN() unsigned long long _kb_t0 = wall_clock64()
+// phase ticks accumulate in LDS (a global read-modify-write per stamp would add
+// a memory round trip to every phase); KB_STAMP_FLUSH adds them to ctl->stamps
+#define KB_STAMP_BEGIN()                                                        \
+    __shared__ unsigned long long _kb_st[32];                                   \
+    if (threadIdx.x < 32) _kb_st[threadIdx.x] = 0;                              \
+    unsigned long long _kb_t0 = wall_clock64()
 #define KB_STAMP(ctl, i)                                                        \
     do {                                                                        \
         __syncthreads();                                                        \
         if (threadIdx.x == 0) {                                                 \
             unsigned long long _t = wall_clock64();                             \
-            (ctl)->stamps[i] += _t - _kb_t0;                                    \
+            _kb_st[i] += _t - _kb_t0;                                           \
             _kb_t0 = _t;                                                        \
         }                                                                       \
+    } while (0)
+#define KB_STAMP_FLUSH(ctl)                                                     \
+    do {                                                                        \
+        __syncthreads();                                                        \
+        if (threadIdx.x < 32 && _kb_st[threadIdx.x])                            \
+            atomicAdd(&(ctl)->stamps[threadIdx.x], _kb_st[threadIdx.x]);        \
     } while (0)
 #define KB_COUNT(ctl, i, v) atomicAdd(&(ctl)->stamps[i], (unsigned long long)(v))
 #else
 #define KB_STAMP_BEGIN() (void)0
 #define KB_STAMP(ctl, i) (void)0
+#define KB_STAMP_FLUSH(ctl) (void)0
 #define KB_COUNT(ctl, i, v) (void)0
 #endif
 

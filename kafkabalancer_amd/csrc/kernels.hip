@@ -87,16 +87,17 @@ __device__ __forceinline__ uint32_t rec_u16(const uint4* v, int idx) {
 __device__ __forceinline__ double gamma_n(int n) { return 1.01 * (double)(n > 1 ? n : 1) * (DBL_EPSILON / 2); }
 
 // Sequential fold of n doubles held in LDS, in order (the reference's fold).
-// Loads are batched 16 at a time so the dependent add chain, not LDS latency,
+// Loads are batched FOLD_BATCH at a time so the dependent add chain, not LDS latency,
 // sets the pace.
+constexpr int FOLD_BATCH = 8;
 __device__ __forceinline__ double fold_lds(const double* x, int n, double acc = 0.0) {
     int k = 0;
-    for (; k + 16 <= n; k += 16) {
-        double v[16];
+    for (; k + FOLD_BATCH <= n; k += FOLD_BATCH) {
+        double v[FOLD_BATCH];
 #pragma unroll
-        for (int i = 0; i < 16; i++) v[i] = x[k + i];
+        for (int i = 0; i < FOLD_BATCH; i++) v[i] = x[k + i];
 #pragma unroll
-        for (int i = 0; i < 16; i++) acc += v[i];
+        for (int i = 0; i < FOLD_BATCH; i++) acc += v[i];
     }
     for (; k < n; k++) acc += x[k];
     return acc;
@@ -107,26 +108,26 @@ __device__ __forceinline__ double fold_lds(const double* x, int n, double acc = 
 __device__ double exact_unbalance_lds(const double* Lm, int n, int ps, int pt, double Ls, double Lt) {
     double S = 0.0;
     int k = 0;
-    for (; k + 16 <= n; k += 16) {
-        double v[16];
+    for (; k + FOLD_BATCH <= n; k += FOLD_BATCH) {
+        double v[FOLD_BATCH];
 #pragma unroll
-        for (int i = 0; i < 16; i++) v[i] = Lm[k + i];
+        for (int i = 0; i < FOLD_BATCH; i++) v[i] = Lm[k + i];
 #pragma unroll
-        for (int i = 0; i < 16; i++) S += (k + i == ps) ? Ls : ((k + i == pt) ? Lt : v[i]);
+        for (int i = 0; i < FOLD_BATCH; i++) S += (k + i == ps) ? Ls : ((k + i == pt) ? Lt : v[i]);
     }
     for (; k < n; k++) S += (k == ps) ? Ls : ((k == pt) ? Lt : Lm[k]);
     const double avg = S / (double)n;
     double U = 0.0;
     k = 0;
-    for (; k + 16 <= n; k += 16) {
-        double t[16];
+    for (; k + FOLD_BATCH <= n; k += FOLD_BATCH) {
+        double t[FOLD_BATCH];
 #pragma unroll
-        for (int i = 0; i < 16; i++) {
+        for (int i = 0; i < FOLD_BATCH; i++) {
             const double L = (k + i == ps) ? Ls : ((k + i == pt) ? Lt : Lm[k + i]);
             t[i] = term_x(L, avg);
         }
 #pragma unroll
-        for (int i = 0; i < 16; i++) U += t[i];
+        for (int i = 0; i < FOLD_BATCH; i++) U += t[i];
     }
     for (; k < n; k++) U += term_x((k == ps) ? Ls : ((k == pt) ? Lt : Lm[k]), avg);
     return U;
@@ -399,7 +400,6 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
     constexpr int U = sr_units(RC);
     constexpr int NW = SCAN_THREADS / 64;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    KB_STAMP_BEGIN();
 
     double2* s_rf = (double2*)smem;                 // (r, f(r)) per broker
     const size_t rbytes = (size_t)a.B * 16;
@@ -415,6 +415,8 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
     __shared__ uint32_t s_f[NF][NW];
     __shared__ unsigned long long s_c[2][NW];
     __shared__ uint32_t s_nk;
+    __shared__ unsigned long long s_benc[2];
+    __shared__ uint32_t s_bslot[2];
 
     // every load that does not depend on the control block goes out first: the
     // first tile's stream, then the lookup tables (one memory round trip)
@@ -430,6 +432,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
     if (LSETS) for (int i = tid; i < a.nsets * U; i += SCAN_THREADS) s_set[i] = a.setrec[i];
     for (int i = tid; i < DEDUP_SCAN; i += SCAN_THREADS) { s_key[i] = NONE32; s_wb[i] = NONE64; s_it[i] = NONE64; }
     if (tid == 0) s_nk = 0;
+    if (tid < 2) { s_benc[tid] = NONE64; s_bslot[tid] = NONE32; }
     const bool run = ctl->halted == H_RUN && ctl->prepped && ctl->steps < ctl->budget;
     const double inv_avg = ctl->inv_avg, eps = ctl->eps;
     const double ubL = ctl->ub[0], ubN = ctl->ub[1];
@@ -615,34 +618,56 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
         wgL = s_wm[0][x] < wgL ? s_wm[0][x] : wgL;
         wgN = s_wm[1][x] < wgN ? s_wm[1][x] : wgN;
     }
-    RecHdr* hdr = (RecHdr*)(a.recs + (size_t)blockIdx.x * WGREC_BYTES);
-    Contender* keys = (Contender*)(hdr + 1);
-    for (int h = tid; h < DEDUP_SCAN; h += SCAN_THREADS) {
-        if (s_key[h] == NONE32 || s_wb[h] == NONE64) continue;
-        const Contender c = dedup_entry(T, h);
+    RecHdr* hdr = a.R.h(blockIdx.x);
+    Contender* keys = a.R.k(blockIdx.x);
+    // the near-tie keys within 4*eps of the workgroup minima; the minimum-score key
+    // per kind (smallest table slot among equal scores) goes into the header
+    static_assert(DEDUP_SCAN <= SCAN_THREADS, "one table slot per thread");
+    int myh = -1, mykind = 0;
+    unsigned long long myenc = NONE64;
+    if (tid < DEDUP_SCAN && s_key[tid] != NONE32 && s_wb[tid] != NONE64) {
+        const Contender c = dedup_entry(T, tid);
         const double g = c.kind == 0 ? wgL : wgN;
         const double dl = c.w * inv_avg;
-        if (!(dsrc_f(s_rf[c.s], dl) + dtgt_f(s_rf[c.t], dl) <= g + 4.0 * eps)) continue;
-        const uint32_t k = atomicAdd(&s_nk, 1u);
-        if (k < (uint32_t)TILE_KEYS) keys[k] = c;
-        else emit_global(ctl, a.cont, a.cont_cap, c);
+        const double d = dsrc_f(s_rf[c.s], dl) + dtgt_f(s_rf[c.t], dl);
+        if (d <= g + 4.0 * eps) {
+            myh = tid; mykind = c.kind; myenc = enc(d);
+            atomicMin(&s_benc[c.kind], myenc);
+            const uint32_t k = atomicAdd(&s_nk, 1u);
+            if (k < (uint32_t)TILE_KEYS) keys[k] = c;
+            else emit_global(ctl, a.cont, a.cont_cap, c);
+        }
     }
+    __syncthreads();
+    if (myh >= 0 && myenc == s_benc[mykind]) atomicMin(&s_bslot[mykind], (uint32_t)myh);
     __syncthreads();
     if (tid == 0) {
         RecHdr r;
+        uint32_t fm = 0;
         for (int x = 1; x < NW; x++) {
             cL += s_c[0][x]; cN += s_c[1][x];
 #pragma unroll
             for (int f = 0; f < NF; f++) fst[f] = min(fst[f], s_f[f][x]);
         }
+#pragma unroll
+        for (int f = 0; f < NF; f++) fm |= fst[f] != NONE32 ? 1u << f : 0u;
         r.dmin[0] = wgL; r.dmin[1] = wgN;
         r.cand[0] = cL; r.cand[1] = cN;
-#pragma unroll
-        for (int f = 0; f < NF; f++) r.first[f] = fst[f];
         r.nkeys = s_nk < (uint32_t)TILE_KEYS ? s_nk : (uint32_t)TILE_KEYS;
         r.flags = 0;
-        r.pad[0] = r.pad[1] = 0;
+        r.fmask = fm;
+        r.ran = 1;
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            if (s_bslot[k] != NONE32) r.best[k] = dedup_entry(T, (int)s_bslot[k]);
+            else { r.best[k].s = r.best[k].t = -1; r.best[k].w = 0.0; r.best[k].iter = NONE64; r.best[k].kind = k; r.best[k].pad = 0; }
+        }
         *hdr = r;
+        if (fm) {
+            uint32_t* fo = a.R.f(blockIdx.x);
+#pragma unroll
+            for (int f = 0; f < NF; f++) fo[f] = fst[f];
+        }
     }
 }
 
@@ -675,11 +700,11 @@ template <typename F>
 __device__ void for_each_contender(const StepArgs& a, const double* s_ld, int kind, double g, double eps,
                                    double inv_avg, F f) {
     const int nt = blockDim.x;
-    for (int i = threadIdx.x; i < a.nrec; i += nt) {
-        const RecHdr* h = (const RecHdr*)(a.recs + (size_t)i * a.rec_stride);
+    for (int i = threadIdx.x; i < a.R.n; i += nt) {
+        const RecHdr* h = a.R.h(i);
         if (!(h->dmin[kind] <= g + 8.0 * eps)) continue;
-        const Contender* keys = (const Contender*)(h + 1);
-        const int nk = (int)min(h->nkeys, (uint32_t)a.rec_keys);
+        const Contender* keys = a.R.k(i);
+        const int nk = (int)min(h->nkeys, (uint32_t)a.R.cap);
         for (int k = 0; k < nk; k++) {
             const Contender c = keys[k];
             if (c.kind != kind) continue;
@@ -705,8 +730,10 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     constexpr int NW = STEP_THREADS / 64;
     __shared__ DevCtl C;
+    KB_STAMP_BEGIN();
     if (tid < CTL_WORDS) ((uint32_t*)&C)[tid] = ((const uint32_t*)ctl)[tid];
     auto write_back = [&]() {
+        KB_STAMP_FLUSH(ctl);
         __syncthreads();
         if (tid < CTL_WORDS) ((uint32_t*)ctl)[tid] = ((const uint32_t*)&C)[tid];
     };
@@ -719,7 +746,7 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
     __shared__ double s_g[2];
     __shared__ unsigned long long s_cand[2];
     __shared__ uint32_t s_first[NF];
-    __shared__ uint32_t s_flags;
+    __shared__ uint32_t s_flags, s_fm;
     __shared__ double s_sux;
     __shared__ uint32_t s_key[DEDUP_STEP];
     __shared__ unsigned long long s_wb[DEDUP_STEP], s_it[DEDUP_STEP];
@@ -735,7 +762,6 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
     __shared__ int s_nd[2], s_li[2], s_kfail[2];
     Dedup T{s_key, s_wb, s_it, DEDUP_STEP, s_nd, s_li};
     const int B = a.B;
-    KB_STAMP_BEGIN();
 
     // ---- one memory round trip: the broker state, the scan records, the control block
     for (int b = tid; b < B; b += STEP_THREADS) {
@@ -768,60 +794,69 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
     if (do_res) {
         double d0 = HUGE_VAL, d1 = HUGE_VAL;
         unsigned long long c0 = 0, c1 = 0;
-        uint32_t f[NF];
-#pragma unroll
-        for (int q = 0; q < NF; q++) f[q] = NONE32;
-        uint32_t flg = 0;
-        for (int i = tid; i < a.nrec; i += STEP_THREADS) {
-            const RecHdr* h = (const RecHdr*)(a.recs + (size_t)i * a.rec_stride);
+        uint32_t flg = 0, fm = 0;
+        for (int i = tid; i < a.R.n; i += STEP_THREADS) {
+            const RecHdr* h = a.R.h(i);
             d0 = h->dmin[0] < d0 ? h->dmin[0] : d0;
             d1 = h->dmin[1] < d1 ? h->dmin[1] : d1;
             c0 += h->cand[0]; c1 += h->cand[1];
-#pragma unroll
-            for (int q = 0; q < NF; q++) f[q] = min(f[q], h->first[q]);
             flg |= h->flags;
+            fm |= h->fmask;
         }
         d0 = wave_min(d0); d1 = wave_min(d1); c0 = wave_sum(c0); c1 = wave_sum(c1);
-#pragma unroll
-        for (int q = 0; q < NF; q++) f[q] = wave_min(f[q]);
         flg = wave_red_or(flg);
+        fm = wave_red_or(fm);
         __shared__ double s_pd[2][NW];
         __shared__ unsigned long long s_pc[2][NW];
-        __shared__ uint32_t s_pf[NF + 1][NW];
+        __shared__ uint32_t s_pf[NF + 2][NW];
         if (lane == 0) {
             s_pd[0][wid] = d0; s_pd[1][wid] = d1; s_pc[0][wid] = c0; s_pc[1][wid] = c1;
-#pragma unroll
-            for (int q = 0; q < NF; q++) s_pf[q][wid] = f[q];
-            s_pf[NF][wid] = flg;
+            s_pf[NF][wid] = flg; s_pf[NF + 1][wid] = fm;
         }
         __syncthreads();
         if (wid == 0) {
             const bool in = lane < NW;
             d0 = in ? s_pd[0][lane] : HUGE_VAL; d1 = in ? s_pd[1][lane] : HUGE_VAL;
             c0 = in ? s_pc[0][lane] : 0ull; c1 = in ? s_pc[1][lane] : 0ull;
-#pragma unroll
-            for (int q = 0; q < NF; q++) f[q] = in ? s_pf[q][lane] : NONE32;
             flg = in ? s_pf[NF][lane] : 0u;
+            fm = in ? s_pf[NF + 1][lane] : 0u;
             d0 = wave_min(d0); d1 = wave_min(d1); c0 = wave_sum(c0); c1 = wave_sum(c1);
-#pragma unroll
-            for (int q = 0; q < NF; q++) f[q] = wave_min(f[q]);
             flg = wave_red_or(flg);
+            fm = wave_red_or(fm);
             if (lane == 0) {
                 s_g[0] = d0; s_g[1] = d1; s_cand[0] = c0; s_cand[1] = c1;
-#pragma unroll
-                for (int q = 0; q < NF; q++) s_first[q] = f[q];
                 s_flags = flg | (a.use_spill && C.cont_overflow ? 1u : 0u);
+                s_fm = fm;
             }
+            if (lane < NF) s_first[lane] = NONE32;
         }
         __syncthreads();
+        if (s_fm) {
+            // some record holds a first-index predicate (the plan is not in shape yet)
+            uint32_t f[NF];
+#pragma unroll
+            for (int q = 0; q < NF; q++) f[q] = NONE32;
+            for (int i = tid; i < a.R.n; i += STEP_THREADS) {
+                if (!a.R.h(i)->fmask) continue;
+                const uint32_t* fi = a.R.f(i);
+#pragma unroll
+                for (int q = 0; q < NF; q++) f[q] = min(f[q], fi[q]);
+            }
+#pragma unroll
+            for (int q = 0; q < NF; q++) {
+                f[q] = wave_min(f[q]);
+                if (lane == 0 && f[q] != NONE32) atomicMin(&s_first[q], f[q]);
+            }
+            __syncthreads();
+        }
         KB_STAMP(ctl, 13);
         const double g0 = s_g[0], g1 = s_g[1];
-        for (int i = tid; i < a.nrec; i += STEP_THREADS) {
-            const RecHdr* h = (const RecHdr*)(a.recs + (size_t)i * a.rec_stride);
+        for (int i = tid; i < a.R.n; i += STEP_THREADS) {
+            const RecHdr* h = a.R.h(i);
             const bool q0 = h->dmin[0] <= g0 + 8.0 * eps, q1 = h->dmin[1] <= g1 + 8.0 * eps;
             if (!q0 && !q1) continue;
-            const Contender* keys = (const Contender*)(h + 1);
-            const int nk = (int)min(h->nkeys, (uint32_t)a.rec_keys);
+            const Contender* keys = a.R.k(i);
+            const int nk = (int)min(h->nkeys, (uint32_t)a.R.cap);
             for (int k = 0; k < nk; k++) {
                 const Contender c = keys[k];
                 if (!(c.kind ? q1 : q0)) continue;
@@ -1350,6 +1385,8 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
         int nb[(MAXB + STEP_THREADS - 1) / STEP_THREADS], np[(MAXB + STEP_THREADS - 1) / STEP_THREADS];
 #pragma unroll
         for (int q = 0; q < (MAXB + STEP_THREADS - 1) / STEP_THREADS; q++) {
+            nb[q] = -1;
+            if (q * STEP_THREADS >= B) continue;         // uniform
             const int i = q * STEP_THREADS + tid;
             const bool in = i < B;
             const int b = in ? s_ord[i] : 0;
@@ -1452,6 +1489,12 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
         return;
     }
     KB_STAMP(ctl, 8);
+    // the records' best keys (re-scored below for the next step's upper bound; one
+    // record per thread): loaded first, their latency overlaps the sums
+    const bool bkeys = do_res && !full && tid < a.R.n;
+    Contender bk0, bk1;
+    bk0.s = bk1.s = -1;
+    if (bkeys) { bk0 = a.R.h(tid)->best[0]; bk1 = a.R.h(tid)->best[1]; }
     // approximate S (exact in integral mode: integers below 2^52), total load error E
     double sS = 0.0, sE = 0.0;
     for (int b = tid; b < B; b += STEP_THREADS)
@@ -1482,20 +1525,16 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
     // just resolved whose partition and brokers the applied move did not touch are
     // still candidates; re-scored on the new loads they bound the new minimum
     double ub0 = HUGE_VAL, ub1 = HUGE_VAL;
-    if (do_res && !full) {
+    if (bkeys) {
         const long long pm = s_moved;
-        for (int i = tid; i < a.nrec; i += STEP_THREADS) {
-            const RecHdr* h = (const RecHdr*)(a.recs + (size_t)i * a.rec_stride);
-            const Contender* keys = (const Contender*)(h + 1);
-            const int nk = (int)min(h->nkeys, (uint32_t)a.rec_keys);
-            for (int k = 0; k < nk; k++) {
-                const Contender c = keys[k];
-                if ((long long)(c.iter >> 21) == pm) continue;
-                if ((s_fl[c.s] | s_fl[c.t]) & BF_TOUCHED) continue;
-                const double d = cont_delta_ld(s_ld, c, iav);
-                if (c.kind == 0) ub0 = d < ub0 ? d : ub0;
-                else ub1 = d < ub1 ? d : ub1;
-            }
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            const Contender& c = k ? bk1 : bk0;
+            if (c.s < 0 || (long long)(c.iter >> 21) == pm) continue;
+            if ((s_fl[c.s] | s_fl[c.t]) & BF_TOUCHED) continue;
+            const double d = cont_delta_ld(s_ld, c, iav);
+            if (k == 0) ub0 = d < ub0 ? d : ub0;
+            else ub1 = d < ub1 ? d : ub1;
         }
     }
     KB_STAMP(ctl, 0);
@@ -1530,51 +1569,106 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
     }
     KB_STAMP(ctl, 9);
     // ---- set records: full, or the sets containing a touched broker
-    for (int w = tid; w < (a.nsets + 31) / 32; w += STEP_THREADS) s_smark[w] = full ? 0xFFFFFFFFu : 0u;
-    __syncthreads();
+    for (int w = tid; w < (a.nsets + 31) / 32; w += STEP_THREADS) {
+        const int rem = a.nsets - w * 32;                 // only bits of existing sets
+        s_smark[w] = full ? (rem >= 32 ? 0xFFFFFFFFu : (1u << rem) - 1u) : 0u;
+    }
     if (!full) {
-        for (int x = 0; x < nT; x++) {
-            const int t = s_T[x];
-            for (int j = a.bset_off[t] + tid; j < a.bset_off[t + 1]; j += STEP_THREADS) {
-                const int s = a.bset_ids[j];
-                atomicOr(&s_smark[s >> 5], 1u << (s & 31));
-            }
+        // two memory round trips: the touched brokers' set-list extents, then the lists
+        __shared__ int s_bo[TMAX + 1], s_bb[TMAX];
+        if (tid < nT) {
+            const int t = s_T[tid];
+            const int o0 = a.bset_off[t], o1 = a.bset_off[t + 1];
+            s_bb[tid] = o0;
+            s_bo[tid] = o1 - o0;
+        }
+        __syncthreads();
+        if (wid == 0) {
+            const int c = lane < nT ? s_bo[lane] : 0;
+            int incl = c;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) { const int y = __shfl_up(incl, o); if (lane >= o) incl += y; }
+            if (lane < nT) s_bo[lane] = incl - c;
+            if (lane == nT - 1) s_bo[nT] = incl;
+            if (nT == 0 && lane == 0) s_bo[0] = 0;
+        }
+        __syncthreads();
+        const int tot = s_bo[nT];
+        for (int q = tid; q < tot; q += STEP_THREADS) {
+            int x = 0;
+            while (x + 1 < nT && s_bo[x + 1] <= q) x++;
+            const int set = a.bset_ids[s_bb[x] + q - s_bo[x]];
+            atomicOr(&s_smark[set >> 5], 1u << (set & 31));
         }
     }
     __syncthreads();
     KB_STAMP(ctl, 16);
     {
-        __shared__ unsigned long long s_wsb[NW][64];
+        // marked sets in chunks: their allowed-set words staged in LDS (one round trip
+        // per chunk; the dedup table is free here), then one wave per set
+        unsigned long long* s_stage = s_wb;               // [CH * W64]
+        int* s_mlist = (int*)s_it;                         // [CH]
+        __shared__ int s_mn, s_cursor;
+        const int W64 = a.W64, KR = a.KR;
+        const int CH = DEDUP_STEP / W64;                   // >= 32 (W64 <= 64)
+        const int nwords = (a.nsets + 31) / 32;
         const unsigned long long lt = (1ull << lane) - 1ull;
-        const int KR = a.KR;
-        for (int set = wid; set < a.nsets; set += NW) {
-            if (!((s_smark[set >> 5] >> (set & 31)) & 1u)) continue;
-            const unsigned long long sbw = lane < a.W64 ? (unsigned long long)a.setbits[(size_t)set * a.W64 + lane] : 0ull;
-            s_wsb[wid][lane] = sbw;
-            auto inset = [&](int b) -> bool { return (s_wsb[wid][b >> 6] >> (b & 63)) & 1ull; };
-            uint16_t* rec16 = (uint16_t*)(a.setrec + (size_t)set * a.units);
-            // the first KR brokers of set ∩ bl_move in bl order (move targets, steps.go:192-201)
-            {
-                const int cap = KR;
+        if (tid == 0) s_cursor = 0;
+        __syncthreads();
+        while (s_cursor < nwords) {
+            if (wid == 0) {
+                // the next marked sets, up to CH, in set order
+                int n = 0, w = s_cursor;
+                while (w < nwords) {
+                    const int ww = w + lane;
+                    const uint32_t bits = ww < nwords ? s_smark[ww] : 0u;
+                    const int c = __popc(bits);
+                    int incl = c;
+#pragma unroll
+                    for (int o = 1; o < 64; o <<= 1) { const int y = __shfl_up(incl, o); if (lane >= o) incl += y; }
+                    const bool fits = ww < nwords && n + incl <= CH;
+                    const int nfit = (int)__popcll(__ballot(fits));       // a prefix of the lanes
+                    if (fits) {
+                        int k = n + incl - c;
+                        for (uint32_t m = bits; m; m &= m - 1) s_mlist[k++] = ww * 32 + __ffs(m) - 1;
+                    }
+                    if (nfit > 0) n += __shfl(incl, nfit - 1);
+                    w += nfit;
+                    if (nfit < 64) break;                  // the words are exhausted or the chunk is full
+                }
+                if (lane == 0) { s_mn = n; s_cursor = w; }
+            }
+            __syncthreads();
+            const int mn = s_mn;
+            for (int q = tid; q < mn * W64; q += STEP_THREADS) {
+                const int i = q / W64, wd = q - i * W64;
+                s_stage[q] = a.setbits[(size_t)s_mlist[i] * W64 + wd];
+            }
+            __syncthreads();
+            for (int i = wid; i < mn; i += NW) {
+                const int set = s_mlist[i];
+                const unsigned long long* sb = s_stage + (size_t)i * W64;
+                uint16_t* rec16 = (uint16_t*)(a.setrec + (size_t)set * a.units);
+                // the first KR brokers of set ∩ bl_move in bl order (move targets, steps.go:192-201)
                 int found = 0;
-                for (int base = 0; base < B && found < cap; base += 64) {
+                for (int base = 0; base < B && found < KR; base += 64) {
                     const int k = base + lane;
                     const int b = k < B ? s_ord[k] : 0;
-                    bool mem = inset(b) && k < B;
-                    mem = mem && ((s_blmb[b >> 6] >> (b & 63)) & 1ull);
+                    const bool mem = k < B && ((sb[b >> 6] >> (b & 63)) & 1ull) && ((s_blmb[b >> 6] >> (b & 63)) & 1ull);
                     const unsigned long long m = __ballot(mem);
                     if (mem) {
                         const int rk = found + (int)__popcll(m & lt);
-                        if (rk < cap) rec16[2 + rk] = (uint16_t)b;
+                        if (rk < KR) rec16[2 + rk] = (uint16_t)b;
                     }
                     found += (int)__popcll(m);
                 }
-                for (int rk = found + lane; rk < cap; rk += 64) rec16[2 + rk] = NONE16;
-                if (lane == 0) rec16[1] = (uint16_t)(found < cap ? found : cap);
+                for (int rk = found + lane; rk < KR; rk += 64) rec16[2 + rk] = NONE16;
+                if (lane == 0) rec16[1] = (uint16_t)(found < KR ? found : KR);
+                int n = lane < W64 ? (int)__popcll(sb[lane] & s_blmb[lane]) : 0;
+                n = wave_sum(n);
+                if (lane == 0) rec16[0] = (uint16_t)n;
             }
-            int n = lane < a.W64 ? (int)__popcll(sbw & s_blmb[lane]) : 0;
-            n = wave_sum(n);
-            if (lane == 0) rec16[0] = (uint16_t)n;
+            __syncthreads();
         }
     }
     if (tid == 0) { C.prepped = 1; C.full_prep = 0; }
@@ -1630,67 +1724,94 @@ __global__ __launch_bounds__(REFRESH_THREADS) void k_refresh(RefreshArgs a) {
 // rank's minimum, a superset of those within 4*eps of the global one)
 __global__ __launch_bounds__(1024) void k_summary(SumArgs a) {
     DevCtl* ctl = a.ctl;
-    RecHdr* out = (RecHdr*)a.out;
-    Contender* okeys = (Contender*)(out + 1);
+    RecHdr* out = a.out.h(0);
+    Contender* okeys = a.out.k(0);
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     __shared__ uint32_t s_key[DEDUP_STEP];
     __shared__ unsigned long long s_wb[DEDUP_STEP], s_it[DEDUP_STEP];
     __shared__ uint32_t s_n, s_fail;
     __shared__ double s_d[2][16];
     __shared__ unsigned long long s_c[2][16];
-    __shared__ uint32_t s_f[NF][16];
+    __shared__ uint32_t s_f[NF];
+    __shared__ uint32_t s_fm[16];
     __shared__ double s_g[2];
+    __shared__ unsigned long long s_benc[2];
+    __shared__ uint32_t s_brec[2];
     Dedup T{s_key, s_wb, s_it, DEDUP_STEP};
     dedup_clear(T);
     if (tid == 0) { s_n = 0; s_fail = 0; }
+    if (tid < NF) s_f[tid] = NONE32;
+    if (tid < 2) { s_benc[tid] = NONE64; s_brec[tid] = NONE32; }
     const bool ran = ctl->halted == H_RUN && ctl->prepped;
+    const double eps = ctl->eps, inv_avg = ctl->inv_avg;
     double d0 = HUGE_VAL, d1 = HUGE_VAL;
     unsigned long long c0 = 0, c1 = 0;
-    uint32_t f[NF];
-    for (int q = 0; q < NF; q++) f[q] = NONE32;
+    uint32_t fm = 0;
     if (ran)
-        for (int i = tid; i < a.nrec; i += 1024) {
-            const RecHdr* h = (const RecHdr*)(a.recs + (size_t)i * WGREC_BYTES);
+        for (int i = tid; i < a.R.n; i += 1024) {
+            const RecHdr* h = a.R.h(i);
             d0 = h->dmin[0] < d0 ? h->dmin[0] : d0;
             d1 = h->dmin[1] < d1 ? h->dmin[1] : d1;
             c0 += h->cand[0]; c1 += h->cand[1];
-            for (int q = 0; q < NF; q++) f[q] = min(f[q], h->first[q]);
+            fm |= h->fmask;
         }
     d0 = wave_min(d0); d1 = wave_min(d1); c0 = wave_sum(c0); c1 = wave_sum(c1);
-    for (int q = 0; q < NF; q++) f[q] = wave_min(f[q]);
+    fm = wave_red_or(fm);
     if (lane == 0) {
         s_d[0][wid] = d0; s_d[1][wid] = d1; s_c[0][wid] = c0; s_c[1][wid] = c1;
-        for (int q = 0; q < NF; q++) s_f[q][wid] = f[q];
+        s_fm[wid] = fm;
     }
     __syncthreads();
+    fm = 0;
+    for (int x = 0; x < 16; x++) fm |= s_fm[x];
+    if (ran && fm) {
+        for (int i = tid; i < a.R.n; i += 1024) {
+            if (!a.R.h(i)->fmask) continue;
+            const uint32_t* fi = a.R.f(i);
+            for (int q = 0; q < NF; q++) if (fi[q] != NONE32) atomicMin(&s_f[q], fi[q]);
+        }
+    }
     if (tid == 0) {
         for (int x = 1; x < 16; x++) {
             d0 = s_d[0][x] < d0 ? s_d[0][x] : d0;
             d1 = s_d[1][x] < d1 ? s_d[1][x] : d1;
             c0 += s_c[0][x]; c1 += s_c[1][x];
-            for (int q = 0; q < NF; q++) f[q] = min(f[q], s_f[q][x]);
         }
         s_g[0] = d0; s_g[1] = d1;
         out->dmin[0] = d0; out->dmin[1] = d1; out->cand[0] = c0; out->cand[1] = c1;
-        for (int q = 0; q < NF; q++) out->first[q] = f[q];
     }
     __syncthreads();
-    const double eps = ctl->eps, inv_avg = ctl->inv_avg;
     auto ins = [&](const Contender& c) {
         const double g = s_g[c.kind];
         if (!(cont_delta(a.r, c, inv_avg) <= g + 4.0 * eps)) return;
         if (dedup_insert(T, c.kind, c.s, c.t, c.w, c.iter) < 0) s_fail = 1;
     };
+    // the rank's best key per kind: the records' best keys re-scored on r
+    unsigned long long myenc[2] = {NONE64, NONE64};
     if (ran) {
-        for (int i = tid; i < a.nrec; i += 1024) {
-            const RecHdr* h = (const RecHdr*)(a.recs + (size_t)i * WGREC_BYTES);
-            const Contender* keys = (const Contender*)(h + 1);
+        for (int i = tid; i < a.R.n; i += 1024) {
+            const RecHdr* h = a.R.h(i);
+            for (int k = 0; k < 2; k++) {
+                const Contender c = h->best[k];
+                if (c.s < 0) continue;
+                const unsigned long long e = enc(cont_delta(a.r, c, inv_avg));
+                if (e < myenc[k]) myenc[k] = e;
+                atomicMin(&s_benc[k], e);
+            }
+            const Contender* keys = a.R.k(i);
             for (uint32_t k = 0; k < h->nkeys; k++) ins(keys[k]);
         }
         const uint32_t nc = min(ctl->ncont, a.cont_cap);
         for (uint32_t i = tid; i < nc; i += 1024) ins(a.cont[i]);
     }
     __syncthreads();
+    if (ran)
+        for (int i = tid; i < a.R.n; i += 1024)
+            for (int k = 0; k < 2; k++) {
+                const Contender c = a.R.h(i)->best[k];
+                if (c.s >= 0 && myenc[k] == s_benc[k] && enc(cont_delta(a.r, c, inv_avg)) == s_benc[k])
+                    atomicMin(&s_brec[k], (uint32_t)i);
+            }
     for (int h = tid; h < DEDUP_STEP; h += 1024) {
         if (s_key[h] == NONE32) continue;
         const uint32_t k = atomicAdd(&s_n, 1u);
@@ -1700,8 +1821,16 @@ __global__ __launch_bounds__(1024) void k_summary(SumArgs a) {
     if (tid == 0) {
         out->nkeys = s_n < (uint32_t)SUMMARY_KEYS ? s_n : (uint32_t)SUMMARY_KEYS;
         out->flags = ((ran && ctl->cont_overflow) || s_fail || s_n > (uint32_t)SUMMARY_KEYS) ? 1u : 0u;
-        out->pad[0] = ran ? 1u : 0u;
-        out->pad[1] = 0;
+        out->ran = ran ? 1u : 0u;
+        uint32_t m = 0;
+        for (int q = 0; q < NF; q++) m |= s_f[q] != NONE32 ? 1u << q : 0u;
+        out->fmask = m;
+        uint32_t* fo = a.out.f(0);
+        for (int q = 0; q < NF; q++) fo[q] = s_f[q];
+        for (int k = 0; k < 2; k++) {
+            if (s_brec[k] != NONE32) out->best[k] = a.R.h((int)s_brec[k])->best[k];
+            else { out->best[k].s = out->best[k].t = -1; out->best[k].w = 0.0; out->best[k].iter = NONE64; out->best[k].kind = k; out->best[k].pad = 0; }
+        }
     }
 }
 

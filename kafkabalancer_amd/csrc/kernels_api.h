@@ -29,7 +29,7 @@ struct ScanArgs {
     const int32_t* blm;
     const int32_t* posm;
     int allow_leader, rebalance, sem_go;
-    unsigned char* recs;      // [nscan][WGREC_BYTES]
+    Recs R;                   // this scan's workgroup records (scan_recs layout)
     Contender* cont;          // spill buffer
     uint32_t cont_cap;
     int listwg;               // 1: the last workgroup applies the pending list op
@@ -59,8 +59,7 @@ struct StepArgs {
     int32_t* cnt;             // [B] replicas held
     const int32_t* bset_off;  // [B+1] sets containing each broker
     const int32_t* bset_ids;
-    const unsigned char* recs;   // scan records or gathered rank summaries
-    int nrec, rec_stride, rec_keys;
+    Recs R;                   // scan records or gathered rank summaries
     const Contender* cont;    // spill buffer (single-GPU mode)
     uint32_t cont_cap;
     int use_spill;
@@ -87,12 +86,11 @@ struct RefreshArgs {
 
 struct SumArgs {
     DevCtl* ctl;
-    const unsigned char* recs;
-    int nrec;
+    Recs R;                   // this rank's scan records
     const Contender* cont;
     uint32_t cont_cap;
     const double* r;
-    unsigned char* out;       // SUMMARY_BYTES
+    Recs out;                 // one summary (summary_recs layout)
 };
 
 void launch_scan(const ScanArgs& a, int rc, bool lds_sets, size_t lds_bytes, hipStream_t st);
