@@ -84,7 +84,7 @@ def main():
     from kafkabalancer_amd import synth
     torch.cuda.set_device(0)
     cl, cfg, desc = synth.config(args.workload, scale=args.scale)
-    eng = E.Engine(cl, cfg, device=0, time_kernels=True)
+    eng = E.Engine(cl, cfg, device=0, time_kernels=False)
     if args.warmup:
         _, err = eng.plan(args.warmup)
         assert err is None, err
@@ -96,10 +96,17 @@ def main():
     wall = time.perf_counter() - t0
     assert err is None, err
     st1 = eng.stats()
-    tk = eng.timings()
     steps = len(changes) + (0 if len(changes) == args.steps else 1)
     cand = st1["candidates"] - st0["candidates"]
     dev_s = st1["device_ms"] / 1e3
+    # per-kernel durations: HIP events around every launch (on the engine's stream)
+    # over a second timed stretch of the same plan; events between the kernels add
+    # their own gaps, so they stay out of the headline timing above
+    eng.set_timing(True)
+    kt_steps = min(args.steps, 200)
+    _, err = eng.plan(kt_steps)
+    assert err is None, err
+    tk = eng.timings()
     scan_ms, scan_n = tk["scan"]
     scan_avg_us = 1e3 * scan_ms / max(scan_n, 1)
     bytes_scan = st1["scan_bytes"]
@@ -123,13 +130,14 @@ def main():
                      "kernel": "k_scan", "bytes_per_launch": bytes_scan,
                      "avg_launch_us": scan_avg_us},
         "kernels_us_per_step": {k: 1e3 * v[0] / max(v[1], 1) for k, v in tk.items()},
+        "kernel_timing_steps": kt_steps,
     }
     if args.stamps:
         st = eng.stamps()
         n = max(1, st1["steps"])
         names = ["prep.S+r+ubloop", "step.loads", "res.reduce", "res.pred", "res.move", "res.apply(tail)", "prep.sort", None,
-                 "prep.blm+cert", "prep.reduce+eps", "prep.sets", "res.move->apply", "loads.bro+ctl", "loads.rec_reduce", "loads.keys", None, "sets.mark"]
-        counts = {"emits": 31, "spills": 30, "walks": 29, "walk_steps": 28, "walk_global": 27}
+                 "prep.blm+cert", "prep.reduce+eps", "prep.sets", "res.move->apply", "loads.bro+ctl", "loads.rec_reduce", "loads.keys", None, "sets.mark", "eps.sync1", "eps.wave0red", "sets.list", "sets.build", "keys.pre", "keys.insert"]
+        counts = {"keys_needed": 26, "emits": 31, "spills": 30, "walks": 29, "walk_steps": 28, "walk_global": 27}
         print(json.dumps({"stamps_us_per_step": {k: st[i] / 100.0 / n for i, k in enumerate(names) if k},
                           "counts_per_step": {k: st[i] / n for k, i in counts.items()},
                           "stats": eng.stats()}))

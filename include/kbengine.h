@@ -173,6 +173,9 @@ int kb_engine_stats(kb_engine *e, kb_stats *out);
  * for k in {0 k_step (resolve + apply + prep), 1 k_scan, 2 k_refresh}.  Returns 3. */
 int kb_engine_timings(kb_engine *e, double *ms, int64_t *launches, int n);
 
+/* Turn the per-kernel events on or off for the following plans (resets the sums). */
+int kb_engine_set_timing(kb_engine *e, int32_t on);
+
 /* Diagnostic: accumulated in-kernel phase stamps (100 MHz ticks) of k_step
  * phases and scan event counts (up to 32 slots, returns the slot count);
  * non-zero only in a -DKB_STAMPS build. */

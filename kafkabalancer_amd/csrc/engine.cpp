@@ -47,6 +47,7 @@ struct kb_engine {
     bool own_st = false;
     int64_t P = 0, Ppad = 0, B = 0, nsets = 0, ntiles = 0, nscan = 0;
     int rcap = 0, rc_dev = 1, K = 3, KR = 6, units = 1, W64 = 1, NP2 = 64;
+    int sb_lds = 0, step_lds_bytes = 0;     // k_step: resident allowed-set words, dynamic LDS
     int sem = KB_SEM_APPLIED, allow_leader = 0, rebalance = 0;
     int64_t minrep = 2;
     double min_unb = 0.01;
@@ -435,6 +436,17 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
     e->nscan = std::min<int64_t>(e->ntiles, (int64_t)per_cu * ncu);
     if (const char* v = getenv("KB_NSCAN")) if (atoi(v) > 0) e->nscan = std::min<int64_t>(e->ntiles, atoi(v));  // diagnostic
     if (const char* v = getenv("KB_DEBUG_SCAN")) e->dbg_scan = atoi(v);                                   // diagnostic
+    {
+        // k_step's LDS: static tables + per-broker arrays (+ every set's words when they fit)
+        const int st_lds = step_static_lds();
+        if (st_lds < 0) { e->last_err = "k_step attributes unavailable"; *out = e; return KB_ERR_HIP; }
+        const int lim = 160 * 1024;
+        const int sbw = (int)e->nsets * e->W64;
+        e->sb_lds = (sbw * 8 <= STEP_SB_MAX && st_lds + step_lds((int)e->B, e->NP2, sbw).total <= lim) ? 1 : 0;
+        if (const char* v = getenv("KB_STEP_SB")) if (*v == '0') e->sb_lds = 0;                           // diagnostic
+        e->step_lds_bytes = step_lds((int)e->B, e->NP2, e->sb_lds ? sbw : 0).total;
+        if (st_lds + e->step_lds_bytes > lim) { e->last_err = "too many brokers for k_step's LDS"; *out = e; return KB_ERR_UNSUPPORTED; }
+    }
     HIPCHK(hipStreamCreateWithFlags(&e->st, hipStreamNonBlocking));
     e->own_st = true;
     HIPCHK(dalloc(&e->w, e->Ppad));
@@ -522,6 +534,7 @@ static void fill_step_args(kb_engine* e, StepArgs& a, const Recs& R, int use_spi
     a.ctl = e->ctl; a.w = e->w; a.rep = e->rep; a.meta = e->meta; a.nc = e->nc; a.Ppad = e->Ppad;
     a.RC = e->rc_dev; a.KR = e->KR; a.K = e->K; a.units = e->units; a.W64 = e->W64; a.B = (int)e->B;
     a.nsets = (int)e->nsets; a.NP2 = e->NP2;
+    a.sb_lds = e->sb_lds; a.lds_bytes = e->step_lds_bytes;
     a.setbits = e->setbits; a.setrec = e->setrec;
     a.order = e->order; a.posu = e->posu; a.blm = e->blm; a.posm = e->posm; a.r = e->r;
     a.load = e->load; a.lerr = e->lerr; a.eb = e->eb; a.bfl = e->bfl; a.cnt = e->cnt;
@@ -836,6 +849,15 @@ extern "C" int kb_engine_timings(kb_engine* e, double* ms, int64_t* launches, in
     return TK_N;
 }
 
+extern "C" int kb_engine_set_timing(kb_engine* e, int32_t on) {
+    if (!e) return KB_ERR_INVALID;
+    HIPCHK(hipStreamSynchronize(e->st));
+    e->tev_used = 0;
+    for (int k = 0; k < TK_N; k++) { e->kms[k] = 0; e->klaunch[k] = 0; }
+    e->time_kernels = on ? 1 : 0;
+    return KB_OK;
+}
+
 extern "C" int kb_engine_stamps(kb_engine* e, uint64_t* out, int n) {
     if (!e || !out) return KB_ERR_INVALID;
     DevCtl c;
@@ -858,12 +880,38 @@ extern "C" int kb_engine_bench_scan(kb_engine* e, int iters, double* avg_us) {
     HIPCHK(hipEventCreate(&a));
     HIPCHK(hipEventCreate(&b));
     enqueue_scan(e);                                  // warm
-    HIPCHK(hipEventRecord(a, e->st));
-    for (int i = 0; i < iters; i++) enqueue_scan(e);
-    HIPCHK(hipEventRecord(b, e->st));
-    HIPCHK(hipEventSynchronize(b));
+    // KB_PROBE_INTERLEAVE (diagnostic): 1 = an empty one-workgroup kernel between the
+    // scans, 2 = one that rewrites the scan's tables (as k_step does); each scan is
+    // then timed on its own
+    int il = 0;
+    if (const char* v = getenv("KB_PROBE_INTERLEAVE")) il = atoi(v);
     float ms = 0;
-    hipEventElapsedTime(&ms, a, b);
+    if (il) {
+        hipEvent_t c, d;
+        HIPCHK(hipEventCreate(&c));
+        HIPCHK(hipEventCreate(&d));
+        double tot = 0;
+        for (int i = 0; i < iters; i++) {
+            launch_touch(e->r, il == 2 ? (int)e->B : 0, e->blm, e->posm, e->setrec,
+                         il == 2 ? (int)e->nsets * e->units : 0, e->st);
+            HIPCHK(hipEventRecord(c, e->st));
+            enqueue_scan(e);
+            HIPCHK(hipEventRecord(d, e->st));
+            HIPCHK(hipEventSynchronize(d));
+            float x = 0;
+            hipEventElapsedTime(&x, c, d);
+            tot += x;
+        }
+        ms = (float)tot;
+        hipEventDestroy(c);
+        hipEventDestroy(d);
+    } else {
+        HIPCHK(hipEventRecord(a, e->st));
+        for (int i = 0; i < iters; i++) enqueue_scan(e);
+        HIPCHK(hipEventRecord(b, e->st));
+        HIPCHK(hipEventSynchronize(b));
+        hipEventElapsedTime(&ms, a, b);
+    }
     *avg_us = 1e3 * ms / iters;
     hipEventDestroy(a);
     hipEventDestroy(b);

@@ -7,9 +7,9 @@ namespace kbe {
 
 constexpr int MAXB = 4096;          // dense broker universe limit (sorted in LDS)
 constexpr int MAXR = 16;            // replica slots per partition
-constexpr int SCAN_THREADS = 512;   // k_scan workgroup
+constexpr int SCAN_THREADS = 1024;  // k_scan workgroup (one per CU)
 constexpr int PER_LANE = 2;         // consecutive partitions per lane (vector loads)
-constexpr int TILE = SCAN_THREADS * PER_LANE;   // 1024 partitions per scan tile
+constexpr int TILE = SCAN_THREADS * PER_LANE;   // 2048 partitions per scan tile
 constexpr int SHARD_ALIGN = 1024;   // shard boundaries (multi-GPU) are multiples of this
 constexpr int STEP_THREADS = 1024;  // k_step: one workgroup
 constexpr uint32_t NONE32 = 0xFFFFFFFFu;
@@ -71,9 +71,9 @@ struct RecHdr {                     // 112 B
     double dmin[2];                 // min score delta {leader, non-leader}
     unsigned long long cand[2];     // reference candidate counts
     uint32_t nkeys;                 // near-tie keys stored for this record
-    uint32_t flags;                 // bit0: keys spilled / overflowed (see k_step)
+    uint32_t flags;                 // bit0: keys overflowed (see k_step); bit1: summaries: the scan ran
     uint32_t fmask;                 // bit q: first[q] != NONE32 (first-index predicates)
-    uint32_t ran;                   // summaries: the rank's scan ran
+    uint16_t nkk[2];                // keys per kind within the window (stored or spilled)
     Contender best[2];              // the record's minimum-score key per kind (s < 0: none);
                                     // k_step re-scores them for the next step's upper bound
 };
@@ -113,6 +113,22 @@ inline Recs summary_recs(unsigned char* base, int n) {
     r.n = n; r.cap = SUMMARY_KEYS;
     return r;
 }
+
+// dynamic LDS of k_step (byte offsets): loads [B], error bounds / sort keys [NP2],
+// universe order [NP2], allowed-set words of every set when resident [sbw], flags [B]
+struct StepLds { int e, ord, sb, fl, total; };
+__host__ __device__ inline StepLds step_lds(int B, int NP2, int sbw) {
+    auto al = [](int x) { return (x + 15) & ~15; };
+    StepLds L;
+    int o = al(B * 8);
+    L.e = o;   o += al(NP2 * 8);
+    L.ord = o; o += al(NP2 * 4);
+    L.sb = o;  o += al(sbw * 8);
+    L.fl = o;  o += al(B);
+    L.total = o;
+    return L;
+}
+constexpr int STEP_SB_MAX = 65536;  // allowed-set words kept in k_step's LDS up to this size
 
 struct ChangeDev {
     int32_t status, step, kind, slot;

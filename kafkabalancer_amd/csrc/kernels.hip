@@ -396,7 +396,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
     extern __shared__ __align__(16) unsigned char smem[];
     __shared__ int s_i;
     DevCtl* ctl = a.ctl;
-    if (a.listwg && (int)blockIdx.x == a.nscan) { do_list_op(ctl, a.L, &s_i); return; }
+    if (a.listwg && (int)blockIdx.x == a.nscan) { if (!(a.dbg & 8)) do_list_op(ctl, a.L, &s_i); return; }
     constexpr int U = sr_units(RC);
     constexpr int NW = SCAN_THREADS / 64;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -416,7 +416,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
     __shared__ unsigned long long s_c[2][NW];
     __shared__ uint32_t s_nk;
     __shared__ unsigned long long s_benc[2];
-    __shared__ uint32_t s_bslot[2];
+    __shared__ uint32_t s_bslot[2], s_nkk[2];
 
     // every load that does not depend on the control block goes out first: the
     // first tile's stream, then the lookup tables (one memory round trip)
@@ -432,7 +432,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
     if (LSETS) for (int i = tid; i < a.nsets * U; i += SCAN_THREADS) s_set[i] = a.setrec[i];
     for (int i = tid; i < DEDUP_SCAN; i += SCAN_THREADS) { s_key[i] = NONE32; s_wb[i] = NONE64; s_it[i] = NONE64; }
     if (tid == 0) s_nk = 0;
-    if (tid < 2) { s_benc[tid] = NONE64; s_bslot[tid] = NONE32; }
+    if (tid < 2) { s_benc[tid] = NONE64; s_bslot[tid] = NONE32; s_nkk[tid] = 0; }
     const bool run = ctl->halted == H_RUN && ctl->prepped && ctl->steps < ctl->budget;
     const double inv_avg = ctl->inv_avg, eps = ctl->eps;
     const double ubL = ctl->ub[0], ubN = ctl->ub[1];
@@ -603,8 +603,13 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
     // workgroup record: counts, first-index predicates, minima, near-tie keys
     cL = wave_sum(cL);
     cN = wave_sum(cN);
+    bool anyf = false;
 #pragma unroll
-    for (int f = 0; f < NF; f++) fst[f] = wave_min(fst[f]);
+    for (int f = 0; f < NF; f++) anyf |= fst[f] != NONE32;
+    if (__ballot(anyf)) {                          // first-index predicates are rare
+#pragma unroll
+        for (int f = 0; f < NF; f++) fst[f] = wave_min(fst[f]);
+    }
     __shared__ double s_wm[2][NW];
     if (lane == 0) {
         s_c[0][wid] = cL; s_c[1][wid] = cN;
@@ -613,11 +618,9 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
         for (int f = 0; f < NF; f++) s_f[f][wid] = fst[f];
     }
     __syncthreads();   // also orders every census insert before the flush
-#pragma unroll
-    for (int x = 0; x < NW; x++) {
-        wgL = s_wm[0][x] < wgL ? s_wm[0][x] : wgL;
-        wgN = s_wm[1][x] < wgN ? s_wm[1][x] : wgN;
-    }
+    // the wave partials, combined lane-parallel (no serial LDS chains)
+    wgL = wave_min(lane < NW ? s_wm[0][lane] : HUGE_VAL);
+    wgN = wave_min(lane < NW ? s_wm[1][lane] : HUGE_VAL);
     RecHdr* hdr = a.R.h(blockIdx.x);
     Contender* keys = a.R.k(blockIdx.x);
     // the near-tie keys within 4*eps of the workgroup minima; the minimum-score key
@@ -633,6 +636,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
         if (d <= g + 4.0 * eps) {
             myh = tid; mykind = c.kind; myenc = enc(d);
             atomicMin(&s_benc[c.kind], myenc);
+            atomicAdd(&s_nkk[c.kind], 1u);
             const uint32_t k = atomicAdd(&s_nk, 1u);
             if (k < (uint32_t)TILE_KEYS) keys[k] = c;
             else emit_global(ctl, a.cont, a.cont_cap, c);
@@ -641,22 +645,31 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
     __syncthreads();
     if (myh >= 0 && myenc == s_benc[mykind]) atomicMin(&s_bslot[mykind], (uint32_t)myh);
     __syncthreads();
-    if (tid == 0) {
-        RecHdr r;
+    static_assert((NF * NW) % 64 == 0 && 64 % NW == 0, "(predicate, wave) partials in whole waves");
+    if (wid == 0) {
+        cL = wave_sum(lane < NW ? s_c[0][lane] : 0ull);
+        cN = wave_sum(lane < NW ? s_c[1][lane] : 0ull);
         uint32_t fm = 0;
-        for (int x = 1; x < NW; x++) {
-            cL += s_c[0][x]; cN += s_c[1][x];
 #pragma unroll
-            for (int f = 0; f < NF; f++) fst[f] = min(fst[f], s_f[f][x]);
+        for (int c0 = 0; c0 < NF * NW; c0 += 64) {
+            const uint32_t fv = (&s_f[0][0])[c0 + lane];     // s_f[f][w] at f * NW + w
+            if (__ballot(fv != NONE32)) {
+#pragma unroll
+                for (int f = c0 / NW; f < (c0 + 64) / NW; f++) {
+                    fst[f] = wave_min((c0 + lane) / NW == f ? fv : NONE32);
+                    fm |= fst[f] != NONE32 ? 1u << f : 0u;
+                }
+            }
         }
-#pragma unroll
-        for (int f = 0; f < NF; f++) fm |= fst[f] != NONE32 ? 1u << f : 0u;
+      if (lane == 0) {
+        RecHdr r;
         r.dmin[0] = wgL; r.dmin[1] = wgN;
         r.cand[0] = cL; r.cand[1] = cN;
         r.nkeys = s_nk < (uint32_t)TILE_KEYS ? s_nk : (uint32_t)TILE_KEYS;
         r.flags = 0;
         r.fmask = fm;
-        r.ran = 1;
+        r.nkk[0] = (uint16_t)min(s_nkk[0], 0xFFFFu);
+        r.nkk[1] = (uint16_t)min(s_nkk[1], 0xFFFFu);
 #pragma unroll
         for (int k = 0; k < 2; k++) {
             if (s_bslot[k] != NONE32) r.best[k] = dedup_entry(T, (int)s_bslot[k]);
@@ -668,6 +681,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
 #pragma unroll
             for (int f = 0; f < NF; f++) fo[f] = fst[f];
         }
+      }
     }
 }
 
@@ -678,6 +692,7 @@ struct Decision {
     long long part;
     int32_t from, to;
     double su, cu;
+    double w;                       // move(): the partition weight of the winning key
     int32_t exact, err, err_broker, pad;
 };
 
@@ -747,14 +762,19 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
     __shared__ unsigned long long s_cand[2];
     __shared__ uint32_t s_first[NF];
     __shared__ uint32_t s_flags, s_fm;
+    __shared__ int s_kc[2], s_sok[2];
+    __shared__ Contender s_single[2];
     __shared__ double s_sux;
     __shared__ uint32_t s_key[DEDUP_STEP];
     __shared__ unsigned long long s_wb[DEDUP_STEP], s_it[DEDUP_STEP];
-    __shared__ double s_ld[MAXB];                    // loads by broker id
-    __shared__ double s_e[MAXB];                     // load error bounds; zero whenever every load is
+    extern __shared__ __align__(16) unsigned char dsm[];
+    const StepLds LY = step_lds(a.B, a.NP2, a.sb_lds ? a.nsets * a.W64 : 0);
+    double* s_ld = (double*)dsm;                     // loads by broker id
+    double* s_e = (double*)(dsm + LY.e);             // load error bounds; zero whenever every load is
                                                      // exact, so then also sort keys / exact bl loads
-    __shared__ int32_t s_ord[MAXB];                  // universe order by (load, id)
-    __shared__ uint8_t s_fl[MAXB];                   // BF_* flags
+    int32_t* s_ord = (int32_t*)(dsm + LY.ord);       // universe order by (load, id)
+    uint64_t* s_sb = (uint64_t*)(dsm + LY.sb);       // allowed-set words (sb_lds)
+    uint8_t* s_fl = dsm + LY.fl;                     // BF_* flags
     __shared__ int s_T[TMAX], s_posT[TMAX];
     __shared__ int s_cntT[TMAX];
     __shared__ uint64_t s_blmb[MAXB / 64], s_presb[MAXB / 64];
@@ -763,12 +783,33 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
     Dedup T{s_key, s_wb, s_it, DEDUP_STEP, s_nd, s_li};
     const int B = a.B;
 
-    // ---- one memory round trip: the broker state, the scan records, the control block
+    // ---- one memory round trip: the broker state, the allowed-set words, the control
+    // block and (speculatively: the buffer always exists) the first record's header
     for (int b = tid; b < B; b += STEP_THREADS) {
         s_ld[b] = a.load[b];
         s_e[b] = a.eb[b];
         s_fl[b] = a.bfl[b];
         s_ord[b] = a.order[b];
+    }
+    if (a.sb_lds) {
+        const int nq = a.nsets * a.W64;                   // 16-B loads (the rows are contiguous)
+        for (int q = 2 * tid; q < nq; q += 2 * STEP_THREADS) {
+            if (q + 1 < nq) *(uint4*)(s_sb + q) = *(const uint4*)(a.setbits + q);
+            else s_sb[q] = a.setbits[q];
+        }
+    }
+    double hd0 = HUGE_VAL, hd1 = HUGE_VAL;
+    unsigned long long hc0 = 0, hc1 = 0;
+    uint32_t hflg = 0, hfm = 0, hnk0 = 0, hnk1 = 0;
+    Contender hb0, hb1;                              // the record's best keys
+    hb0.s = hb1.s = -1;
+    if (tid < a.R.n) {
+        const RecHdr* h = a.R.h(tid);
+        hd0 = h->dmin[0]; hd1 = h->dmin[1];
+        hc0 = h->cand[0]; hc1 = h->cand[1];
+        hflg = h->flags & 1u; hfm = h->fmask;
+        hnk0 = h->nkk[0]; hnk1 = h->nkk[1];
+        hb0 = h->best[0]; hb1 = h->best[1];
     }
     dedup_clear(T);
     if (tid < 2) { s_nd[tid] = 0; s_li[tid] = -1; s_kfail[tid] = 0; }
@@ -792,15 +833,15 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
     // its record's near-tie keys of both kinds within 4*eps of the minima (distinct
     // keys, earliest iteration index per key)
     if (do_res) {
-        double d0 = HUGE_VAL, d1 = HUGE_VAL;
-        unsigned long long c0 = 0, c1 = 0;
-        uint32_t flg = 0, fm = 0;
-        for (int i = tid; i < a.R.n; i += STEP_THREADS) {
+        double d0 = hd0, d1 = hd1;
+        unsigned long long c0 = hc0, c1 = hc1;
+        uint32_t flg = hflg, fm = hfm;
+        for (int i = tid + STEP_THREADS; i < a.R.n; i += STEP_THREADS) {
             const RecHdr* h = a.R.h(i);
             d0 = h->dmin[0] < d0 ? h->dmin[0] : d0;
             d1 = h->dmin[1] < d1 ? h->dmin[1] : d1;
             c0 += h->cand[0]; c1 += h->cand[1];
-            flg |= h->flags;
+            flg |= h->flags & 1u;
             fm |= h->fmask;
         }
         d0 = wave_min(d0); d1 = wave_min(d1); c0 = wave_sum(c0); c1 = wave_sum(c1);
@@ -829,6 +870,7 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
                 s_fm = fm;
             }
             if (lane < NF) s_first[lane] = NONE32;
+            if (lane < 2) s_kc[lane] = 0;
         }
         __syncthreads();
         if (s_fm) {
@@ -851,9 +893,40 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
         }
         KB_STAMP(ctl, 13);
         const double g0 = s_g[0], g1 = s_g[1];
-        for (int i = tid; i < a.R.n; i += STEP_THREADS) {
+        // keys within the window, per kind, over the records within 8*eps of the
+        // minimum; a kind with exactly one such key needs no key round trip: it is
+        // that record's best key (inserted here speculatively in any case)
+        {
+            int kc0 = 0, kc1 = 0;
+            KB_STAMP(ctl, 21);
+            if (tid < a.R.n) {
+                const bool q0 = hd0 <= g0 + 8.0 * eps, q1 = hd1 <= g1 + 8.0 * eps;
+                kc0 = q0 ? (int)hnk0 : 0;
+                kc1 = q1 ? (int)hnk1 : 0;
+                // (a kind with one key overall: this record's best key is it; the write
+                // is meaningful only then)
+                if (kc0 && hb0.s >= 0) { s_single[0] = hb0; s_sok[0] = cont_delta_ld(s_ld, hb0, inv_avg) <= g0 + 4.0 * eps; }
+                if (kc1 && hb1.s >= 0) { s_single[1] = hb1; s_sok[1] = cont_delta_ld(s_ld, hb1, inv_avg) <= g1 + 4.0 * eps; }
+            }
+            KB_STAMP(ctl, 22);
+            kc0 = wave_sum(kc0); kc1 = wave_sum(kc1);
+            if (lane == 0) {
+                if (kc0) atomicAdd(&s_kc[0], kc0);
+                if (kc1) atomicAdd(&s_kc[1], kc1);
+            }
+        }
+        __syncthreads();
+        // single-key kinds need the raw spill buffer to be empty (its keys are not counted)
+        const bool many = a.R.n > STEP_THREADS || (a.use_spill && C.ncont > 0);
+        const bool need0 = many || s_kc[0] > 1, need1 = many || s_kc[1] > 1;
+        if (tid < 2 && !(tid ? need1 : need0) && s_kc[tid] == 1) {
+            s_nd[tid] = s_sok[tid] ? 1 : 0;          // resolve takes s_single (s_li == -2)
+            s_li[tid] = -2;
+        }
+        if (tid == 0 && (need0 || need1)) KB_COUNT(ctl, 26, 1);
+        for (int i = tid; (need0 || need1) && i < a.R.n; i += STEP_THREADS) {
             const RecHdr* h = a.R.h(i);
-            const bool q0 = h->dmin[0] <= g0 + 8.0 * eps, q1 = h->dmin[1] <= g1 + 8.0 * eps;
+            const bool q0 = need0 && h->dmin[0] <= g0 + 8.0 * eps, q1 = need1 && h->dmin[1] <= g1 + 8.0 * eps;
             if (!q0 && !q1) continue;
             const Contender* keys = a.R.k(i);
             const int nk = (int)min(h->nkeys, (uint32_t)a.R.cap);
@@ -1058,7 +1131,7 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
             cw.s = cw.t = -1; cw.w = 0; cw.iter = NONE64; cw.kind = kind; cw.pad = 0;
             bool certain = false, c_improved = false, c_take = false;
             if (!fail && ndist == 1) {
-                cw = dedup_entry(T, s_li[kind]);    // the one claimed slot
+                cw = s_li[kind] == -2 ? s_single[kind] : dedup_entry(T, s_li[kind]);   // the one key
                 Ua = U0h + cont_delta_ld(s_ld, cw, inv_avg);
                 // |Ua - U'| <= eps and |U0h - su| <= eps; margins of 3*eps on both decisions
                 const double thr = U0h - a.min_unbalance;
@@ -1159,7 +1232,7 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
                     } else {
                         D.status = 1; D.step = step; D.kind = 1;
                         D.part = (long long)(witer >> 21); D.slot = (int)((witer >> 16) & 31);
-                        D.from = cw.s; D.to = cw.t; D.su = sux; D.cu = Ustar; D.exact = exact;
+                        D.from = cw.s; D.to = cw.t; D.w = cw.w; D.su = sux; D.cu = Ustar; D.exact = exact;
                         s_done = 1;
                     }
                 } else {
@@ -1183,89 +1256,123 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
 
         // ---------------------------------------------------------- apply
         // wave 0, one lane per replica slot (lanes 0..15 the old replicas, 16..31 the
-        // new ones); cross-lane work by ballot / readlane, three memory round trips
+        // new ones); cross-lane work by ballot / readlane.  A move() replacement takes
+        // a one-round-trip path: no partition holds a disallowed replica when move()
+        // runs (MoveDisallowedReplicas comes first, balancer.go:34-44) and the target is
+        // inside the set, so the meta word is unchanged and only the source and the
+        // target change (contribution W, or W * (len(R) + NumConsumers) at slot 0)
         KB_STAMP(ctl, 11);
         if (wid == 0) {
             int nT = 0;
             const bool chg = D.status == 1;
             const long long p = D.part;
             const int kind = D.kind, slot = D.slot, to = D.to;
-            int ro = -1;                                 // old replica at slot `lane`
-            uint32_t m = 0;
-            double wv = 0.0;
-            int ncp = 0;
-            if (chg) {
-                if (lane < a.RC) ro = (int)a.rep[(long long)lane * a.Ppad + p];
-                m = a.meta[p];
-                wv = a.w[p];
-                ncp = a.nc[p];
-            }
-            const int nrep = (int)meta_nrep(m);
-            if (lane >= nrep) ro = -1;
-            // the new replica list (replacepl / addpl, utils.go:166-202)
-            int rn = ro, nn = nrep;
-            bool state_changed = chg;
-            const unsigned long long ball_to = __ballot(ro == to && lane < 16);
-            if (kind == 1) {                             // replace at slot (utils.go:186-190)
-                if (lane == slot) rn = to;
-            } else if (kind == 4) {                      // swap with the existing replica (utils.go:179-185)
-                const int ex = ball_to ? (int)__ffsll((long long)ball_to) - 1 : 0;
-                const int ro_slot = __shfl(ro, slot);
-                if (lane == slot) rn = to;
-                else if (lane == ex) rn = ro_slot;
-            } else if (kind == 2) {                      // remove (utils.go:176-178)
-                const int nxt = __shfl(ro, (lane + 1) & 63);
-                if (lane >= slot && lane + 1 < nrep) rn = nxt;
-                if (a.sem_go) state_changed = false;     // pl keeps its length: duplicates
-                else { nn = nrep - 1; if (lane == nn) rn = -1; }
-            } else if (kind == 3) {                      // add (utils.go:199-202)
-                if (a.sem_go) state_changed = false;     // the append is not visible through pl
-                else { nn = nrep + 1; if (lane == nrep) rn = to; }
-            }
-            const bool go_remove = chg && a.sem_go && kind == 2;
-            const int nw = go_remove ? nrep : nn;        // the replica slots written
-            if (state_changed || go_remove) {
-                // the allowed-set words of the new replicas (Disallowed trigger, in-set count)
-                bool in = false;
-                if (lane < nw) in = (a.setbits[(size_t)meta_set(m) * a.W64 + (rn >> 6)] >> (rn & 63)) & 1ull;
-                const unsigned long long bin = __ballot(in && lane < nw), bout = __ballot(!in && lane < nw);
-                if (lane < nw) a.rep[(long long)lane * a.Ppad + p] = (uint16_t)rn;
-                if (lane == 0)
-                    a.meta[p] = make_meta((uint32_t)nw, meta_want(m), meta_elig(m), bout ? 1u : 0u,
-                                          (uint32_t)__popcll(bin), meta_set(m));
-            }
-            if (state_changed) {
-                // contributions of getBrokerLoad (utils.go:92-105): the leader slot carries
-                // W * (len(R) + NumConsumers); lanes 0..15 hold the old replicas, 16..31 the new
-                const int j = lane & 15;
-                const bool old_lane = lane < 16 && j < nrep, new_lane = lane >= 16 && lane < 32 && j < nn;
-                const int rnew_j = __shfl(rn, j);
-                const int b = old_lane ? ro : (new_lane ? rnew_j : -1);
-                const double oc = old_lane ? (j == 0 ? wv * (double)(nrep + ncp) : wv) : 0.0;
-                const double nc_here = new_lane ? (j == 0 ? wv * (double)(nn + ncp) : wv) : 0.0;
-                // pair an old replica with the same broker among the new ones
-                double cn_other = 0.0;
-                bool matched = false;
-                for (int q = 0; q < 16; q++) {
-                    const int bq = __shfl(rn, q);           // new replica q
-                    const int bo = __shfl(ro, q);           // old replica q
-                    const double ncq = q < nn ? (q == 0 ? wv * (double)(nn + ncp) : wv) : 0.0;
-                    if (old_lane && q < nn && bq == b) { cn_other = ncq; matched = true; }
-                    if (new_lane && q < nrep && bo == b) matched = true;
-                }
-                // per broker: (old, new) contribution; new-only brokers from the new lanes
-                const bool rep_lane = old_lane || (new_lane && !matched);
-                const double oldc = old_lane ? oc : 0.0;
-                const double newc = old_lane ? cn_other : nc_here;
-                const int dcnt = old_lane ? (matched ? 0 : -1) : 1;
-                const bool touched = rep_lane && oldc != newc;
-                const bool cnt_changes = rep_lane && dcnt != 0;
-                int cv = 0;
-                double av = 0.0;
-                if (touched || cnt_changes) {               // their counts and error terms
+            const bool fast = chg && kind == 1 && (D.step == 7 || D.step == 8);
+            bool upd = false, act = false;
+            int b = -1, dcnt = 0, cv = 0;
+            double oldc = 0.0, newc = 0.0, av = 0.0;
+            if (fast) {
+                b = lane == 0 ? D.from : to;
+                if (lane < 2) {                              // every load in one round trip
                     cv = a.cnt[b];
                     if (!a.integral) av = a.lerr[b];
                 }
+                double c = D.w;
+                if (slot == 0) {
+                    const uint32_t m = a.meta[p];
+                    c = D.w * (double)((int)meta_nrep(m) + a.nc[p]);
+                }
+                if (lane == 0) a.rep[(long long)slot * a.Ppad + p] = (uint16_t)to;
+                act = lane < 2;
+                oldc = lane == 0 ? c : 0.0;
+                newc = lane == 0 ? 0.0 : c;
+                dcnt = lane == 0 ? -1 : 1;
+                upd = true;
+            } else {
+                int ro = -1;                                 // old replica at slot `lane`
+                uint32_t m = 0;
+                double wv = 0.0;
+                int ncp = 0;
+                if (chg) {
+                    if (lane < a.RC) ro = (int)a.rep[(long long)lane * a.Ppad + p];
+                    m = a.meta[p];
+                    wv = a.w[p];
+                    ncp = a.nc[p];
+                }
+                const int nrep = (int)meta_nrep(m);
+                if (lane >= nrep) ro = -1;
+                // the new replica list (replacepl / addpl, utils.go:166-202)
+                int rn = ro, nn = nrep;
+                bool state_changed = chg;
+                const unsigned long long ball_to = __ballot(ro == to && lane < 16);
+                if (kind == 1) {                             // replace at slot (utils.go:186-190)
+                    if (lane == slot) rn = to;
+                } else if (kind == 4) {                      // swap with the existing replica (utils.go:179-185)
+                    const int ex = ball_to ? (int)__ffsll((long long)ball_to) - 1 : 0;
+                    const int ro_slot = __builtin_amdgcn_readlane(ro, __builtin_amdgcn_readfirstlane(slot));
+                    if (lane == slot) rn = to;
+                    else if (lane == ex) rn = ro_slot;
+                } else if (kind == 2) {                      // remove (utils.go:176-178)
+                    const int nxt = __shfl(ro, (lane + 1) & 63);
+                    if (lane >= slot && lane + 1 < nrep) rn = nxt;
+                    if (a.sem_go) state_changed = false;     // pl keeps its length: duplicates
+                    else { nn = nrep - 1; if (lane == nn) rn = -1; }
+                } else if (kind == 3) {                      // add (utils.go:199-202)
+                    if (a.sem_go) state_changed = false;     // the append is not visible through pl
+                    else { nn = nrep + 1; if (lane == nrep) rn = to; }
+                }
+                const bool go_remove = chg && a.sem_go && kind == 2;
+                const int nw = go_remove ? nrep : nn;        // the replica slots written
+                if (state_changed || go_remove) {
+                    // the allowed-set words of the new replicas (Disallowed trigger, in-set count)
+                    bool in = false;
+                    if (lane < nw) {
+                        // (typed LDS pointer: the two loads must not merge into one flat load)
+                        const size_t wi = (size_t)meta_set(m) * a.W64 + (rn >> 6);
+                        const uint64_t wd = a.sb_lds ? ((const __attribute__((address_space(3))) uint64_t*)s_sb)[wi]
+                                                     : a.setbits[wi];
+                        in = (wd >> (rn & 63)) & 1ull;
+                    }
+                    const unsigned long long bin = __ballot(in && lane < nw), bout = __ballot(!in && lane < nw);
+                    if (lane < nw) a.rep[(long long)lane * a.Ppad + p] = (uint16_t)rn;
+                    if (lane == 0)
+                        a.meta[p] = make_meta((uint32_t)nw, meta_want(m), meta_elig(m), bout ? 1u : 0u,
+                                              (uint32_t)__popcll(bin), meta_set(m));
+                }
+                if (state_changed) {
+                    // contributions of getBrokerLoad (utils.go:92-105): the leader slot carries
+                    // W * (len(R) + NumConsumers); lanes 0..15 hold the old replicas, 16..31 the new
+                    const int j = lane & 15;
+                    const bool old_lane = lane < 16 && j < nrep, new_lane = lane >= 16 && lane < 32 && j < nn;
+                    const int rnew_j = __shfl(rn, j);
+                    b = old_lane ? ro : (new_lane ? rnew_j : -1);
+                    const double oc = old_lane ? (j == 0 ? wv * (double)(nrep + ncp) : wv) : 0.0;
+                    const double nc_here = new_lane ? (j == 0 ? wv * (double)(nn + ncp) : wv) : 0.0;
+                    // pair an old replica with the same broker among the new ones
+                    double cn_other = 0.0;
+                    bool matched = false;
+                    for (int q = 0; q < 16; q++) {
+                        const int bq = __builtin_amdgcn_readlane(rn, q);   // new replica q
+                        const int bo = __builtin_amdgcn_readlane(ro, q);   // old replica q
+                        const double ncq = q < nn ? (q == 0 ? wv * (double)(nn + ncp) : wv) : 0.0;
+                        if (old_lane && q < nn && bq == b) { cn_other = ncq; matched = true; }
+                        if (new_lane && q < nrep && bo == b) matched = true;
+                    }
+                    // per broker: (old, new) contribution; new-only brokers from the new lanes
+                    act = old_lane || (new_lane && !matched);
+                    oldc = old_lane ? oc : 0.0;
+                    newc = old_lane ? cn_other : nc_here;
+                    dcnt = old_lane ? (matched ? 0 : -1) : 1;
+                    if (act && (oldc != newc || dcnt != 0)) {    // their counts and error terms
+                        cv = a.cnt[b];
+                        if (!a.integral) av = a.lerr[b];
+                    }
+                    upd = true;
+                }
+            }
+            if (upd) {
+                const bool touched = act && oldc != newc;
+                const bool cnt_changes = act && dcnt != 0;
                 int dd = 0;
                 if (touched || cnt_changes) {
                     const int cnew = cv + dcnt;
@@ -1455,13 +1562,12 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
             }
         }
         int incl = c;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) { int y = __shfl_up(incl, o); if (lane >= o) incl += y; }
+        incl = wave_incl_scan(incl);
         __shared__ int s_wcnt[NW];
         if (lane == 63) s_wcnt[wid] = incl;
         __syncthreads();
-        int woff = 0, total = 0;
-        for (int x = 0; x < NW; x++) { if (x < wid) woff += s_wcnt[x]; total += s_wcnt[x]; }
+        const int wc = lane < NW ? s_wcnt[lane] : 0;
+        const int woff = wave_sum(lane < wid ? wc : 0), total = wave_sum(wc);
         int pos = woff + incl - c;
 #pragma unroll
         for (int q = 0; q < 4; q++) {
@@ -1503,9 +1609,8 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
     sS = wave_sum(sS); sE = wave_sum(sE);
     if (lane == 0) { s_q[0][wid] = sS; s_q[1][wid] = sE; }
     __syncthreads();
-    double S = 0.0, E = 0.0;
-#pragma unroll
-    for (int x = 0; x < NW; x++) { S += s_q[0][x]; E += s_q[1][x]; }
+    // the wave partials, combined lane-parallel (no serial LDS chain)
+    const double S = wave_sum(lane < NW ? s_q[0][lane] : 0.0), E = wave_sum(lane < NW ? s_q[1][lane] : 0.0);
     const double avg = S / (double)nblm;
     const double iav = 1.0 / avg;
     double su = 0.0, v = 0.0, rm = 0.0;
@@ -1543,15 +1648,17 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
     __syncthreads();
     if (lane == 0) { s_q[0][wid] = su; s_q[1][wid] = v; s_q[2][wid] = rm; s_ubw[0][wid] = ub0; s_ubw[1][wid] = ub1; }
     __syncthreads();
-    double U0 = 0.0, V = 0.0, Rm = 0.0;
-    if (tid == 0)
-#pragma unroll
-        for (int x = 0; x < NW; x++) {
-            U0 += s_q[0][x]; V += s_q[1][x]; Rm = s_q[2][x] > Rm ? s_q[2][x] : Rm;
-            ub0 = s_ubw[0][x] < ub0 ? s_ubw[0][x] : ub0;
-            ub1 = s_ubw[1][x] < ub1 ? s_ubw[1][x] : ub1;
-        }
-    if (tid == 0) {
+    KB_STAMP(ctl, 17);
+    if (wid == 0) {
+        const bool in = lane < NW;
+        const double U0 = wave_sum(in ? s_q[0][lane] : 0.0), V = wave_sum(in ? s_q[1][lane] : 0.0);
+        const double Rm = wave_max(in ? s_q[2][lane] : 0.0);
+        ub0 = wave_min(in ? s_ubw[0][lane] : HUGE_VAL);
+        ub1 = wave_min(in ? s_ubw[1][lane] : HUGE_VAL);
+#ifdef KB_STAMPS
+        if (lane == 0) { const unsigned long long _t = wall_clock64(); _kb_st[18] += _t - _kb_t0; _kb_t0 = _t; }
+#endif
+      if (lane == 0) {
         const double u = DBL_EPSILON / 2;
         const double n = (double)nblm;
         const double R = Rm + a.wmax * iav;
@@ -1566,6 +1673,7 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
         C.want_refresh = (epsl > epsf || C.ndirty >= 256) ? 1 : 0;
         C.ncont = 0;
         C.cont_overflow = 0;
+      }
     }
     KB_STAMP(ctl, 9);
     // ---- set records: full, or the sets containing a touched broker
@@ -1573,7 +1681,19 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
         const int rem = a.nsets - w * 32;                 // only bits of existing sets
         s_smark[w] = full ? (rem >= 32 ? 0xFFFFFFFFu : (1u << rem) - 1u) : 0u;
     }
-    if (!full) {
+    if (!full && a.sb_lds) {
+        // resident words: a set is marked when it holds a touched broker
+        __syncthreads();
+        for (int set = tid; set < a.nsets; set += STEP_THREADS) {
+            const uint64_t* sb = s_sb + (size_t)set * a.W64;
+            bool hit = false;
+            for (int x = 0; x < nT; x++) {
+                const int t = s_T[x];
+                hit |= (sb[t >> 6] >> (t & 63)) & 1ull;
+            }
+            if (hit) atomicOr(&s_smark[set >> 5], 1u << (set & 31));
+        }
+    } else if (!full) {
         // two memory round trips: the touched brokers' set-list extents, then the lists
         __shared__ int s_bo[TMAX + 1], s_bb[TMAX];
         if (tid < nT) {
@@ -1586,8 +1706,7 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
         if (wid == 0) {
             const int c = lane < nT ? s_bo[lane] : 0;
             int incl = c;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) { const int y = __shfl_up(incl, o); if (lane >= o) incl += y; }
+            incl = wave_incl_scan(incl);
             if (lane < nT) s_bo[lane] = incl - c;
             if (lane == nT - 1) s_bo[nT] = incl;
             if (nT == 0 && lane == 0) s_bo[0] = 0;
@@ -1604,13 +1723,15 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
     __syncthreads();
     KB_STAMP(ctl, 16);
     {
-        // marked sets in chunks: their allowed-set words staged in LDS (one round trip
-        // per chunk; the dedup table is free here), then one wave per set
-        unsigned long long* s_stage = s_wb;               // [CH * W64]
+        // marked sets in chunks of the compact list (allowed-set words resident in LDS,
+        // or staged per chunk: one round trip); each wave rebuilds four records at a
+        // time so their LDS chains overlap
+        constexpr int G = 4;
+        uint64_t* s_stage = (uint64_t*)s_wb;               // [CH * W64] (dedup table: free here)
         int* s_mlist = (int*)s_it;                         // [CH]
         __shared__ int s_mn, s_cursor;
         const int W64 = a.W64, KR = a.KR;
-        const int CH = DEDUP_STEP / W64;                   // >= 32 (W64 <= 64)
+        const int CH = a.sb_lds ? 2 * DEDUP_STEP : DEDUP_STEP / W64;   // >= 32
         const int nwords = (a.nsets + 31) / 32;
         const unsigned long long lt = (1ull << lane) - 1ull;
         if (tid == 0) s_cursor = 0;
@@ -1624,8 +1745,7 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
                     const uint32_t bits = ww < nwords ? s_smark[ww] : 0u;
                     const int c = __popc(bits);
                     int incl = c;
-#pragma unroll
-                    for (int o = 1; o < 64; o <<= 1) { const int y = __shfl_up(incl, o); if (lane >= o) incl += y; }
+                    incl = wave_incl_scan(incl);
                     const bool fits = ww < nwords && n + incl <= CH;
                     const int nfit = (int)__popcll(__ballot(fits));       // a prefix of the lanes
                     if (fits) {
@@ -1639,36 +1759,65 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
                 if (lane == 0) { s_mn = n; s_cursor = w; }
             }
             __syncthreads();
+            KB_STAMP(ctl, 19);
             const int mn = s_mn;
-            for (int q = tid; q < mn * W64; q += STEP_THREADS) {
-                const int i = q / W64, wd = q - i * W64;
-                s_stage[q] = a.setbits[(size_t)s_mlist[i] * W64 + wd];
-            }
-            __syncthreads();
-            for (int i = wid; i < mn; i += NW) {
-                const int set = s_mlist[i];
-                const unsigned long long* sb = s_stage + (size_t)i * W64;
-                uint16_t* rec16 = (uint16_t*)(a.setrec + (size_t)set * a.units);
-                // the first KR brokers of set ∩ bl_move in bl order (move targets, steps.go:192-201)
-                int found = 0;
-                for (int base = 0; base < B && found < KR; base += 64) {
-                    const int k = base + lane;
-                    const int b = k < B ? s_ord[k] : 0;
-                    const bool mem = k < B && ((sb[b >> 6] >> (b & 63)) & 1ull) && ((s_blmb[b >> 6] >> (b & 63)) & 1ull);
-                    const unsigned long long m = __ballot(mem);
-                    if (mem) {
-                        const int rk = found + (int)__popcll(m & lt);
-                        if (rk < KR) rec16[2 + rk] = (uint16_t)b;
-                    }
-                    found += (int)__popcll(m);
+            if (!a.sb_lds) {
+                for (int q = tid; q < mn * W64; q += STEP_THREADS) {
+                    const int i = q / W64, wd = q - i * W64;
+                    s_stage[q] = a.setbits[(size_t)s_mlist[i] * W64 + wd];
                 }
-                for (int rk = found + lane; rk < KR; rk += 64) rec16[2 + rk] = NONE16;
-                if (lane == 0) rec16[1] = (uint16_t)(found < KR ? found : KR);
-                int n = lane < W64 ? (int)__popcll(sb[lane] & s_blmb[lane]) : 0;
-                n = wave_sum(n);
-                if (lane == 0) rec16[0] = (uint16_t)n;
+                __syncthreads();
+            }
+            for (int g = wid * G; g < mn; g += NW * G) {
+                const int ng = mn - g < G ? mn - g : G;
+                const uint64_t* sb[G];
+                uint16_t* rec16[G];
+                int found[G];
+#pragma unroll
+                for (int j = 0; j < G; j++) {
+                    const int jj = j < ng ? j : 0;
+                    const int set = s_mlist[g + jj];
+                    sb[j] = a.sb_lds ? s_sb + (size_t)set * W64 : s_stage + (size_t)(g + jj) * W64;
+                    rec16[j] = (uint16_t*)(a.setrec + (size_t)set * a.units);
+                    found[j] = j < ng ? 0 : KR;
+                }
+                // the first KR brokers of set ∩ bl_move in bl order (move targets, steps.go:192-201)
+                for (int base = 0; base < B; base += 64) {
+                    bool need = false;
+#pragma unroll
+                    for (int j = 0; j < G; j++) need |= found[j] < KR;
+                    if (!need) break;
+                    const int k = base + lane;
+                    const int b = s_ord[k < B ? k : 0];
+                    // every word read unconditionally: one LDS round trip for all of them
+                    uint64_t wj[G];
+#pragma unroll
+                    for (int j = 0; j < G; j++) wj[j] = sb[j][b >> 6];
+                    const uint64_t wb = s_blmb[b >> 6];
+                    const bool inb = k < B && ((wb >> (b & 63)) & 1ull);
+#pragma unroll
+                    for (int j = 0; j < G; j++) {
+                        const bool mem = inb && ((wj[j] >> (b & 63)) & 1ull);
+                        const unsigned long long m = __ballot(mem);
+                        if (mem && found[j] < KR) {
+                            const int rk = found[j] + (int)__popcll(m & lt);
+                            if (rk < KR) rec16[j][2 + rk] = (uint16_t)b;
+                        }
+                        found[j] += (int)__popcll(m);
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < G; j++) {
+                    if (j >= ng) break;
+                    for (int rk = found[j] + lane; rk < KR; rk += 64) rec16[j][2 + rk] = NONE16;
+                    if (lane == 0) rec16[j][1] = (uint16_t)(found[j] < KR ? found[j] : KR);
+                    int n = lane < W64 ? (int)__popcll(sb[j][lane] & s_blmb[lane]) : 0;
+                    n = wave_sum(n);
+                    if (lane == 0) rec16[j][0] = (uint16_t)n;
+                }
             }
             __syncthreads();
+            KB_STAMP(ctl, 20);
         }
     }
     if (tid == 0) { C.prepped = 1; C.full_prep = 0; }
@@ -1812,16 +1961,22 @@ __global__ __launch_bounds__(1024) void k_summary(SumArgs a) {
                 if (c.s >= 0 && myenc[k] == s_benc[k] && enc(cont_delta(a.r, c, inv_avg)) == s_benc[k])
                     atomicMin(&s_brec[k], (uint32_t)i);
             }
+    __shared__ uint32_t s_nkk[2];
+    if (tid < 2) s_nkk[tid] = 0;
+    __syncthreads();
     for (int h = tid; h < DEDUP_STEP; h += 1024) {
         if (s_key[h] == NONE32) continue;
         const uint32_t k = atomicAdd(&s_n, 1u);
+        atomicAdd(&s_nkk[s_key[h] >> 30], 1u);
         if (k < (uint32_t)SUMMARY_KEYS) okeys[k] = dedup_entry(T, h);
     }
     __syncthreads();
     if (tid == 0) {
         out->nkeys = s_n < (uint32_t)SUMMARY_KEYS ? s_n : (uint32_t)SUMMARY_KEYS;
         out->flags = ((ran && ctl->cont_overflow) || s_fail || s_n > (uint32_t)SUMMARY_KEYS) ? 1u : 0u;
-        out->ran = ran ? 1u : 0u;
+        if (ran) out->flags |= 2u;
+        out->nkk[0] = (uint16_t)min(s_nkk[0], 0xFFFFu);
+        out->nkk[1] = (uint16_t)min(s_nkk[1], 0xFFFFu);
         uint32_t m = 0;
         for (int q = 0; q < NF; q++) m |= s_f[q] != NONE32 ? 1u << q : 0u;
         out->fmask = m;
@@ -1876,8 +2031,27 @@ int scan_blocks_per_cu(int rc, bool lds_sets, size_t lds) {
     }
 }
 
+__global__ __launch_bounds__(1024) void k_touch(double* r, int B, int32_t* blm, int32_t* posm, uint4* setrec, int nrec) {
+    for (int i = threadIdx.x; i < B; i += 1024) {
+        const double x = r[i]; const int32_t y = blm[i], z = posm[i];
+        __syncthreads();
+        r[i] = x; blm[i] = y; posm[i] = z;
+    }
+    for (int i = threadIdx.x; i < nrec; i += 1024) { const uint4 v = setrec[i]; __syncthreads(); setrec[i] = v; }
+}
+
+void launch_touch(double* r, int B, int32_t* blm, int32_t* posm, uint4* setrec, int nrec, hipStream_t st) {
+    hipLaunchKernelGGL(k_touch, dim3(1), dim3(1024), 0, st, r, B, blm, posm, setrec, nrec);
+}
+
+int step_static_lds() {
+    hipFuncAttributes fa;
+    if (hipFuncGetAttributes(&fa, (const void*)k_step) != hipSuccess) return -1;
+    return (int)fa.sharedSizeBytes;
+}
+
 void launch_step(const StepArgs& a, hipStream_t st) {
-    hipLaunchKernelGGL(k_step, dim3(1), dim3(STEP_THREADS), 0, st, a);
+    hipLaunchKernelGGL(k_step, dim3(1), dim3(STEP_THREADS), a.lds_bytes, st, a);
 }
 void launch_listop(DevCtl* ctl, const Lists& L, hipStream_t st) {
     hipLaunchKernelGGL(k_listop, dim3(1), dim3(1024), 0, st, ctl, L);

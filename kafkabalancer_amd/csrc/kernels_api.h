@@ -45,6 +45,8 @@ struct StepArgs {
     const int32_t* nc;        // NumConsumers
     long long Ppad;
     int RC, KR, K, units, W64, B, nsets, NP2;
+    int sb_lds;               // 1: every set's allowed-set words are staged in LDS
+    int lds_bytes;            // dynamic LDS (step_lds(B, NP2, sb_lds ? nsets * W64 : 0).total)
     const uint64_t* setbits;
     uint4* setrec;
     int32_t* order;           // [B] universe sorted by (load, id)
@@ -96,6 +98,9 @@ struct SumArgs {
 void launch_scan(const ScanArgs& a, int rc, bool lds_sets, size_t lds_bytes, hipStream_t st);
 int scan_blocks_per_cu(int rc, bool lds_sets, size_t lds_bytes);
 void launch_step(const StepArgs& a, hipStream_t st);
+int step_static_lds();
+// diagnostic: one workgroup rewrites the given tables in place (n = 0: nothing)
+void launch_touch(double* r, int B, int32_t* blm, int32_t* posm, uint4* setrec, int nrec, hipStream_t st);
 void launch_listop(DevCtl* ctl, const Lists& L, hipStream_t st);
 void launch_refresh(const RefreshArgs& a, hipStream_t st);
 void launch_summary(const SumArgs& a, hipStream_t st);

@@ -75,4 +75,16 @@ __device__ __forceinline__ T wave_red_max(T v) { return wave_reduce(v, [](T a, T
 template <typename T>
 __device__ __forceinline__ T wave_red_or(T v) { return wave_reduce(v, [](T a, T b) { return a | b; }); }
 
+// inclusive prefix sum over the 64 lanes (lane i: lanes 0..i): Hillis-Steele
+// row_shr steps within the 16-lane rows, then the row totals via row_bcast
+__device__ __forceinline__ int wave_incl_scan(int v) {
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, true);   // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, true);   // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, true);   // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, true);   // row_shr:8
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
+    return v;
+}
+
 }  // namespace kbe

@@ -23,7 +23,7 @@ KIND_NAMES = {0: "none", 1: "replace", 2: "remove", 3: "add", 4: "swap"}
 
 EXPORTS = ["kb_abi_version", "kb_engine_create", "kb_engine_balance", "kb_engine_plan",
            "kb_engine_replicas", "kb_engine_loads", "kb_engine_unbalance", "kb_engine_stats",
-           "kb_engine_timings", "kb_engine_stamps", "kb_engine_bench_scan",
+           "kb_engine_timings", "kb_engine_set_timing", "kb_engine_stamps", "kb_engine_bench_scan",
            "kb_engine_last_error", "kb_engine_destroy", "kb_engine_summary_bytes",
            "kb_engine_step_begin", "kb_engine_step_finish", "kb_engine_set_stream"]
 
@@ -90,6 +90,8 @@ def lib():
         L.kb_engine_stats.restype = C.c_int
         L.kb_engine_timings.argtypes = [vp, PD, P64, C.c_int]
         L.kb_engine_timings.restype = C.c_int
+        L.kb_engine_set_timing.argtypes = [vp, C.c_int32]
+        L.kb_engine_set_timing.restype = C.c_int
         L.kb_engine_stamps.argtypes = [vp, P64, C.c_int]
         L.kb_engine_stamps.restype = C.c_int
         L.kb_engine_bench_scan.argtypes = [vp, C.c_int, PD]
@@ -303,6 +305,12 @@ class Engine:
         n = np.zeros(3, np.int64)
         lib().kb_engine_timings(self.h, ms.ctypes.data_as(PD), n.ctypes.data_as(P64), 3)
         return {k: (float(ms[i]), int(n[i])) for i, k in enumerate(self.KERNELS)}
+
+    def set_timing(self, on):
+        """Per-kernel HIP events on/off for the following plans (resets the sums)."""
+        rc = lib().kb_engine_set_timing(self.h, int(bool(on)))
+        if rc != 0:
+            raise EngineError(rc, self.last_error())
 
     def stamps(self):
         """Diagnostic build only: accumulated phase ticks (100 MHz) of the k_step phases."""
