@@ -507,6 +507,8 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
     memset(&z, 0, sizeof z);
     z.logcap = e->logcap;
     z.full_prep = 1;
+    z.tk_on = e->time_kernels;
+    z.ts_beg = NONE64;
     HIPCHK(hipMemcpy(e->ctl, &z, sizeof z, hipMemcpyHostToDevice));
     HIPCHK(hipEventCreate(&e->ev0));
     HIPCHK(hipEventCreate(&e->ev1));
@@ -551,6 +553,7 @@ static const int kStepBatch = 64;
 
 static void mark(kb_engine* e, int kind_next) {
     if (!e->time_kernels) return;
+    if (kind_next == TK_SCAN || kind_next == TK_STEP) return;   // device-clock timed (no events between them)
     if (e->tev.empty()) {
         e->tev.resize((size_t)kStepBatch * 2 + 8);
         e->tkind.resize(e->tev.size());
@@ -840,11 +843,23 @@ extern "C" int kb_engine_stats(kb_engine* e, kb_stats* o) {
     return KB_OK;
 }
 
+// k_step / k_scan durations come from the device clock (100 MHz): each scan workgroup
+// stamps its start and end, k_step folds the scan's interval and its own into
+// ctl->tk_*; k_refresh (rare) is timed with events around its launches
 extern "C" int kb_engine_timings(kb_engine* e, double* ms, int64_t* launches, int n) {
     if (!e) return KB_ERR_INVALID;
+    DevCtl c;
+    HIPCHK(hipStreamSynchronize(e->st));
+    HIPCHK(hipMemcpy(&c, e->ctl, sizeof c, hipMemcpyDeviceToHost));
+    const double tick_ms = 1e-5;
+    double kms[TK_N];
+    int64_t kn[TK_N];
+    for (int k = 0; k < TK_N; k++) { kms[k] = e->kms[k]; kn[k] = e->klaunch[k]; }
+    kms[TK_STEP] = (double)c.tk_sum[1] * tick_ms; kn[TK_STEP] = (int64_t)c.tk_n[1];
+    kms[TK_SCAN] = (double)c.tk_sum[0] * tick_ms; kn[TK_SCAN] = (int64_t)c.tk_n[0];
     for (int k = 0; k < TK_N && k < n; k++) {
-        if (ms) ms[k] = e->kms[k];
-        if (launches) launches[k] = e->klaunch[k];
+        if (ms) ms[k] = kms[k];
+        if (launches) launches[k] = kn[k];
     }
     return TK_N;
 }
@@ -855,6 +870,14 @@ extern "C" int kb_engine_set_timing(kb_engine* e, int32_t on) {
     e->tev_used = 0;
     for (int k = 0; k < TK_N; k++) { e->kms[k] = 0; e->klaunch[k] = 0; }
     e->time_kernels = on ? 1 : 0;
+    DevCtl c;
+    HIPCHK(hipMemcpy(&c, e->ctl, sizeof c, hipMemcpyDeviceToHost));
+    c.tk_on = e->time_kernels;
+    c.tk_sum[0] = c.tk_sum[1] = c.tk_n[0] = c.tk_n[1] = 0;
+    c.ts_beg = NONE64;
+    c.ts_end = 0;
+    HIPCHK(hipMemcpy(e->ctl, &c, sizeof c, hipMemcpyHostToDevice));
+    *e->h_ctl = c;
     return KB_OK;
 }
 

@@ -153,9 +153,16 @@ struct DevCtl {
     int32_t pl_kind, pl_from, pl_to, pl_pad;  // pending per-broker list operation
     long long pl_part;
     unsigned long long total_cand, total_cont, total_folds, total_exact_halts;
+    // kernel timing (tk_on): summed device-clock durations (100 MHz ticks) and launch
+    // counts, {k_scan, k_step}; k_step folds in the scan's interval below
+    unsigned long long tk_sum[2], tk_n[2];
+    int32_t tk_on, tk_pad;
     // diagnostic phase stamps (builds with -DKB_STAMPS): accumulated
     // wall_clock64 ticks (100 MHz) per phase of k_step
     unsigned long long stamps[32];
+    // the running scan's interval: earliest workgroup start, latest end (atomics;
+    // outside the block k_step copies to LDS and back)
+    unsigned long long ts_beg, ts_end;
 };
 
 #ifdef KB_STAMPS

@@ -400,6 +400,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
     constexpr int U = sr_units(RC);
     constexpr int NW = SCAN_THREADS / 64;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const unsigned long long t_in = wall_clock64();
 
     double2* s_rf = (double2*)smem;                 // (r, f(r)) per broker
     const size_t rbytes = (size_t)a.B * 16;
@@ -437,6 +438,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
     const double inv_avg = ctl->inv_avg, eps = ctl->eps;
     const double ubL = ctl->ub[0], ubN = ctl->ub[1];
     const int heavy = ctl->heavy, nblm = ctl->nblm;
+    const bool tk_on = ctl->tk_on != 0;
     __syncthreads();
     if (!run || (a.dbg & 4)) return;
 
@@ -681,6 +683,10 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
 #pragma unroll
             for (int f = 0; f < NF; f++) fo[f] = fst[f];
         }
+        if (tk_on) {                                   // the scan's interval (kernel timing)
+            atomicMin(&ctl->ts_beg, t_in);
+            atomicMax(&ctl->ts_end, wall_clock64());
+        }
       }
     }
 }
@@ -745,10 +751,21 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     constexpr int NW = STEP_THREADS / 64;
     __shared__ DevCtl C;
+    const unsigned long long t_in = wall_clock64();
     KB_STAMP_BEGIN();
     if (tid < CTL_WORDS) ((uint32_t*)&C)[tid] = ((const uint32_t*)ctl)[tid];
     auto write_back = [&]() {
         KB_STAMP_FLUSH(ctl);
+        __syncthreads();
+        if (tid == 0 && C.tk_on) {
+            // kernel timing: this launch, and the scan that ran before it (if any)
+            C.tk_sum[1] += wall_clock64() - t_in;
+            C.tk_n[1]++;
+            const unsigned long long b = ctl->ts_beg, e = ctl->ts_end;
+            if (b != NONE64 && e > b) { C.tk_sum[0] += e - b; C.tk_n[0]++; }
+            ctl->ts_beg = NONE64;
+            ctl->ts_end = 0;
+        }
         __syncthreads();
         if (tid < CTL_WORDS) ((uint32_t*)ctl)[tid] = ((const uint32_t*)&C)[tid];
     };
