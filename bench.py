@@ -57,6 +57,15 @@ def cpu_baseline(cl, cfg, seconds=12.0):
                       "(reference Go not buildable: no Go toolchain)" % (k, P, n, dt)}
 
 
+def pmc_traffic(kernel):
+    """HBM-side bytes per launch from the committed rocprofv3 PMC passes (tools/pmc_bench.sh)."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "pmc_traffic.json")) as f:
+            return json.load(f)[kernel]["traffic_bytes_per_launch"]
+    except (OSError, KeyError, ValueError):
+        return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -126,9 +135,11 @@ def main():
         "data": "synthetic (numpy PCG64 seed 0x5EED0003), Zipf weights r^-1.1",
         "config": dict(desc, parallelism="single-gpu", device_ms_per_step=1e3 * dev_s / max(steps, 1)),
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic("k_scan"),
                      "kernel": "k_scan", "bytes_per_launch": bytes_scan,
-                     "avg_launch_us": scan_avg_us},
+                     "avg_launch_us": scan_avg_us,
+                     "timing": "device clock: earliest workgroup start to latest workgroup end, every launch",
+                     "traffic_source": "profiles/pmc_traffic.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE per launch)"},
         "kernels_us_per_step": {k: 1e3 * v[0] / max(v[1], 1) for k, v in tk.items()},
         "kernel_timing_steps": kt_steps,
     }
