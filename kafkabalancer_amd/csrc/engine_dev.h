@@ -171,7 +171,8 @@ struct DevCtl {
 #define KB_STAMP_BEGIN()                                                        \
     __shared__ unsigned long long _kb_st[32];                                   \
     if (threadIdx.x < 32) _kb_st[threadIdx.x] = 0;                              \
-    unsigned long long _kb_t0 = wall_clock64()
+    unsigned long long _kb_t0 = wall_clock64();                                 \
+    const unsigned long long _kb_r0 = _kb_t0, _kb_c0 = clock64()
 #define KB_STAMP(ctl, i)                                                        \
     do {                                                                        \
         __syncthreads();                                                        \
@@ -183,6 +184,11 @@ struct DevCtl {
     } while (0)
 #define KB_STAMP_FLUSH(ctl)                                                     \
     do {                                                                        \
+        __syncthreads();                                                        \
+        if (threadIdx.x == 0) {                                                 \
+            _kb_st[24] += wall_clock64() - _kb_r0;                              \
+            _kb_st[25] += clock64() - _kb_c0;                                   \
+        }                                                                       \
         __syncthreads();                                                        \
         if (threadIdx.x < 32 && _kb_st[threadIdx.x])                            \
             atomicAdd(&(ctl)->stamps[threadIdx.x], _kb_st[threadIdx.x]);        \

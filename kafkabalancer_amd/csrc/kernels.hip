@@ -1798,29 +1798,46 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
                     rec16[j] = (uint16_t*)(a.setrec + (size_t)set * a.units);
                     found[j] = j < ng ? 0 : KR;
                 }
-                // the first KR brokers of set ∩ bl_move in bl order (move targets, steps.go:192-201)
-                for (int base = 0; base < B; base += 64) {
+                // the first KR brokers of set ∩ bl_move in bl order (move targets, steps.go:192-201);
+                // PP positions per lane and iteration (one iteration almost always suffices)
+#ifndef KB_SET_PP
+#define KB_SET_PP 1
+#endif
+                constexpr int PP = KB_SET_PP;
+                for (int base = 0; base < B; base += 64 * PP) {
                     bool need = false;
 #pragma unroll
                     for (int j = 0; j < G; j++) need |= found[j] < KR;
                     if (!need) break;
-                    const int k = base + lane;
-                    const int b = s_ord[k < B ? k : 0];
                     // every word read unconditionally: one LDS round trip for all of them
-                    uint64_t wj[G];
+                    int bq[PP];
+                    bool inb[PP];
+                    uint64_t wj[PP][G];
 #pragma unroll
-                    for (int j = 0; j < G; j++) wj[j] = sb[j][b >> 6];
-                    const uint64_t wb = s_blmb[b >> 6];
-                    const bool inb = k < B && ((wb >> (b & 63)) & 1ull);
+                    for (int q = 0; q < PP; q++) {
+                        const int k = base + q * 64 + lane;
+                        bq[q] = s_ord[k < B ? k : 0];
+                    }
+#pragma unroll
+                    for (int q = 0; q < PP; q++) {
+                        const int b = bq[q];
+                        inb[q] = base + q * 64 + lane < B && ((s_blmb[b >> 6] >> (b & 63)) & 1ull);
+#pragma unroll
+                        for (int j = 0; j < G; j++) wj[q][j] = sb[j][b >> 6];
+                    }
 #pragma unroll
                     for (int j = 0; j < G; j++) {
-                        const bool mem = inb && ((wj[j] >> (b & 63)) & 1ull);
-                        const unsigned long long m = __ballot(mem);
-                        if (mem && found[j] < KR) {
-                            const int rk = found[j] + (int)__popcll(m & lt);
-                            if (rk < KR) rec16[j][2 + rk] = (uint16_t)b;
+#pragma unroll
+                        for (int q = 0; q < PP; q++) {
+                            const int b = bq[q];
+                            const bool mem = inb[q] && ((wj[q][j] >> (b & 63)) & 1ull);
+                            const unsigned long long m = __ballot(mem);
+                            if (mem && found[j] < KR) {
+                                const int rk = found[j] + (int)__popcll(m & lt);
+                                if (rk < KR) rec16[j][2 + rk] = (uint16_t)b;
+                            }
+                            found[j] += (int)__popcll(m);
                         }
-                        found[j] += (int)__popcll(m);
                     }
                 }
 #pragma unroll
