@@ -145,10 +145,10 @@ def main():
     }
     if args.stamps:
         st = eng.stamps()
-        n = max(1, st1["steps"])
+        n = max(1, eng.stats()["steps"])       # every step since the engine was created
         names = ["prep.S+r+ubloop", "step.loads", "res.reduce", "res.pred", "res.move", "res.apply(tail)", "prep.sort", None,
                  "prep.blm+cert", "prep.reduce+eps", "prep.sets", "res.move->apply", "loads.bro+ctl", "loads.rec_reduce", "loads.keys", None, "sets.mark", "eps.sync1", "eps.wave0red", "sets.list", "sets.build", "keys.pre", "keys.insert"]
-        counts = {"keys_needed": 26, "emits": 31, "spills": 30, "walks": 29, "walk_steps": 28, "walk_global": 27}
+        counts = {"waves_scored": 7, "waves_gated_in": 15, "emits": 31, "spills": 30, "walks": 29, "walk_steps": 28, "walk_global": 27}
         print(json.dumps({"k_step_clock_mhz": 100.0 * st[25] / max(st[24], 1),
                           "k_step_us": st[24] / 100.0 / n,
                           "stamps_us_per_step": {k: st[i] / 100.0 / n for i, k in enumerate(names) if k},

@@ -11,7 +11,10 @@ constexpr int SCAN_THREADS = 1024;  // k_scan workgroup (one per CU)
 constexpr int PER_LANE = 2;         // consecutive partitions per lane (vector loads)
 constexpr int TILE = SCAN_THREADS * PER_LANE;   // 2048 partitions per scan tile
 constexpr int SHARD_ALIGN = 1024;   // shard boundaries (multi-GPU) are multiples of this
-constexpr int STEP_THREADS = 1024;  // k_step: one workgroup
+#ifndef KB_STEP_THREADS
+#define KB_STEP_THREADS 1024
+#endif
+constexpr int STEP_THREADS = KB_STEP_THREADS;  // k_step: one workgroup
 constexpr uint32_t NONE32 = 0xFFFFFFFFu;
 constexpr unsigned long long NONE64 = ~0ull;
 constexpr uint16_t NONE16 = 0xFFFFu;

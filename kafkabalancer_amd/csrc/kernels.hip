@@ -268,6 +268,13 @@ __device__ void do_list_op(DevCtl* ctl, const Lists& L, int* s_i) {
 }
 
 // --------------------------------------------------------------- k_scan
+// census event counters (stamps build with -DKB_WALK_COUNTS only: their global atomics
+// distort the census timing)
+#ifdef KB_WALK_COUNTS
+#define KB_COUNT_WALK(ctl, i, v) KB_COUNT(ctl, i, v)
+#else
+#define KB_COUNT_WALK(ctl, i, v) (void)0
+#endif
 
 static_assert(PER_LANE == 2, "the scan's register layout assumes two partitions per lane");
 
@@ -301,9 +308,9 @@ __device__ __forceinline__ void emit_global(DevCtl* ctl, Contender* cont, uint32
 
 __device__ __forceinline__ void emit(const ScanArgs& a, const Dedup& T, int kind, int s, int t, double w,
                                      unsigned long long iter) {
-    KB_COUNT(a.ctl, 31, 1);
+    KB_COUNT_WALK(a.ctl, 31, 1);
     if (dedup_insert(T, kind, s, t, w, iter) < 0) {   // table full or weight conflict: spill it raw
-        KB_COUNT(a.ctl, 30, 1);
+        KB_COUNT_WALK(a.ctl, 30, 1);
         Contender c;
         c.s = s; c.t = t; c.w = w; c.iter = iter; c.kind = kind; c.pad = 0;
         emit_global(a.ctl, a.cont, a.cont_cap, c);
@@ -323,10 +330,10 @@ __device__ void walk_targets(const ScanArgs& a, const Dedup& T, const double2* s
     const double delta = w * inv_avg;
     const int nl = rec16[1];
     int last = -1;
-    KB_COUNT(a.ctl, 29, 1);
+    KB_COUNT_WALK(a.ctl, 29, 1);
     for (int i = 0; i < nl; i++) {                // the set's first KR eligible brokers
         const int b = rec16[2 + i];
-        KB_COUNT(a.ctl, 28, 1);
+        KB_COUNT_WALK(a.ctl, 28, 1);
         last = b;
         bool isrep = false;
 #pragma unroll
@@ -339,7 +346,7 @@ __device__ void walk_targets(const ScanArgs& a, const Dedup& T, const double2* s
     if (nl < KR || last < 0) return;              // the set is exhausted
     const uint64_t* sb = a.setbits + (size_t)set * a.W64;
     for (int k = s_pos[last] + 1; k < nblm; k++) {   // rare: more than KR near-tied targets
-        KB_COUNT(a.ctl, 27, 1);
+        KB_COUNT_WALK(a.ctl, 27, 1);
         const int b = s_blm[k];
         if (!setbit(sb, b)) continue;
         bool isrep = false;
@@ -540,6 +547,12 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
         const double tL = wave_min(lL), tN = wave_min(lN);
         const bool hasL = tL < HUGE_VAL && tL <= ubL + 12.0 * eps;
         const bool hasN = tN < HUGE_VAL && tN <= ubN + 12.0 * eps;
+#ifdef KB_WALK_COUNTS
+        if (lane == 0) {
+            KB_COUNT(a.ctl, 7, 1);                                  // waves scored
+            if (hasL || hasN) KB_COUNT(a.ctl, 15, 1);               // waves past the ub gate
+        }
+#endif
         if (!(a.dbg & 1) && ((hasL && lL <= tL + 8.0 * eps) || (hasN && lN <= tN + 8.0 * eps))) {
             // the (partition, slot) pairs within 8*eps of the wave minimum, as bits j*16 + slot
             uint32_t todo = 0;
@@ -940,7 +953,7 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
             s_nd[tid] = s_sok[tid] ? 1 : 0;          // resolve takes s_single (s_li == -2)
             s_li[tid] = -2;
         }
-        if (tid == 0 && (need0 || need1)) KB_COUNT(ctl, 26, 1);
+
         for (int i = tid; (need0 || need1) && i < a.R.n; i += STEP_THREADS) {
             const RecHdr* h = a.R.h(i);
             const bool q0 = need0 && h->dmin[0] <= g0 + 8.0 * eps, q1 = need1 && h->dmin[1] <= g1 + 8.0 * eps;
