@@ -1481,6 +1481,217 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
     // (next step): getBL's (load, id) order, bl_move, relative loads, eps, sets
     const bool full = C.full_prep != 0;
     const int nT = s_nT;
+    bool marked = false;                              // sets already marked (fused path)
+    if (!full && a.sb_lds) {
+        // ---- fused incremental prep: the order-independent work (S, E, r, U0, eps, the
+        // upper bound, the set marks) rides along with the re-sort's phases, so the
+        // whole prep takes six barriers
+        const bool srt = nT > 0;
+        constexpr int NQ = (MAXB + STEP_THREADS - 1) / STEP_THREADS;
+        __shared__ double s_fq[2][NW], s_fq2[5][NW];     // F1 / F2 wave partials (distinct: no overwrite race)
+        __shared__ int s_fcnt[NW];
+        __shared__ int s_fwc[NW];
+        // F1: touched marks; S, E and |bl_move| partials; clears; best keys issued
+        if (srt && tid < nT) { s_fl[s_T[tid]] |= BF_TOUCHED; s_cntT[tid] = 0; }
+        for (int w = tid; w < MAXB / 64; w += STEP_THREADS) { s_blmb[w] = 0; s_presb[w] = 0; }
+        for (int w = tid; w < (a.nsets + 31) / 32; w += STEP_THREADS) s_smark[w] = 0u;
+        if (tid == 0) s_unc = 0;
+        const bool bkeys = do_res && tid < a.R.n;
+        Contender bk0, bk1;
+        bk0.s = bk1.s = -1;
+        if (bkeys) { bk0 = a.R.h(tid)->best[0]; bk1 = a.R.h(tid)->best[1]; }
+        {
+            double sS = 0.0, sE = 0.0;
+            int cn = 0;
+            for (int b = tid; b < B; b += STEP_THREADS)
+                if (s_fl[b] & (BF_PRESENT | BF_INCFG)) { sS += s_ld[b]; sE += s_e[b]; cn++; }
+            sS = wave_sum(sS); sE = wave_sum(sE); cn = wave_sum(cn);
+            if (lane == 0) { s_fq[0][wid] = sS; s_fq[1][wid] = sE; s_fcnt[wid] = cn; }
+        }
+        __syncthreads();
+        // F2: touched old positions; S, avg, r, U0/V/Rm partials; upper bound partials; set marks
+        if (srt)
+            for (int i = tid; i < B; i += STEP_THREADS) {
+                const int b = s_ord[i];
+                if (s_fl[b] & BF_TOUCHED)
+                    for (int x = 0; x < nT; x++) if (s_T[x] == b) s_posT[x] = i;
+            }
+        const double S = wave_sum(lane < NW ? s_fq[0][lane] : 0.0), E = wave_sum(lane < NW ? s_fq[1][lane] : 0.0);
+        const int nblm = wave_sum(lane < NW ? s_fcnt[lane] : 0);
+        const double avg = S / (double)nblm;
+        const double iav = 1.0 / avg;
+        {
+            double su = 0.0, v = 0.0, rm = 0.0;
+            for (int b = tid; b < B; b += STEP_THREADS) {
+                double r = 0.0;
+                if (s_fl[b] & (BF_PRESENT | BF_INCFG)) {
+                    r = rel_ld(s_ld, b, iav);
+                    su += fsq(r);
+                    const double ar = fabs(r);
+                    v += ar * (1.0 + ar);
+                    rm = ar > rm ? ar : rm;
+                }
+                a.r[b] = r;
+            }
+            // upper bound of the next step's minimum per kind: the best keys of the scan
+            // just resolved whose partition and brokers the applied move did not touch
+            // are still candidates; re-scored on the new loads they bound the new minimum
+            double ub0 = HUGE_VAL, ub1 = HUGE_VAL;
+            if (bkeys) {
+                const long long pm = s_moved;
+#pragma unroll
+                for (int k = 0; k < 2; k++) {
+                    const Contender& c = k ? bk1 : bk0;
+                    if (c.s < 0 || (long long)(c.iter >> 21) == pm) continue;
+                    if ((s_fl[c.s] | s_fl[c.t]) & BF_TOUCHED) continue;
+                    const double d = cont_delta_ld(s_ld, c, iav);
+                    if (k == 0) ub0 = d < ub0 ? d : ub0;
+                    else ub1 = d < ub1 ? d : ub1;
+                }
+            }
+            su = wave_sum(su); v = wave_sum(v); rm = wave_max(rm);
+            ub0 = wave_min(ub0); ub1 = wave_min(ub1);
+            if (lane == 0) { s_fq2[0][wid] = su; s_fq2[1][wid] = v; s_fq2[2][wid] = rm; s_fq2[3][wid] = ub0; s_fq2[4][wid] = ub1; }
+        }
+        for (int set = tid; set < a.nsets; set += STEP_THREADS) {
+            // a set is marked when it holds a touched broker
+            const uint64_t* sb = s_sb + (size_t)set * a.W64;
+            bool hit = false;
+            for (int x = 0; x < nT; x++) {
+                const int t = s_T[x];
+                hit |= (sb[t >> 6] >> (t & 63)) & 1ull;
+            }
+            if (hit) atomicOr(&s_smark[set >> 5], 1u << (set & 31));
+        }
+        __syncthreads();
+        KB_STAMP(ctl, 6);
+        // F3: new positions of the untouched brokers; eps and the control block (wave 0)
+        int nb[NQ], np[NQ];
+        if (srt) {
+#pragma unroll
+            for (int q = 0; q < NQ; q++) {
+                nb[q] = -1;
+                if (q * STEP_THREADS >= B) continue;         // uniform
+                const int i = q * STEP_THREADS + tid;
+                const bool in = i < B;
+                const int b = in ? s_ord[i] : 0;
+                const bool untouched = in && !(s_fl[b] & BF_TOUCHED);
+                const double Lb = s_ld[b];
+                int below = 0, before = 0;
+                for (int x = 0; x < nT; x++) {
+                    const int t = s_T[x];
+                    const double Lt = s_ld[t];
+                    below += ((Lt < Lb) || (Lt == Lb && t < b)) ? 1 : 0;
+                    before += s_posT[x] < i ? 1 : 0;
+                    // count, for touched t, the untouched brokers below it
+                    const bool b_lt_t = untouched && ((Lb < Lt) || (Lb == Lt && b < t));
+                    const unsigned long long bal = __ballot(b_lt_t);
+                    if (lane == 0 && bal) atomicAdd(&s_cntT[x], (int)__popcll(bal));
+                }
+                nb[q] = untouched ? b : -1;
+                np[q] = i - before + below;
+            }
+        }
+        if (wid == 0) {
+            const bool in = lane < NW;
+            const double U0 = wave_sum(in ? s_fq2[0][lane] : 0.0), V = wave_sum(in ? s_fq2[1][lane] : 0.0);
+            const double Rm = wave_max(in ? s_fq2[2][lane] : 0.0);
+            const double ub0 = wave_min(in ? s_fq2[3][lane] : HUGE_VAL);
+            const double ub1 = wave_min(in ? s_fq2[4][lane] : HUGE_VAL);
+            if (lane == 0) {
+                const double u = DBL_EPSILON / 2;
+                const double n = (double)nblm;
+                const double R = Rm + a.wmax * iav;
+                const double Ea = E * iav;
+                double epsf = 64.0 * u * ((n + 8.0) * (U0 + 2.0 * V) + 4.0 * (1.0 + R) * (1.0 + R));
+                double epsl = 16.0 * Ea * (V / (n > 0 ? n : 1.0) + R + 1.0) + 4.0 * Ea * Ea;
+                double ep = epsf + epsl;
+                if (!(ep > 1e-300)) ep = 1e-300;
+                C.S = S; C.avg = avg; C.inv_avg = iav; C.U0 = U0;
+                C.V = V; C.eps = ep; C.E = E; C.nblm = nblm;
+                C.ub[0] = ub0; C.ub[1] = ub1;
+                C.want_refresh = (epsl > epsf || C.ndirty >= 256) ? 1 : 0;
+                C.ncont = 0;
+                C.cont_overflow = 0;
+            }
+        }
+        __syncthreads();
+        // F4: scatter into the new order
+        if (srt) {
+#pragma unroll
+            for (int q = 0; q < NQ; q++)
+                if (q * STEP_THREADS < B && nb[q] >= 0) s_ord[np[q]] = nb[q];
+            if (tid < nT) {
+                const int t = s_T[tid];
+                const double Lt = s_ld[t];
+                int rank = 0;
+                for (int x = 0; x < nT; x++) {
+                    const int t2 = s_T[x];
+                    const double L2 = s_ld[t2];
+                    rank += ((L2 < Lt) || (L2 == Lt && t2 < t)) ? 1 : 0;
+                }
+                s_ord[s_cntT[tid] + rank] = t;
+            }
+        }
+        __syncthreads();
+        KB_STAMP(ctl, 8);
+        // F5: bl_move = brokers present in the load map or listed in -broker-ids
+        // (steps.go:150-157): membership bits, order / position writes, order certification
+        constexpr int PT = MAXB / STEP_THREADS;          // universe positions per thread
+        int flag[PT], c = 0;
+        const int base = tid * PT;
+#pragma unroll
+        for (int q = 0; q < PT; q++) {
+            const int i = base + q;
+            flag[q] = 0;
+            if (i < B) {
+                const int b = s_ord[i];
+                const uint8_t fl = s_fl[b];
+                const bool pres = (fl & BF_PRESENT) != 0;
+                flag[q] = (fl & (BF_PRESENT | BF_INCFG)) ? 1 : 0;
+                if (flag[q]) atomicOr((unsigned long long*)&s_blmb[b >> 6], 1ull << (b & 63));
+                if (pres) atomicOr((unsigned long long*)&s_presb[b >> 6], 1ull << (b & 63));
+                c += flag[q];
+                a.order[i] = b;
+                a.posu[b] = i;
+                // with approximate loads, neighbours must be separated by more than
+                // their error bounds (else the exact order is unknown)
+                if (i + 1 < B) {
+                    const int b2 = s_ord[i + 1];
+                    const double e = s_e[b] + s_e[b2];
+                    if (e > 0.0 && !(s_ld[b2] - s_ld[b] > e)) s_unc = 1;
+                }
+            }
+        }
+        const int incl = wave_incl_scan(c);
+        if (lane == 63) s_fwc[wid] = incl;
+        __syncthreads();
+        // F6: bl_move positions; getBL's lightest / heaviest
+        {
+            const int wc = lane < NW ? s_fwc[lane] : 0;
+            const int woff = wave_sum(lane < wid ? wc : 0);
+            int pos = woff + incl - c;
+#pragma unroll
+            for (int q = 0; q < PT; q++) {
+                const int i = base + q;
+                if (i < B) {
+                    const int b = s_ord[i];
+                    if (flag[q]) {
+                        if (pos == 0) C.light = b;
+                        if (pos == nblm - 1) C.heavy = b;
+                        a.blm[pos] = b; a.posm[b] = pos; pos++;
+                    } else a.posm[b] = -1;
+                }
+            }
+            if (tid == 0 && nblm == 0) { C.light = -1; C.heavy = -1; }
+        }
+        if (s_unc) {
+            if (tid == 0) { C.halted = H_NEED_EXACT; C.prepped = 0; C.total_exact_halts++; }
+            write_back();
+            return;
+        }
+        marked = true;
+    } else {
     if (full) {
         // every load is exact here (fresh state or after k_refresh): s_e holds the sort keys
         unsigned long long* s_k64 = (unsigned long long*)s_e;
@@ -1705,13 +1916,16 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
         C.cont_overflow = 0;
       }
     }
+    }
     KB_STAMP(ctl, 9);
     // ---- set records: full, or the sets containing a touched broker
-    for (int w = tid; w < (a.nsets + 31) / 32; w += STEP_THREADS) {
+    for (int w = tid; !marked && w < (a.nsets + 31) / 32; w += STEP_THREADS) {
         const int rem = a.nsets - w * 32;                 // only bits of existing sets
         s_smark[w] = full ? (rem >= 32 ? 0xFFFFFFFFu : (1u << rem) - 1u) : 0u;
     }
-    if (!full && a.sb_lds) {
+    if (marked) {
+        // (marked by the fused prep)
+    } else if (!full && a.sb_lds) {
         // resident words: a set is marked when it holds a touched broker
         __syncthreads();
         for (int set = tid; set < a.nsets; set += STEP_THREADS) {
