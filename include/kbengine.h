@@ -200,6 +200,16 @@ int kb_engine_step_finish(kb_engine *e, const void *gathered_dev, int32_t n_rank
 /* hipStream_t on which all engine work is enqueued (NULL = engine-owned stream) */
 int kb_engine_set_stream(kb_engine *e, void *hip_stream);
 
+/* Batched multi-GPU steps (no host round trip per step): sharded_reset(budget) once,
+ * then per step sharded_scan(summary) -> all-gather -> sharded_resolve(gathered, n),
+ * then sharded_collect: the steps' changes (the log of the batch, at most cap), and
+ * KB_CHANGE (go on), KB_RETRY (loads were refolded exactly; go on), or the plan's last
+ * status (KB_NOCHANGE / error) as the last entry.  Steps after a halt are no-ops. */
+int kb_engine_sharded_reset(kb_engine *e, int64_t budget_steps);
+int kb_engine_sharded_scan(kb_engine *e, void *summary_dev);
+int kb_engine_sharded_resolve(kb_engine *e, const void *gathered_dev, int32_t n_ranks);
+int kb_engine_sharded_collect(kb_engine *e, kb_change *out, int64_t cap, int64_t *n_out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -991,6 +991,65 @@ extern "C" int kb_engine_step_begin(kb_engine* e, void* summary_dev) {
     return KB_OK;
 }
 
+// ---- batched multi-GPU steps: the host enqueues several (scan, summary, all-gather,
+// resolve) rounds without a host round trip; a halted step turns the rest into no-ops
+extern "C" int kb_engine_sharded_reset(kb_engine* e, int64_t budget_steps) {
+    if (!e || budget_steps < 1) return KB_ERR_INVALID;
+    if (e->pending) return e->pending;
+    if (reset_ctl(e, budget_steps) != KB_OK) return KB_ERR_HIP;
+    if (!e->h_ctl->prepped) enqueue_step(e);       // prep only (nothing to resolve yet)
+    HIPCHK(hipGetLastError());
+    return KB_OK;
+}
+
+extern "C" int kb_engine_sharded_scan(kb_engine* e, void* summary_dev) {
+    if (!e || !summary_dev) return KB_ERR_INVALID;
+    enqueue_scan(e);
+    SumArgs s;
+    s.ctl = e->ctl; s.R = scan_recs(e->recs, (int)e->nscan); s.cont = e->cont; s.cont_cap = e->cont_cap;
+    s.r = e->r; s.out = summary_recs((unsigned char*)summary_dev, 1);
+    launch_summary(s, e->st);
+    HIPCHK(hipGetLastError());
+    return KB_OK;
+}
+
+extern "C" int kb_engine_sharded_resolve(kb_engine* e, const void* gathered_dev, int32_t n_ranks) {
+    if (!e || !gathered_dev || n_ranks < 1) return KB_ERR_INVALID;
+    StepArgs a;
+    fill_step_args(e, a, summary_recs((unsigned char*)gathered_dev, n_ranks), 0);
+    launch_step(a, e->st);
+    HIPCHK(hipGetLastError());
+    return KB_OK;
+}
+
+extern "C" int kb_engine_sharded_collect(kb_engine* e, kb_change* out, int64_t cap, int64_t* n_out) {
+    if (!e || !n_out || cap < 0) return KB_ERR_INVALID;
+    *n_out = 0;
+    HIPCHK(hipMemcpyAsync(e->h_ctl, e->ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, e->st));
+    HIPCHK(hipStreamSynchronize(e->st));
+    const DevCtl c = *e->h_ctl;
+    const int nlog = (int)std::min<int64_t>(std::min<int64_t>(c.logpos, e->logcap), cap);
+    std::vector<ChangeDev> logv((size_t)nlog);
+    if (nlog) HIPCHK(hipMemcpy(logv.data(), e->log, (size_t)nlog * sizeof(ChangeDev), hipMemcpyDeviceToHost));
+    int rc = KB_CHANGE;
+    int64_t k = 0;
+    for (int i = 0; i < nlog; i++) {
+        kb_change tmp;
+        const int r = convert(e, logv[i], out ? &out[k] : &tmp);
+        k++;
+        if (r != KB_CHANGE) { rc = r; break; }
+    }
+    *n_out = k;
+    if (rc != KB_CHANGE) return rc;                   // no change / error: the plan ends
+    // exact loads needed (the resolve could not decide, or the load error grew):
+    // every rank reaches the same verdict on the same state -- refold, then go on
+    if (c.halted == H_NEED_EXACT || c.want_refresh) {
+        if (refresh(e) != KB_OK) return KB_ERR_HIP;
+        return KB_RETRY;
+    }
+    return KB_CHANGE;
+}
+
 extern "C" int kb_engine_step_finish(kb_engine* e, const void* gathered_dev, int32_t n_ranks, kb_change* out) {
     if (!e || !gathered_dev || n_ranks < 1 || !out) return KB_ERR_INVALID;
     if (e->pending) return pending_result(e, out);

@@ -28,22 +28,37 @@ def shard_bounds(n, world, rank):
 
 
 class ShardedPlanner:
-    def __init__(self, engine, world, device_tensors=True, group=None):
+    """staged=True: device summaries exchanged through host copies over gloo (rehearsal
+    of the N-rank protocol on a box whose ranks share one GPU; RCCL needs one GPU per rank)."""
+
+    def __init__(self, engine, world, device_tensors=True, group=None, staged=False):
         import torch
         self.engine = engine
         self.world = world
         self.group = group
+        self.staged = staged
         nb = engine.summary_bytes()
         dev = "cuda" if device_tensors else "cpu"
         self.summary = torch.zeros(nb, dtype=torch.uint8, device=dev)
         self.gathered = torch.zeros(world * nb, dtype=torch.uint8, device=dev)
         self.parts = list(self.gathered.chunk(world))
+        if staged:
+            self.h_summary = torch.zeros(nb, dtype=torch.uint8)
+            self.h_gathered = torch.zeros(world * nb, dtype=torch.uint8)
+            self.h_parts = list(self.h_gathered.chunk(world))
 
     def step(self):
+        import torch
         import torch.distributed as dist
         while True:
             self.engine.step_begin(self.summary)
-            if self.summary.is_cuda:
+            if self.staged:
+                torch.cuda.synchronize()
+                self.h_summary.copy_(self.summary)
+                dist.all_gather(self.h_parts, self.h_summary, group=self.group)
+                self.gathered.copy_(self.h_gathered)
+                torch.cuda.synchronize()
+            elif self.summary.is_cuda:
                 dist.all_gather_into_tensor(self.gathered, self.summary, group=self.group)
             else:
                 dist.all_gather(self.parts, self.summary, group=self.group)
@@ -53,14 +68,39 @@ class ShardedPlanner:
             if not (isinstance(ch, str) and ch == "retry"):
                 return ch
 
-    def plan(self, steps):
+    def plan(self, steps, batch=64):
+        """`steps` merged steps; engines with the batched protocol (sharded_*) enqueue
+        `batch` rounds (scan, summary, all-gather, resolve) per host round trip."""
+        if not hasattr(self.engine, "sharded_collect"):
+            out = []
+            for _ in range(steps):
+                ch = self.step()
+                if ch is None:
+                    break
+                out.append(ch)
+            return out
+        import torch
+        import torch.distributed as dist
         out = []
-        for _ in range(steps):
-            ch = self.step()
-            if ch is None:
+        while len(out) < steps:
+            b = min(batch, steps - len(out))
+            self.engine.sharded_reset(b)
+            for _ in range(b):
+                self.engine.sharded_scan(self.summary)
+                if self.staged:
+                    torch.cuda.synchronize()
+                    self.h_summary.copy_(self.summary)
+                    dist.all_gather(self.h_parts, self.h_summary, group=self.group)
+                    self.gathered.copy_(self.h_gathered)
+                    torch.cuda.synchronize()
+                else:
+                    dist.all_gather_into_tensor(self.gathered, self.summary, group=self.group)
+                self.engine.sharded_resolve(self.gathered, self.world)
+            status, changes = self.engine.sharded_collect(b + 1)
+            out.extend(changes)
+            if status == "done":
                 break
-            out.append(ch)
-        return out
+        return out[:steps]
 
 
 class _DeviceEngineAdapter:
@@ -78,6 +118,18 @@ class _DeviceEngineAdapter:
     def step_finish(self, gathered, world):
         return self.eng.step_finish(gathered.data_ptr(), world)
 
+    def sharded_reset(self, budget):
+        self.eng.sharded_reset(budget)
+
+    def sharded_scan(self, summary):
+        self.eng.sharded_scan(summary.data_ptr())
+
+    def sharded_resolve(self, gathered, world):
+        self.eng.sharded_resolve(gathered.data_ptr(), world)
+
+    def sharded_collect(self, cap):
+        return self.eng.sharded_collect(cap)
+
 
 def bench_main(args, world, rank, local):
     """bench.py for N > 1 (launched by torch.distributed.run)."""
@@ -85,14 +137,18 @@ def bench_main(args, world, rank, local):
     import torch.distributed as dist
     from . import engine as E
     from . import synth
+    import os
+    # KB_DIST_BACKEND=gloo: rehearsal with host-staged summaries (ranks may share a GPU)
+    backend = os.environ.get("KB_DIST_BACKEND", "nccl")
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
-    dist.init_process_group("nccl")
+    dist.init_process_group(backend)
     # weak scaling: 1M partitions per GPU (c3 shape), the same seed on every rank
     cl, cfg, desc = synth.config(args.workload, scale=args.scale * world)
     begin, end = shard_bounds(cl.n, world, rank)
     eng = E.Engine(cl, cfg, device=local, shard=(begin, end))
     eng.set_stream(torch.cuda.current_stream().cuda_stream)
-    sp = ShardedPlanner(_DeviceEngineAdapter(eng), world, device_tensors=True)
+    sp = ShardedPlanner(_DeviceEngineAdapter(eng), world, device_tensors=True, staged=backend != "nccl")
     sp.plan(args.warmup)
     st0 = eng.stats()
     torch.cuda.synchronize()
@@ -103,12 +159,21 @@ def bench_main(args, world, rank, local):
     torch.cuda.synchronize()
     dist.barrier()
     torch.cuda.synchronize()
-    dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device="cuda")
+    dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64,
+                      device="cuda" if backend == "nccl" else "cpu")
     dist.all_reduce(dt, op=dist.ReduceOp.MAX)
     wall = float(dt.item())
     st1 = eng.stats()
     steps = max(1, len(changes))
     cand = st1["candidates"] - st0["candidates"]       # merged counts: the whole job
+    # per-kernel device-clock durations over a second stretch (this rank's shard)
+    eng.set_timing(True)
+    sp.plan(min(args.steps, 100))
+    tk = eng.timings()
+    scan_ms, scan_n = tk["scan"]
+    scan_us = 1e3 * scan_ms / max(scan_n, 1)
+    shard_bytes = st1["scan_bytes"]
+    achieved = shard_bytes / (scan_us * 1e-6) / 1e9 if scan_us > 0 else 0.0
     if rank == 0:
         out = {
             "metric": "candidate moves scored/sec (+ ms per reassignment step)",
@@ -125,6 +190,12 @@ def bench_main(args, world, rank, local):
             "data": "synthetic (numpy PCG64), Zipf weights r^-1.1",
             "config": dict(desc, parallelism="partition-sharded x%d, replicated broker state, "
                                               "1 all-gather per step" % world),
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": 8000.0, "unit": "GB/s",
+                         "frac": achieved / 8000.0, "traffic": None, "kernel": "k_scan (rank 0 shard)",
+                         "bytes_per_launch": shard_bytes, "avg_launch_us": scan_us,
+                         "timing": "device clock: earliest workgroup start to latest workgroup end"},
+            "kernels_us_per_step": {k: 1e3 * v[0] / max(v[1], 1) for k, v in tk.items()},
+            "exchange": backend,
         }
         print(json.dumps(out))
     eng.close()

@@ -25,7 +25,9 @@ EXPORTS = ["kb_abi_version", "kb_engine_create", "kb_engine_balance", "kb_engine
            "kb_engine_replicas", "kb_engine_loads", "kb_engine_unbalance", "kb_engine_stats",
            "kb_engine_timings", "kb_engine_set_timing", "kb_engine_stamps", "kb_engine_bench_scan",
            "kb_engine_last_error", "kb_engine_destroy", "kb_engine_summary_bytes",
-           "kb_engine_step_begin", "kb_engine_step_finish", "kb_engine_set_stream"]
+           "kb_engine_step_begin", "kb_engine_step_finish", "kb_engine_set_stream",
+           "kb_engine_sharded_reset", "kb_engine_sharded_scan", "kb_engine_sharded_resolve",
+           "kb_engine_sharded_collect"]
 
 P64 = C.POINTER(C.c_int64)
 PD = C.POINTER(C.c_double)
@@ -108,6 +110,14 @@ def lib():
         L.kb_engine_step_finish.restype = C.c_int
         L.kb_engine_set_stream.argtypes = [vp, vp]
         L.kb_engine_set_stream.restype = C.c_int
+        L.kb_engine_sharded_reset.argtypes = [vp, C.c_int64]
+        L.kb_engine_sharded_reset.restype = C.c_int
+        L.kb_engine_sharded_scan.argtypes = [vp, vp]
+        L.kb_engine_sharded_scan.restype = C.c_int
+        L.kb_engine_sharded_resolve.argtypes = [vp, vp, C.c_int32]
+        L.kb_engine_sharded_resolve.restype = C.c_int
+        L.kb_engine_sharded_collect.argtypes = [vp, C.POINTER(kb_change), C.c_int64, P64]
+        L.kb_engine_sharded_collect.restype = C.c_int
         if L.kb_abi_version() != 2:
             raise ImportError("libkbengine.so ABI mismatch")
         _lib = L
@@ -337,6 +347,34 @@ class Engine:
         rc = lib().kb_engine_step_begin(self.h, C.c_void_p(summary_ptr))
         if rc < 0:
             raise EngineError(rc, self.last_error())
+
+    # ---- batched sharded steps (no host round trip per step)
+    def sharded_reset(self, budget):
+        rc = lib().kb_engine_sharded_reset(self.h, budget)
+        if rc < 0:
+            raise EngineError(rc, self.last_error())
+
+    def sharded_scan(self, summary_ptr):
+        rc = lib().kb_engine_sharded_scan(self.h, C.c_void_p(summary_ptr))
+        if rc < 0:
+            raise EngineError(rc, self.last_error())
+
+    def sharded_resolve(self, gathered_ptr, n_ranks):
+        rc = lib().kb_engine_sharded_resolve(self.h, C.c_void_p(gathered_ptr), n_ranks)
+        if rc < 0:
+            raise EngineError(rc, self.last_error())
+
+    def sharded_collect(self, cap):
+        """(status, changes): status "ok" / "retry" (go on), "done" (no change), or raises."""
+        buf = (kb_change * max(1, cap))()
+        n = C.c_int64()
+        rc = lib().kb_engine_sharded_collect(self.h, buf, cap, C.byref(n))
+        changes = [_change_dict(buf[i]) for i in range(n.value)]
+        if rc < 0:
+            raise EngineError(rc, self.last_error(), changes[-1] if changes else None)
+        if rc == KB_NOCHANGE:
+            return "done", changes[:-1]
+        return ("retry" if rc == KB_RETRY else "ok"), changes
 
     def step_finish(self, gathered_ptr, n_ranks):
         """The merged step; None for no change, "retry" when the step must be redone

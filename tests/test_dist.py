@@ -184,3 +184,49 @@ def test_two_engines_one_gpu_match_unsharded(workload):
     key = lambda c: (c["step"], c["pidx"], c["kind"], c["from_"], c["to"], c["slot"])
     assert [key(c) for c in got] == [key(c) for c in want]
     assert engs[0].state() == ref.state() == engs[1].state()
+
+
+@pytest.mark.gpu
+def test_two_engines_one_gpu_batched_protocol():
+    """The batched sharded protocol (sharded_reset / scan / resolve / collect: no host
+    round trip per step) gives the unsharded plan."""
+    from kafkabalancer_amd import engine as E
+    from kafkabalancer_amd import synth
+    cl = synth.make_cluster(5000, 200, 3, "zipf", nsets=16, set_size=40, seed=3)
+    cfg = default_cfg(allow_leader=True, min_unbalance=0.0)
+    ref = E.Engine(cl, cfg)
+    want, err = ref.plan(40)
+    assert err is None
+    world = 2
+    engs = [E.Engine(cl, cfg, shard=shard_bounds(cl.n, world, r)) for r in range(world)]
+    nb = engs[0].summary_bytes()
+    got = [[], []]
+    done = False
+    while not done and len(got[0]) < 40:
+        batch = min(16, 40 - len(got[0]))
+        for e in engs:
+            e.sharded_reset(batch)
+        # every buffer of the batch exists (and is zeroed) before the engines' streams
+        # write into them
+        allb = [[torch.zeros(nb, dtype=torch.uint8, device="cuda") for _ in range(world)] for _ in range(batch)]
+        torch.cuda.synchronize()
+        keep = []
+        for bufs in allb:
+            for e, b in zip(engs, bufs):
+                e.sharded_scan(b.data_ptr())
+            torch.cuda.synchronize()
+            gathered = torch.cat(bufs)
+            torch.cuda.synchronize()                   # the engines' streams read it next
+            keep.append((bufs, gathered))
+            for e in engs:
+                e.sharded_resolve(gathered.data_ptr(), world)
+        res = [e.sharded_collect(batch + 1) for e in engs]
+        assert res[0][0] == res[1][0]
+        for r in range(world):
+            got[r].extend(res[r][1])
+        done = res[0][0] == "done"
+    key = lambda c: (c["step"], c["pidx"], c["kind"], c["from_"], c["to"], c["slot"])
+    assert [key(c) for c in got[0]] == [key(c) for c in got[1]]
+    assert [key(c) for c in got[0]][:40] == [key(c) for c in want][:len(got[0][:40])]
+    assert len(got[0]) == len(want)
+    assert engs[0].state() == ref.state() == engs[1].state()

@@ -1,0 +1,12 @@
+#!/bin/bash
+# SQ counter passes over a short bench run (k_step / k_scan instruction mix and waits).
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out
+TAG=${1:-pmcs}
+i=0
+for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS" \
+           "SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_ACTIVE_INST_SCA SQ_INSTS_BRANCH"; do
+  i=$((i+1))
+  timeout -k 5 -s KILL 150 rocprofv3 --kernel-trace --pmc $grp --output-format csv -d gpurun_out/${TAG}_p$i -o run \
+      -- python3 bench.py --steps 200 --warmup 5 --no-cpu-baseline > gpurun_out/${TAG}_p$i.log 2>&1 || { echo "pass $i failed rc=$?"; tail -5 gpurun_out/${TAG}_p$i.log; exit 1; }
+done
+exit 0
