@@ -993,283 +993,330 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
         }
         KB_STAMP(ctl, 2);
 
-        // ---- Validate(dup) / RemoveExtra / AddMissing / MoveDisallowed / ReassignLeaders
+        // ---- fast path (one thread, one barrier): no first-index predicate, no
+        // ReassignLeaders, and every move() kind decided by the bounds on at most one key;
+        // anything else takes the general path below
+        __shared__ int s_fast;
         if (tid == 0) {
-            const double su = U0h;
-            D.status = 0; D.step = -1; D.kind = 0; D.slot = -1; D.part = -1;
-            D.from = -1; D.to = -1; D.su = su; D.cu = su; D.exact = 0; D.err = E_NONE; D.err_broker = -1;
-            const uint32_t* F = s_first;
-            auto rd = [&](uint32_t p, int k) -> int { return (int)a.rep[(long long)k * a.Ppad + p]; };
-            if (C.list_overflow) {
-                D.status = -1; D.step = 8; D.err = E_LIST_OVERFLOW; s_done = 1;
-            } else if (a.sem_go && F[F_DUP] != NONE32) {
-                D.status = -1; D.step = 1; D.err = E_DUP; D.part = F[F_DUP]; s_done = 1;
-            } else if (F[F_REMOVE] != NONE32) {                      // steps.go:70-89
-                const uint32_t p = F[F_REMOVE];
-                const uint32_t m = a.meta[p];
-                const int nrep = (int)meta_nrep(m), set = (int)meta_set(m);
-                const uint64_t* sb = a.setbits + (size_t)set * a.W64;
-                // lightest allowed replica in (load, id) order = smallest universe position
-                int best = -1, bslot = -1, bpos = 0x7FFFFFFF;
-                for (int k = 0; k < nrep; k++) {
-                    const int b = rd(p, k);
-                    if (!setbit(sb, b)) continue;
-                    const int ps = a.posu[b];
-                    if (ps < bpos) { bpos = ps; best = b; bslot = k; }
-                }
-                D.step = 3; D.part = p;
-                if (best < 0) { D.status = -1; D.err = E_REMOVE; }
-                else {
-                    // replacepl removes the FIRST slot holding that broker (utils.go:167-178)
-                    D.status = 1; D.kind = 2; D.slot = bslot; D.from = best; D.to = -1;
-                }
-                s_done = 1;
-            } else if (F[F_ADD] != NONE32) {                         // steps.go:93-113
-                s_lkind = 2; s_lpart = F[F_ADD];                      // pick list below
-            } else if (F[F_DIS] != NONE32) {                         // steps.go:117-143
-                s_lkind = 1; s_lpart = F[F_DIS];
-            } else if (a.rebalance) {                                 // steps.go:234-282
-                // su < MinUnbalance decides; certify it against eps or use the exact su
-                const bool lo = su + 2.0 * eps < a.min_unbalance, hi = su - 2.0 * eps >= a.min_unbalance;
-                if (!lo && !hi) {
-                    s_exact_need = (!a.integral && ndirty0 > 0) ? 1 : 2;
-                } else if (hi) {
-                    s_exact_need = 3;                                 // leader pick below
+            int fast = !C.list_overflow && !s_fm && !a.rebalance && !(s_flags & 1u) && !a.exact_unb;
+            Decision d;
+            d.status = 0; d.step = -1; d.kind = 0; d.slot = -1; d.part = -1; d.from = -1; d.to = -1;
+            d.su = U0h; d.cu = U0h; d.w = 0.0; d.exact = 0; d.err = E_NONE; d.err_broker = -1; d.pad = 0;
+            for (int kind = a.allow_leader ? 0 : 1; fast && kind < 2; kind++) {
+                const int step = kind == 0 ? 7 : 8;
+                const int ndist = s_nd[kind];
+                if (s_kfail[kind] || ndist > 1) { fast = 0; break; }
+                if (ndist == 1) {
+                    const Contender cw = s_li[kind] == -2 ? s_single[kind] : dedup_entry(T, s_li[kind]);
+                    const double Ua = U0h + cont_delta_ld(s_ld, cw, inv_avg);
+                    // the general path's certification (3*eps margins on both decisions)
+                    const double thr = U0h - a.min_unbalance;
+                    const double rel = 4.0 * DBL_EPSILON * fabs(thr);
+                    const bool imp_t = Ua + 3.0 * eps < U0h, imp_f = Ua - 3.0 * eps >= U0h;
+                    const bool take_t = Ua + 3.0 * eps + rel < thr, take_f = Ua - 3.0 * eps - rel >= thr;
+                    if (!((imp_t || imp_f) && (take_t || take_f))) { fast = 0; break; }
+                    if (take_t) {
+                        if (!imp_t) { d.status = -1; d.step = step; d.err = E_PANIC; }
+                        else {
+                            d.status = 1; d.step = step; d.kind = 1;
+                            d.part = (long long)(cw.iter >> 21); d.slot = (int)((cw.iter >> 16) & 31);
+                            d.from = cw.s; d.to = cw.t; d.w = cw.w; d.su = U0h; d.cu = Ua; d.exact = 0;
+                        }
+                        break;
+                    }
+                    d.su = U0h; d.cu = U0h; d.exact = 0;
+                } else {
+                    // no candidate: cu = su; the decision is su < fl(su - MinUnbalance)
+                    const bool t_t = -a.min_unbalance > 4.0 * DBL_EPSILON * (fabs(U0h) + eps);
+                    const bool t_f = a.min_unbalance >= 0.0;
+                    if (!(t_t || t_f)) { fast = 0; break; }
+                    if (t_t) { d.status = -1; d.step = step; d.err = E_PANIC; break; }
+                    d.su = U0h; d.cu = U0h; d.exact = 0;
                 }
             }
+            if (fast) { D = d; s_done = 1; }
+            s_fast = fast;
         }
         __syncthreads();
-        if (s_lkind) {
-            // AddMissingReplicas / MoveDisallowedReplicas pick from the allowed brokers in
-            // (load, id) order from the heaviest down: getBrokerListByLoad over the load
-            // map with absent brokers at 0 (Add, utils.go:66-79), getBrokerListByLoadBL
-            // over the brokers holding replicas (Disallowed, utils.go:81-90)
-            const uint32_t p = s_lpart;
-            const uint32_t m = a.meta[p];
-            const int nrep = (int)meta_nrep(m), set = (int)meta_set(m);
-            if (wid == 0) {
-                if (lane < nrep) s_lrep[lane] = (int)a.rep[(long long)lane * a.Ppad + p];
-                const unsigned long long sbw = lane < a.W64 ? (unsigned long long)a.setbits[(size_t)set * a.W64 + lane] : 0ull;
-                s_lsb[lane] = sbw;
-                if (lane == 0) s_lpick = -1;
-                const unsigned long long lt = (1ull << lane) - 1ull;
-                bool done = false;
-                for (int base = 0; base < B && !done; base += 64) {
-                    const int k = base + lane;
-                    const int b = k < B ? s_ord[B - 1 - k] : 0;
-                    bool mem = k < B && ((s_lsb[b >> 6] >> (b & 63)) & 1ull);
-                    if (s_lkind == 1) mem = mem && (s_fl[b] & BF_PRESENT);
-                    bool isrep = false;
-                    for (int q = 0; q < nrep; q++) isrep |= s_lrep[q] == b;
-                    const bool ok = mem && !isrep;
-                    const unsigned long long bal = __ballot(ok);
-                    if (bal) {
-                        if (ok && (bal & lt) == 0) s_lpick = b;      // first eligible from the heavy end
-                        done = true;
-                    }
-                }
-            }
-            __syncthreads();
+        if (!s_fast) {
+            // ---- Validate(dup) / RemoveExtra / AddMissing / MoveDisallowed / ReassignLeaders
             if (tid == 0) {
-                const int t = s_lpick;
-                if (s_lkind == 2) {
-                    D.step = 4; D.part = p;
-                    if (t < 0) { D.status = -1; D.err = E_ADD; }
-                    else { D.status = 1; D.kind = 3; D.slot = nrep; D.from = -1; D.to = t; }
-                } else {
-                    int vslot = -1;
-                    for (int k = 0; k < nrep && vslot < 0; k++)
-                        if (!((s_lsb[s_lrep[k] >> 6] >> (s_lrep[k] & 63)) & 1ull)) vslot = k;
-                    D.step = 5; D.part = p; D.slot = vslot; D.from = s_lrep[vslot];
-                    if (t < 0) { D.status = -1; D.err = E_DIS; D.err_broker = D.from; }
-                    else { D.status = 1; D.kind = 1; D.to = t; }
-                }
-                s_done = 1;
-            }
-            __syncthreads();
-        }
-        // exact su (sequential folds in bl order); s_e doubles as the bl-ordered loads
-        // (every load is exact here, so every error bound is zero)
-        double* s_Lm = s_e;
-        auto exact_su = [&]() {
-            for (int k = tid; k < nblm0; k += STEP_THREADS) s_Lm[k] = s_ld[a.blm[k]];
-            __syncthreads();
-            if (tid == 0) {
-                const double S = fold_lds(s_Lm, nblm0);
-                const double avg = S / (double)nblm0;
-                double U = 0.0;
-                for (int k = 0; k < nblm0; k++) U += term_x(s_Lm[k], avg);
-                s_sux = U;
-                atomicAdd(&C.total_folds, 1ull);
-            }
-            __syncthreads();
-        };
-        auto unstage = [&]() {
-            for (int b = tid; b < B; b += STEP_THREADS) s_e[b] = 0.0;
-            __syncthreads();
-        };
-        if (s_exact_need >= 2) {
-            bool take = s_exact_need == 3;
-            if (s_exact_need == 2) {
-                exact_su();
-                unstage();
-                take = !(s_sux < a.min_unbalance);
-            }
-            if (tid == 0) {
-                s_exact_need = 0;
+                const double su = U0h;
+                D.status = 0; D.step = -1; D.kind = 0; D.slot = -1; D.part = -1;
+                D.from = -1; D.to = -1; D.su = su; D.cu = su; D.exact = 0; D.err = E_NONE; D.err_broker = -1;
                 const uint32_t* F = s_first;
-                if (take) {
-                    auto rd = [&](uint32_t p, int k) -> int { return (int)a.rep[(long long)k * a.Ppad + p]; };
-                    if (F[F_EMPTY] != NONE32 || nblm0 == 0) {
-                        D.status = -1; D.step = 6; D.err = E_PANIC; D.part = F[F_EMPTY]; s_done = 1;
-                    } else if (F[F_LEAD] != NONE32) {
-                        const uint32_t p = F[F_LEAD];
-                        const int nrep = (int)meta_nrep(a.meta[p]);
-                        const int light = C.light;
-                        int ex = -1;
-                        for (int k = 0; k < nrep && ex < 0; k++) if (rd(p, k) == light) ex = k;
-                        D.status = 1; D.step = 6; D.part = p; D.slot = 0; D.from = rd(p, 0); D.to = light;
-                        D.kind = ex >= 0 ? 4 : 1;       // swap when bl[0] is already a replica
-                        s_done = 1;
+                auto rd = [&](uint32_t p, int k) -> int { return (int)a.rep[(long long)k * a.Ppad + p]; };
+                if (C.list_overflow) {
+                    D.status = -1; D.step = 8; D.err = E_LIST_OVERFLOW; s_done = 1;
+                } else if (a.sem_go && F[F_DUP] != NONE32) {
+                    D.status = -1; D.step = 1; D.err = E_DUP; D.part = F[F_DUP]; s_done = 1;
+                } else if (F[F_REMOVE] != NONE32) {                      // steps.go:70-89
+                    const uint32_t p = F[F_REMOVE];
+                    const uint32_t m = a.meta[p];
+                    const int nrep = (int)meta_nrep(m), set = (int)meta_set(m);
+                    const uint64_t* sb = a.setbits + (size_t)set * a.W64;
+                    // lightest allowed replica in (load, id) order = smallest universe position
+                    int best = -1, bslot = -1, bpos = 0x7FFFFFFF;
+                    for (int k = 0; k < nrep; k++) {
+                        const int b = rd(p, k);
+                        if (!setbit(sb, b)) continue;
+                        const int ps = a.posu[b];
+                        if (ps < bpos) { bpos = ps; best = b; bslot = k; }
+                    }
+                    D.step = 3; D.part = p;
+                    if (best < 0) { D.status = -1; D.err = E_REMOVE; }
+                    else {
+                        // replacepl removes the FIRST slot holding that broker (utils.go:167-178)
+                        D.status = 1; D.kind = 2; D.slot = bslot; D.from = best; D.to = -1;
+                    }
+                    s_done = 1;
+                } else if (F[F_ADD] != NONE32) {                         // steps.go:93-113
+                    s_lkind = 2; s_lpart = F[F_ADD];                      // pick list below
+                } else if (F[F_DIS] != NONE32) {                         // steps.go:117-143
+                    s_lkind = 1; s_lpart = F[F_DIS];
+                } else if (a.rebalance) {                                 // steps.go:234-282
+                    // su < MinUnbalance decides; certify it against eps or use the exact su
+                    const bool lo = su + 2.0 * eps < a.min_unbalance, hi = su - 2.0 * eps >= a.min_unbalance;
+                    if (!lo && !hi) {
+                        s_exact_need = (!a.integral && ndirty0 > 0) ? 1 : 2;
+                    } else if (hi) {
+                        s_exact_need = 3;                                 // leader pick below
                     }
                 }
             }
             __syncthreads();
-        }
-        KB_STAMP(ctl, 3);
-
-        // ---- move(): leader step (if allowed), then non-leader step (steps.go:284-298)
-        for (int kind = a.allow_leader ? 0 : 1; kind < 2 && !s_done && !s_exact_need; kind++) {
-            const int step = kind == 0 ? 7 : 8;
-            const double g = s_g[kind];
-            if (tid == 0) {
-                if (s_first[F_EMPTY_ELIG] != NONE32) {
-                    D.status = -1; D.step = step; D.err = E_PANIC; D.part = s_first[F_EMPTY_ELIG]; s_done = 1;
-                } else if (s_flags & 1u) {
-                    D.status = -1; D.step = step; D.err = E_CONT_OVERFLOW; s_done = 1;
+            if (s_lkind) {
+                // AddMissingReplicas / MoveDisallowedReplicas pick from the allowed brokers in
+                // (load, id) order from the heaviest down: getBrokerListByLoad over the load
+                // map with absent brokers at 0 (Add, utils.go:66-79), getBrokerListByLoadBL
+                // over the brokers holding replicas (Disallowed, utils.go:81-90)
+                const uint32_t p = s_lpart;
+                const uint32_t m = a.meta[p];
+                const int nrep = (int)meta_nrep(m), set = (int)meta_set(m);
+                if (wid == 0) {
+                    if (lane < nrep) s_lrep[lane] = (int)a.rep[(long long)lane * a.Ppad + p];
+                    const unsigned long long sbw = lane < a.W64 ? (unsigned long long)a.setbits[(size_t)set * a.W64 + lane] : 0ull;
+                    s_lsb[lane] = sbw;
+                    if (lane == 0) s_lpick = -1;
+                    const unsigned long long lt = (1ull << lane) - 1ull;
+                    bool done = false;
+                    for (int base = 0; base < B && !done; base += 64) {
+                        const int k = base + lane;
+                        const int b = k < B ? s_ord[B - 1 - k] : 0;
+                        bool mem = k < B && ((s_lsb[b >> 6] >> (b & 63)) & 1ull);
+                        if (s_lkind == 1) mem = mem && (s_fl[b] & BF_PRESENT);
+                        bool isrep = false;
+                        for (int q = 0; q < nrep; q++) isrep |= s_lrep[q] == b;
+                        const bool ok = mem && !isrep;
+                        const unsigned long long bal = __ballot(ok);
+                        if (bal) {
+                            if (ok && (bal & lt) == 0) s_lpick = b;      // first eligible from the heavy end
+                            done = true;
+                        }
+                    }
                 }
-            }
-            __syncthreads();
-            if (s_done) break;
-            // (1) the distinct keys of this kind were collected with the records
-            const int ndist = s_nd[kind];
-            const bool fail = s_kfail[kind] != 0;
-            const bool have = ndist > 0 || fail;
-            // (2) certified decision for one key; exact folds otherwise
-            double Ua = 0.0;
-            Contender cw;
-            cw.s = cw.t = -1; cw.w = 0; cw.iter = NONE64; cw.kind = kind; cw.pad = 0;
-            bool certain = false, c_improved = false, c_take = false;
-            if (!fail && ndist == 1) {
-                cw = s_li[kind] == -2 ? s_single[kind] : dedup_entry(T, s_li[kind]);   // the one key
-                Ua = U0h + cont_delta_ld(s_ld, cw, inv_avg);
-                // |Ua - U'| <= eps and |U0h - su| <= eps; margins of 3*eps on both decisions
-                const double thr = U0h - a.min_unbalance;
-                const double rel = 4.0 * DBL_EPSILON * fabs(thr);
-                const bool imp_t = Ua + 3.0 * eps < U0h, imp_f = Ua - 3.0 * eps >= U0h;
-                const bool take_t = Ua + 3.0 * eps + rel < thr, take_f = Ua - 3.0 * eps - rel >= thr;
-                certain = (imp_t || imp_f) && (take_t || take_f) && !a.exact_unb;
-                c_improved = imp_t;
-                c_take = take_t;
-            } else if (!have) {
-                // no candidate: cu = su; the decision is su < fl(su - MinUnbalance)
-                const bool t_t = -a.min_unbalance > 4.0 * DBL_EPSILON * (fabs(U0h) + eps);
-                const bool t_f = a.min_unbalance >= 0.0;
-                certain = (t_t || t_f) && !a.exact_unb;
-                c_improved = false;
-                c_take = t_t;
-            }
-            if (!certain && !a.integral && ndirty0 > 0) {
-                if (tid == 0) s_exact_need = 1;
                 __syncthreads();
-                break;
+                if (tid == 0) {
+                    const int t = s_lpick;
+                    if (s_lkind == 2) {
+                        D.step = 4; D.part = p;
+                        if (t < 0) { D.status = -1; D.err = E_ADD; }
+                        else { D.status = 1; D.kind = 3; D.slot = nrep; D.from = -1; D.to = t; }
+                    } else {
+                        int vslot = -1;
+                        for (int k = 0; k < nrep && vslot < 0; k++)
+                            if (!((s_lsb[s_lrep[k] >> 6] >> (s_lrep[k] & 63)) & 1ull)) vslot = k;
+                        D.step = 5; D.part = p; D.slot = vslot; D.from = s_lrep[vslot];
+                        if (t < 0) { D.status = -1; D.err = E_DIS; D.err_broker = D.from; }
+                        else { D.status = 1; D.kind = 1; D.to = t; }
+                    }
+                    s_done = 1;
+                }
+                __syncthreads();
             }
-            double Ustar = U0h, sux = U0h;
-            unsigned long long witer = NONE64;
-            int exact = 0;
-            bool improved = false, take = false;
-            if (certain) {
-                improved = c_improved;
-                take = c_take;
-                Ustar = Ua;
-                witer = cw.iter;
-            } else {
-                exact = 1;
-                exact_su();                      // also stages the exact loads in bl order
-                sux = s_sux;
+            // exact su (sequential folds in bl order); s_e doubles as the bl-ordered loads
+            // (every load is exact here, so every error bound is zero)
+            double* s_Lm = s_e;
+            auto exact_su = [&]() {
+                for (int k = tid; k < nblm0; k += STEP_THREADS) s_Lm[k] = s_ld[a.blm[k]];
+                __syncthreads();
+                if (tid == 0) {
+                    const double S = fold_lds(s_Lm, nblm0);
+                    const double avg = S / (double)nblm0;
+                    double U = 0.0;
+                    for (int k = 0; k < nblm0; k++) U += term_x(s_Lm[k], avg);
+                    s_sux = U;
+                    atomicAdd(&C.total_folds, 1ull);
+                }
+                __syncthreads();
+            };
+            auto unstage = [&]() {
+                for (int b = tid; b < B; b += STEP_THREADS) s_e[b] = 0.0;
+                __syncthreads();
+            };
+            if (s_exact_need >= 2) {
+                bool take = s_exact_need == 3;
+                if (s_exact_need == 2) {
+                    exact_su();
+                    unstage();
+                    take = !(s_sux < a.min_unbalance);
+                }
+                if (tid == 0) {
+                    s_exact_need = 0;
+                    const uint32_t* F = s_first;
+                    if (take) {
+                        auto rd = [&](uint32_t p, int k) -> int { return (int)a.rep[(long long)k * a.Ppad + p]; };
+                        if (F[F_EMPTY] != NONE32 || nblm0 == 0) {
+                            D.status = -1; D.step = 6; D.err = E_PANIC; D.part = F[F_EMPTY]; s_done = 1;
+                        } else if (F[F_LEAD] != NONE32) {
+                            const uint32_t p = F[F_LEAD];
+                            const int nrep = (int)meta_nrep(a.meta[p]);
+                            const int light = C.light;
+                            int ex = -1;
+                            for (int k = 0; k < nrep && ex < 0; k++) if (rd(p, k) == light) ex = k;
+                            D.status = 1; D.step = 6; D.part = p; D.slot = 0; D.from = rd(p, 0); D.to = light;
+                            D.kind = ex >= 0 ? 4 : 1;       // swap when bl[0] is already a replica
+                            s_done = 1;
+                        }
+                    }
+                }
+                __syncthreads();
+            }
+            KB_STAMP(ctl, 3);
+
+            // ---- move(): leader step (if allowed), then non-leader step (steps.go:284-298)
+            for (int kind = a.allow_leader ? 0 : 1; kind < 2 && !s_done && !s_exact_need; kind++) {
+                const int step = kind == 0 ? 7 : 8;
+                const double g = s_g[kind];
+                if (tid == 0) {
+                    if (s_first[F_EMPTY_ELIG] != NONE32) {
+                        D.status = -1; D.step = step; D.err = E_PANIC; D.part = s_first[F_EMPTY_ELIG]; s_done = 1;
+                    } else if (s_flags & 1u) {
+                        D.status = -1; D.step = step; D.err = E_CONT_OVERFLOW; s_done = 1;
+                    }
+                }
+                __syncthreads();
+                if (s_done) break;
+                // (1) the distinct keys of this kind were collected with the records
+                const int ndist = s_nd[kind];
+                const bool fail = s_kfail[kind] != 0;
+                const bool have = ndist > 0 || fail;
+                // (2) certified decision for one key; exact folds otherwise
+                double Ua = 0.0;
+                Contender cw;
+                cw.s = cw.t = -1; cw.w = 0; cw.iter = NONE64; cw.kind = kind; cw.pad = 0;
+                bool certain = false, c_improved = false, c_take = false;
                 if (!fail && ndist == 1) {
-                    if (tid == 0) {
-                        s_dv[0] = exact_unbalance_lds(s_Lm, nblm0, a.posm[cw.s], a.posm[cw.t],
-                                                      s_ld[cw.s] - cw.w, s_ld[cw.t] + cw.w);
-                        atomicAdd(&C.total_folds, 1ull);
-                    }
+                    cw = s_li[kind] == -2 ? s_single[kind] : dedup_entry(T, s_li[kind]);   // the one key
+                    Ua = U0h + cont_delta_ld(s_ld, cw, inv_avg);
+                    // |Ua - U'| <= eps and |U0h - su| <= eps; margins of 3*eps on both decisions
+                    const double thr = U0h - a.min_unbalance;
+                    const double rel = 4.0 * DBL_EPSILON * fabs(thr);
+                    const bool imp_t = Ua + 3.0 * eps < U0h, imp_f = Ua - 3.0 * eps >= U0h;
+                    const bool take_t = Ua + 3.0 * eps + rel < thr, take_f = Ua - 3.0 * eps - rel >= thr;
+                    certain = (imp_t || imp_f) && (take_t || take_f) && !a.exact_unb;
+                    c_improved = imp_t;
+                    c_take = take_t;
+                } else if (!have) {
+                    // no candidate: cu = su; the decision is su < fl(su - MinUnbalance)
+                    const bool t_t = -a.min_unbalance > 4.0 * DBL_EPSILON * (fabs(U0h) + eps);
+                    const bool t_f = a.min_unbalance >= 0.0;
+                    certain = (t_t || t_f) && !a.exact_unb;
+                    c_improved = false;
+                    c_take = t_t;
+                }
+                if (!certain && !a.integral && ndirty0 > 0) {
+                    if (tid == 0) s_exact_need = 1;
                     __syncthreads();
-                    Ustar = s_dv[0];
+                    break;
+                }
+                double Ustar = U0h, sux = U0h;
+                unsigned long long witer = NONE64;
+                int exact = 0;
+                bool improved = false, take = false;
+                if (certain) {
+                    improved = c_improved;
+                    take = c_take;
+                    Ustar = Ua;
                     witer = cw.iter;
-                } else if (have) {
-                    // several keys (or an overfull table): exact sequential folds, lexicographic min
-                    double bu = HUGE_VAL;
-                    unsigned long long bi = NONE64;
-                    int bs = -1, bt = -1;
-                    double bw = 0.0;
-                    unsigned long long nf = 0;
-                    auto consider = [&](const Contender& c) {
-                        const double u = exact_unbalance_lds(s_Lm, nblm0, a.posm[c.s], a.posm[c.t],
-                                                             s_ld[c.s] - c.w, s_ld[c.t] + c.w);
-                        nf++;
-                        if (u < bu || (u == bu && c.iter < bi)) { bu = u; bi = c.iter; bs = c.s; bt = c.t; bw = c.w; }
-                    };
-                    if (!fail) {
-                        for (int h = tid; h < DEDUP_STEP; h += STEP_THREADS)
-                            if (s_key[h] != NONE32 && (int)(s_key[h] >> 30) == kind) consider(dedup_entry(T, h));
-                    } else {
-                        for_each_contender(a, s_ld, kind, g, eps, inv_avg, consider);
-                    }
-                    nf = wave_sum(nf);
-                    if (lane == 0 && nf) atomicAdd(&C.total_folds, nf);
-                    for (int o = 32; o > 0; o >>= 1) {
-                        const double ou = __shfl_xor(bu, o);
-                        const unsigned long long oi = __shfl_xor(bi, o);
-                        const int os = __shfl_xor(bs, o), ot = __shfl_xor(bt, o);
-                        const double ow = __shfl_xor(bw, o);
-                        if (ou < bu || (ou == bu && oi < bi)) { bu = ou; bi = oi; bs = os; bt = ot; bw = ow; }
-                    }
-                    __syncthreads();
-                    if (lane == 0) { s_dv[wid] = bu; s_u[wid] = bi; s_bs[wid] = bs; s_bt[wid] = bt; s_bw[wid] = bw; }
-                    __syncthreads();
-                    if (tid == 0) {
-                        for (int q = 1; q < NW; q++)
-                            if (s_dv[q] < s_dv[0] || (s_dv[q] == s_dv[0] && s_u[q] < s_u[0])) {
-                                s_dv[0] = s_dv[q]; s_u[0] = s_u[q]; s_bs[0] = s_bs[q]; s_bt[0] = s_bt[q]; s_bw[0] = s_bw[q];
-                            }
-                    }
-                    __syncthreads();
-                    Ustar = s_dv[0]; witer = s_u[0];
-                    cw.s = s_bs[0]; cw.t = s_bt[0]; cw.w = s_bw[0]; cw.iter = witer;
-                }
-                unstage();
-                // cu starts at su and only a strictly smaller u replaces it (steps.go:163,211)
-                improved = have && Ustar < sux;
-                const double cu = improved ? Ustar : sux;
-                take = cu < sux - a.min_unbalance;
-            }
-            __syncthreads();
-            if (tid == 0) {
-                if (take) {
-                    if (!improved) {
-                        // replacepl on the zero Partition: the reference panics
-                        D.status = -1; D.step = step; D.err = E_PANIC; s_done = 1;
-                    } else {
-                        D.status = 1; D.step = step; D.kind = 1;
-                        D.part = (long long)(witer >> 21); D.slot = (int)((witer >> 16) & 31);
-                        D.from = cw.s; D.to = cw.t; D.w = cw.w; D.su = sux; D.cu = Ustar; D.exact = exact;
-                        s_done = 1;
-                    }
                 } else {
-                    D.su = sux; D.cu = sux; D.exact = exact;
+                    exact = 1;
+                    exact_su();                      // also stages the exact loads in bl order
+                    sux = s_sux;
+                    if (!fail && ndist == 1) {
+                        if (tid == 0) {
+                            s_dv[0] = exact_unbalance_lds(s_Lm, nblm0, a.posm[cw.s], a.posm[cw.t],
+                                                          s_ld[cw.s] - cw.w, s_ld[cw.t] + cw.w);
+                            atomicAdd(&C.total_folds, 1ull);
+                        }
+                        __syncthreads();
+                        Ustar = s_dv[0];
+                        witer = cw.iter;
+                    } else if (have) {
+                        // several keys (or an overfull table): exact sequential folds, lexicographic min
+                        double bu = HUGE_VAL;
+                        unsigned long long bi = NONE64;
+                        int bs = -1, bt = -1;
+                        double bw = 0.0;
+                        unsigned long long nf = 0;
+                        auto consider = [&](const Contender& c) {
+                            const double u = exact_unbalance_lds(s_Lm, nblm0, a.posm[c.s], a.posm[c.t],
+                                                                 s_ld[c.s] - c.w, s_ld[c.t] + c.w);
+                            nf++;
+                            if (u < bu || (u == bu && c.iter < bi)) { bu = u; bi = c.iter; bs = c.s; bt = c.t; bw = c.w; }
+                        };
+                        if (!fail) {
+                            for (int h = tid; h < DEDUP_STEP; h += STEP_THREADS)
+                                if (s_key[h] != NONE32 && (int)(s_key[h] >> 30) == kind) consider(dedup_entry(T, h));
+                        } else {
+                            for_each_contender(a, s_ld, kind, g, eps, inv_avg, consider);
+                        }
+                        nf = wave_sum(nf);
+                        if (lane == 0 && nf) atomicAdd(&C.total_folds, nf);
+                        for (int o = 32; o > 0; o >>= 1) {
+                            const double ou = __shfl_xor(bu, o);
+                            const unsigned long long oi = __shfl_xor(bi, o);
+                            const int os = __shfl_xor(bs, o), ot = __shfl_xor(bt, o);
+                            const double ow = __shfl_xor(bw, o);
+                            if (ou < bu || (ou == bu && oi < bi)) { bu = ou; bi = oi; bs = os; bt = ot; bw = ow; }
+                        }
+                        __syncthreads();
+                        if (lane == 0) { s_dv[wid] = bu; s_u[wid] = bi; s_bs[wid] = bs; s_bt[wid] = bt; s_bw[wid] = bw; }
+                        __syncthreads();
+                        if (tid == 0) {
+                            for (int q = 1; q < NW; q++)
+                                if (s_dv[q] < s_dv[0] || (s_dv[q] == s_dv[0] && s_u[q] < s_u[0])) {
+                                    s_dv[0] = s_dv[q]; s_u[0] = s_u[q]; s_bs[0] = s_bs[q]; s_bt[0] = s_bt[q]; s_bw[0] = s_bw[q];
+                                }
+                        }
+                        __syncthreads();
+                        Ustar = s_dv[0]; witer = s_u[0];
+                        cw.s = s_bs[0]; cw.t = s_bt[0]; cw.w = s_bw[0]; cw.iter = witer;
+                    }
+                    unstage();
+                    // cu starts at su and only a strictly smaller u replaces it (steps.go:163,211)
+                    improved = have && Ustar < sux;
+                    const double cu = improved ? Ustar : sux;
+                    take = cu < sux - a.min_unbalance;
                 }
+                __syncthreads();
+                if (tid == 0) {
+                    if (take) {
+                        if (!improved) {
+                            // replacepl on the zero Partition: the reference panics
+                            D.status = -1; D.step = step; D.err = E_PANIC; s_done = 1;
+                        } else {
+                            D.status = 1; D.step = step; D.kind = 1;
+                            D.part = (long long)(witer >> 21); D.slot = (int)((witer >> 16) & 31);
+                            D.from = cw.s; D.to = cw.t; D.w = cw.w; D.su = sux; D.cu = Ustar; D.exact = exact;
+                            s_done = 1;
+                        }
+                    } else {
+                        D.su = sux; D.cu = sux; D.exact = exact;
+                    }
+                }
+                __syncthreads();
             }
-            __syncthreads();
         }
         KB_STAMP(ctl, 4);
 
