@@ -855,8 +855,9 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
     __shared__ int s_lrep[MAXR + 1];
     __shared__ unsigned long long s_lsb[64];
     if (tid == 0) { s_nT = 0; s_done = 0; s_exact_need = 0; s_moved = -1; s_lkind = 0; }
+    if (tid < NF) s_first[tid] = NONE32;
+    if (tid < 2) s_kc[tid] = 0;
     if (halted != H_RUN) return;
-    __syncthreads();
     KB_STAMP(ctl, 12);
     // ---- the scan records (or the gathered rank summaries): one per thread, reduced
     // per wave with DPP and across the waves by wave 0; then every thread collects
@@ -885,25 +886,21 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
             s_pf[NF][wid] = flg; s_pf[NF + 1][wid] = fm;
         }
         __syncthreads();
+        // every wave combines the wave partials of the minima itself (lane-parallel):
+        // no second barrier; wave 0 publishes the rest for the resolve
+        const bool pin = lane < NW;
+        const double g0 = wave_min(pin ? s_pd[0][lane] : HUGE_VAL), g1 = wave_min(pin ? s_pd[1][lane] : HUGE_VAL);
+        fm = wave_red_or(pin ? s_pf[NF + 1][lane] : 0u);
         if (wid == 0) {
-            const bool in = lane < NW;
-            d0 = in ? s_pd[0][lane] : HUGE_VAL; d1 = in ? s_pd[1][lane] : HUGE_VAL;
-            c0 = in ? s_pc[0][lane] : 0ull; c1 = in ? s_pc[1][lane] : 0ull;
-            flg = in ? s_pf[NF][lane] : 0u;
-            fm = in ? s_pf[NF + 1][lane] : 0u;
-            d0 = wave_min(d0); d1 = wave_min(d1); c0 = wave_sum(c0); c1 = wave_sum(c1);
-            flg = wave_red_or(flg);
-            fm = wave_red_or(fm);
+            c0 = wave_sum(pin ? s_pc[0][lane] : 0ull); c1 = wave_sum(pin ? s_pc[1][lane] : 0ull);
+            flg = wave_red_or(pin ? s_pf[NF][lane] : 0u);
             if (lane == 0) {
-                s_g[0] = d0; s_g[1] = d1; s_cand[0] = c0; s_cand[1] = c1;
+                s_g[0] = g0; s_g[1] = g1; s_cand[0] = c0; s_cand[1] = c1;
                 s_flags = flg | (a.use_spill && C.cont_overflow ? 1u : 0u);
                 s_fm = fm;
             }
-            if (lane < NF) s_first[lane] = NONE32;
-            if (lane < 2) s_kc[lane] = 0;
         }
-        __syncthreads();
-        if (s_fm) {
+        if (fm) {
             // some record holds a first-index predicate (the plan is not in shape yet)
             uint32_t f[NF];
 #pragma unroll
@@ -922,7 +919,6 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
             __syncthreads();
         }
         KB_STAMP(ctl, 13);
-        const double g0 = s_g[0], g1 = s_g[1];
         // keys within the window, per kind, over the records within 8*eps of the
         // minimum; a kind with exactly one such key needs no key round trip: it is
         // that record's best key (inserted here speculatively in any case)
