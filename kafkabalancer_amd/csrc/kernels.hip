@@ -431,12 +431,19 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
     int tile = blockIdx.x;
     PartRaw<RC> A, Bq;
     if (tile < a.ntiles) load_parts<RC>(a, a.shard_begin + (long long)tile * TILE + (long long)tid * PER_LANE, A);
+    double rlo = HUGE_VAL, rhi = -HUGE_VAL;          // range of the relative loads (prune bound)
     for (int i = tid; i < a.B; i += SCAN_THREADS) {
         const double r = a.r[i];
         s_rf[i] = make_double2(r, fsq(r));
         s_pos[i] = (int16_t)a.posm[i];
         s_blm[i] = (uint16_t)a.blm[i];
+        rlo = r < rlo ? r : rlo;
+        rhi = r > rhi ? r : rhi;
     }
+    __shared__ double s_rr[2][NW];
+    rlo = wave_min(rlo);
+    rhi = wave_max(rhi);
+    if (lane == 0) { s_rr[0][wid] = rlo; s_rr[1][wid] = rhi; }
     if (LSETS) for (int i = tid; i < a.nsets * U; i += SCAN_THREADS) s_set[i] = a.setrec[i];
     for (int i = tid; i < DEDUP_SCAN; i += SCAN_THREADS) { s_key[i] = NONE32; s_wb[i] = NONE64; s_it[i] = NONE64; }
     if (tid == 0) s_nk = 0;
@@ -448,6 +455,21 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
     const bool tk_on = ctl->tk_on != 0;
     __syncthreads();
     if (!run || (a.dbg & 4)) return;
+    // Lower-bound prune.  The source delta f(r_s - delta) - f(r_s) decreases and the
+    // target delta f(r_t + delta) - f(r_t) increases with the relative load (f is
+    // convex), so every candidate of a partition with weight w scores
+    //     d >= LB(delta) = [f(rmax - delta) - f(rmax)] + [f(rmin + delta) - f(rmin)],
+    // delta = w / avg, over the range [rmin, rmax] of r[] (all brokers; absent ones
+    // hold 0, which only widens it).  ub bounds the step's minimum per kind, and the
+    // census never looks past ub + 12 eps (the wave gate below), so a wave whose
+    // partitions all have LB > ub + 16 eps (rounding of d and LB: < 2 eps, see the
+    // (1+R)^2 term of eps) holds neither the minimum nor a near tie: it only counts
+    // its candidates.  With skewed weights that is almost every wave.
+    const double rmin = wave_min(lane < NW ? s_rr[0][lane] : HUGE_VAL);
+    const double rmax = wave_max(lane < NW ? s_rr[1][lane] : -HUGE_VAL);
+    const double fmn = fsq(rmin), fmx = fsq(rmax);
+    const double ubP = a.allow_leader ? (ubL > ubN ? ubL : ubN) : ubN;
+    const double prune_t = (a.dbg & 16) ? HUGE_VAL : ubP + 16.0 * eps;    // dbg 16: no pruning
 
     double wgL = HUGE_VAL, wgN = HUGE_VAL;
     uint32_t fst[NF];
@@ -484,7 +506,40 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
             }
             spec |= sp && base + j < a.shard_end;
         }
-        if (__ballot(spec)) {
+        const bool anyspec = __ballot(spec) != 0;
+        // the lower-bound prune (waves without a rare predicate only)
+        bool need = anyspec;
+        if (!need) {
+            bool nd = false;
+#pragma unroll
+            for (int j = 0; j < PER_LANE; j++) {
+                const double dl = P.wt(j) * inv_avg;
+                const double lb = (fsq(rmax - dl) - fmx) + (fsq(rmin + dl) - fmn);
+                nd |= !(lb > prune_t);
+            }
+            need = __ballot(nd) != 0;
+        }
+        if (!need) {
+            // counts only: the eligible non-replica targets are |set ∩ bl_move| minus the
+            // replicas inside the set (every replica broker is in bl_move), the same
+            // number the scoring path derives from its first-target pick
+            uint32_t cl = 0, cn = 0;
+#pragma unroll
+            for (int j = 0; j < PER_LANE; j++) {
+                const uint32_t m = P.mt(j);
+                const uint32_t nrep = meta_nrep(m), nin = meta_nin(m), set = meta_set(m);
+                const uint32_t nelig = LSETS ? (uint32_t)((const uint16_t*)(s_set + (size_t)set * U))[0]
+                                             : (uint32_t)((const uint16_t*)(a.setrec + (size_t)set * U))[0];
+                const bool ok = base + j < a.shard_end && meta_elig(m) && nrep > 0 && nelig > nin;
+                const uint32_t ne = ok ? nelig - nin : 0u;
+                if (a.allow_leader) cl += ne;
+                cn += ne * (nrep > 0 ? nrep - 1 : 0u);
+            }
+            cL += cl;
+            cN += cn;
+            return;
+        }
+        if (anyspec) {
 #pragma unroll
             for (int j = 0; j < PER_LANE; j++) {
                 const long long p = base + j;

@@ -4,6 +4,7 @@ Bit-exact bar: identical change sequences (step, partition, kind, from, to,
 slot), identical final replica state and broker loads, identical error
 messages; unbalance values within 1e-9 relative (BASELINE.json north_star).
 """
+import os
 import random
 
 import numpy as np
@@ -202,3 +203,72 @@ def test_full_size_properties():
     del loads0, state
     eng.close()
     eng2.close()
+
+
+# ------------------------------------- lower-bound prune of the scan (k_scan)
+
+def _plan_with_scan_dbg(cl, cfg, steps, dbg):
+    old = os.environ.get("KB_DEBUG_SCAN")
+    os.environ["KB_DEBUG_SCAN"] = str(dbg)
+    try:
+        eng = E.Engine(cl, cfg)
+    finally:
+        if old is None:
+            del os.environ["KB_DEBUG_SCAN"]
+        else:
+            os.environ["KB_DEBUG_SCAN"] = old
+    ch, err = eng.plan(steps)
+    st = eng.stats()
+    eng.close()
+    return ch, err, st
+
+
+@pytest.mark.parametrize("variant", ["c3", "c2", "c4s"])
+def test_scan_prune_invariant(variant):
+    """The prune (waves whose lower bound is above ub + 16 eps only count their
+    candidates) changes neither the plan nor the candidate count: same run with the
+    prune disabled (KB_DEBUG_SCAN=16)."""
+    if variant == "c3":
+        cl, cfg, _ = synth.config("c3")
+        steps = 60
+    elif variant == "c2":
+        cl, cfg, _ = synth.config("c2")
+        steps = 100
+    else:
+        nr = np.zeros(200000, np.int64)
+        nr[[5, 90000, 150000]] = 2
+        nr[[7, 100000, 190000]] = 4
+        cl = synth.make_cluster(200000, 400, 3, "zipf", nsets=64, set_size=48, seed=21, num_replicas=nr)
+        cfg = default_cfg(allow_leader=True, min_unbalance=0.0, brokers=list(range(1, 451)))
+        steps = 40
+    ch1, e1, s1 = _plan_with_scan_dbg(cl, cfg, steps, 0)
+    ch0, e0, s0 = _plan_with_scan_dbg(cl, cfg, steps, 16)
+    assert e1 == e0
+    assert [tuple(sorted(c.items())) for c in ch1] == [tuple(sorted(c.items())) for c in ch0]
+    assert s1["candidates"] == s0["candidates"] > 0
+
+
+def test_candidate_count_first_step():
+    """Metric 1 on the first step, counted independently in numpy:
+    sum over eligible partitions of |allowed ∩ bl| - |replicas ∩ allowed| per
+    non-leader slot (steps.go:167-201; no leader step without -allow-leader)."""
+    cl = synth.make_cluster(300000, 500, 3, "zipf", nsets=40, set_size=64, seed=33)
+    cfg = default_cfg(min_unbalance=0.0)
+    eng = E.Engine(cl, cfg)
+    ch, err = eng.plan(1)
+    assert err is None and len(ch) == 1
+    cand = eng.stats()["candidates"]
+    eng.close()
+    reps = cl.replica_ids.reshape(-1, 3)
+    present = np.zeros(int(reps.max()) + 2, bool)
+    present[reps.reshape(-1)] = True
+    want = 0
+    for s in range(len(cl.set_off) - 1):
+        members = cl.set_ids[cl.set_off[s]:cl.set_off[s + 1]]
+        inset = np.zeros_like(present)
+        inset[members] = True
+        n_elig = int((present & inset).sum())
+        rows = reps[cl.set_idx == s]
+        nin = inset[rows].sum(axis=1)
+        want += int(((n_elig - nin) * 2).sum())
+    assert cand == want
