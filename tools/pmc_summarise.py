@@ -1,0 +1,48 @@
+"""Fold the two rocprofv3 PMC passes of tools/pmc_bench.sh into profiles/pmc_traffic.json:
+per kernel, mean FETCH_SIZE / WRITE_SIZE per dispatch (after the first 10), FETCH_SIZE
+doubled as MI355X_MICROARCH.md prescribes for gfx950 16-B streaming reads."""
+import csv
+import glob
+import json
+import sys
+from collections import defaultdict
+
+tag = sys.argv[1] if len(sys.argv) > 1 else "pmcb"
+out = sys.argv[2] if len(sys.argv) > 2 else None
+
+
+def per_kernel(counter):
+    files = glob.glob("gpurun_out/%s_%s/**/*counter_collection.csv" % (tag, counter), recursive=True)
+    vals = defaultdict(dict)
+    for f in files:
+        for r in csv.DictReader(open(f)):
+            if r["Counter_Name"] != counter:
+                continue
+            name = r["Kernel_Name"]
+            k = "k_scan" if "k_scan" in name else "k_step" if "k_step" in name else None
+            if k:
+                d = int(r["Dispatch_Id"])
+                vals[k][d] = vals[k].get(d, 0.0) + float(r["Counter_Value"])
+    res = {}
+    for k, m in vals.items():
+        xs = [m[d] for d in sorted(m)][10:]
+        res[k] = (sum(xs) / max(len(xs), 1), len(xs))
+    return res
+
+
+fetch, write = per_kernel("FETCH_SIZE"), per_kernel("WRITE_SIZE")
+doc = {}
+for k in sorted(set(fetch) & set(write)):
+    rd = 2 * fetch[k][0] * 1024
+    wr = write[k][0] * 1024
+    doc[k] = {"FETCH_SIZE_kb_mean": fetch[k][0], "dispatches": fetch[k][1], "WRITE_SIZE_kb_mean": write[k][0],
+              "read_bytes_per_launch": rd, "write_bytes_per_launch": wr, "traffic_bytes_per_launch": rd + wr}
+doc["method"] = ("rocprofv3 --kernel-trace --pmc FETCH_SIZE, then --pmc WRITE_SIZE (separate passes) over "
+                 "'python3 bench.py --steps 200 --warmup 5 --no-cpu-baseline' (tools/pmc_bench.sh); mean over "
+                 "dispatches after the first 10; FETCH_SIZE doubled per MI355X_MICROARCH.md (gfx950 reports half "
+                 "of 16-B/lane streaming reads); KB = 1024 B. k_step's reads are not 16-B streaming, so its "
+                 "doubled figure is an upper estimate.")
+s = json.dumps(doc, indent=1)
+if out:
+    open(out, "w").write(s + "\n")
+print(s)
