@@ -589,6 +589,18 @@ static void enqueue_scan(kb_engine* e) {
     launch_scan(s, e->rc_dev, e->lds_sets, e->scan_lds, e->st);
 }
 
+// the first step after a full prep has no best keys to bound its minimum: a
+// census-free scan (no list op) plus k_ubinit sets ub to the step's own minima
+static void enqueue_ubinit(kb_engine* e) {
+    if (e->nscan == 0) return;
+    ScanArgs s;
+    fill_scan_args(e, s);
+    s.listwg = 0;
+    s.dbg |= 1;
+    launch_scan(s, e->rc_dev, e->lds_sets, e->scan_lds, e->st);
+    launch_ubinit(e->ctl, scan_recs(e->recs, (int)e->nscan), e->st);
+}
+
 static void enqueue_step(kb_engine* e) {
     StepArgs a;
     fill_step_args(e, a, scan_recs(e->recs, (int)e->nscan), 1);
@@ -715,7 +727,10 @@ static int run_steps(kb_engine* e, int64_t max_steps) {
         const int64_t done = e->h_ctl->steps - steps0;
         if (done >= max_steps) break;
         const int64_t pairs = std::min<int64_t>(kStepBatch, max_steps - done + (prepped ? 0 : 1));
-        for (int64_t s = 0; s < pairs; s++) enqueue_pair(e);
+        for (int64_t s = 0; s < pairs; s++) {
+            if (s == 1 && !prepped) enqueue_ubinit(e);   // pair 0 ran the full prep
+            enqueue_pair(e);
+        }
         mark(e, -1);
         HIPCHK(hipGetLastError());
         HIPCHK(hipMemcpyAsync(e->h_ctl, e->ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, e->st));

@@ -156,6 +156,7 @@ struct DevCtl {
     int32_t pl_kind, pl_from, pl_to, pl_pad;  // pending per-broker list operation
     long long pl_part;
     unsigned long long total_cand, total_cont, total_folds, total_exact_halts;
+    unsigned long long total_retries;   // steps re-scanned with a tightened census bound (k_step)
     // kernel timing (tk_on): summed device-clock durations (100 MHz ticks) and launch
     // counts, {k_scan, k_step}; k_step folds in the scan's interval below
     unsigned long long tk_sum[2], tk_n[2];

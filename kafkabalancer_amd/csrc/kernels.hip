@@ -838,7 +838,7 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
         if (tid < CTL_WORDS) ((uint32_t*)ctl)[tid] = ((const uint32_t*)&C)[tid];
     };
     __shared__ Decision D;
-    __shared__ int s_done, s_i, s_exact_need, s_nT, s_unc, s_nblm;
+    __shared__ int s_done, s_i, s_exact_need, s_retry, s_nT, s_unc, s_nblm;
     __shared__ unsigned long long s_u[NW];
     __shared__ double s_dv[NW];
     __shared__ int s_bs[NW], s_bt[NW];
@@ -909,7 +909,7 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
     __shared__ uint32_t s_lpart;
     __shared__ int s_lrep[MAXR + 1];
     __shared__ unsigned long long s_lsb[64];
-    if (tid == 0) { s_nT = 0; s_done = 0; s_exact_need = 0; s_moved = -1; s_lkind = 0; }
+    if (tid == 0) { s_nT = 0; s_done = 0; s_exact_need = 0; s_retry = 0; s_moved = -1; s_lkind = 0; }
     if (tid < NF) s_first[tid] = NONE32;
     if (tid < 2) s_kc[tid] = 0;
     if (halted != H_RUN) return;
@@ -1243,11 +1243,18 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
                     if (s_first[F_EMPTY_ELIG] != NONE32) {
                         D.status = -1; D.step = step; D.err = E_PANIC; D.part = s_first[F_EMPTY_ELIG]; s_done = 1;
                     } else if (s_flags & 1u) {
-                        D.status = -1; D.step = step; D.err = E_CONT_OVERFLOW; s_done = 1;
+                        // near-tie spill overflow.  If the scan's census gate ran on a loose
+                        // upper bound (ub > g: no surviving best keys, e.g. 4096 brokers with
+                        // tiny weights), tighten it to the minima g just found and re-run
+                        // this step's scan (the state is untouched; the next enqueued pair
+                        // scans again); with ub already at g it is a capacity error
+                        const bool loose = a.use_spill && (C.ub[1] > s_g[1] || (a.allow_leader && C.ub[0] > s_g[0]));
+                        if (loose) s_retry = 1;
+                        else { D.status = -1; D.step = step; D.err = E_CONT_OVERFLOW; s_done = 1; }
                     }
                 }
                 __syncthreads();
-                if (s_done) break;
+                if (s_done || s_retry) break;
                 // (1) the distinct keys of this kind were collected with the records
                 const int ndist = s_nd[kind];
                 const bool fail = s_kfail[kind] != 0;
@@ -1371,6 +1378,17 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
         }
         KB_STAMP(ctl, 4);
 
+        if (s_retry) {
+            if (tid == 0) {
+                C.ub[0] = C.ub[0] < s_g[0] ? C.ub[0] : s_g[0];
+                C.ub[1] = C.ub[1] < s_g[1] ? C.ub[1] : s_g[1];
+                C.ncont = 0;
+                C.cont_overflow = 0;
+                C.total_retries++;
+            }
+            write_back();
+            return;
+        }
         if (s_exact_need) {
             // the bounds cannot decide and some loads are approximate: refold first
             if (tid == 0) {
@@ -2397,6 +2415,43 @@ __global__ __launch_bounds__(1024) void k_touch(double* r, int B, int32_t* blm, 
         r[i] = x; blm[i] = y; posm[i] = z;
     }
     for (int i = threadIdx.x; i < nrec; i += 1024) { const uint4 v = setrec[i]; __syncthreads(); setrec[i] = v; }
+}
+
+// Upper bound of the first step's minimum.  Without a previous step's best keys
+// ub = +inf, which sends every wave of the scan through the near-tie census (and
+// defeats the lower-bound prune); with many near-tied targets per wave (4096
+// brokers, tiny weights) that overflows the spill buffer.  The minima of a
+// census-free scan of the same state are the step minimum g itself, so ub = g is
+// valid for the census gate (tL <= ub + 12 eps) and the prune (LB > ub + 16 eps).
+__global__ __launch_bounds__(256) void k_ubinit(DevCtl* ctl, Recs R) {
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const bool run = ctl->halted == H_RUN && ctl->prepped && ctl->steps < ctl->budget;
+    if (!run) return;                            // uniform over the workgroup
+    double m0 = HUGE_VAL, m1 = HUGE_VAL;
+    for (int i = tid; i < R.n; i += 256) {
+        const RecHdr* h = R.h(i);
+        m0 = h->dmin[0] < m0 ? h->dmin[0] : m0;
+        m1 = h->dmin[1] < m1 ? h->dmin[1] : m1;
+    }
+    m0 = wave_min(m0);
+    m1 = wave_min(m1);
+    __shared__ double s_m[2][4];
+    if (lane == 0) { s_m[0][wid] = m0; s_m[1][wid] = m1; }
+    __syncthreads();
+    if (tid == 0) {
+        for (int w = 1; w < 4; w++) {
+            m0 = s_m[0][w] < m0 ? s_m[0][w] : m0;
+            m1 = s_m[1][w] < m1 ? s_m[1][w] : m1;
+        }
+        m0 = s_m[0][0] < m0 ? s_m[0][0] : m0;
+        m1 = s_m[1][0] < m1 ? s_m[1][0] : m1;
+        if (m0 < ctl->ub[0]) ctl->ub[0] = m0;
+        if (m1 < ctl->ub[1]) ctl->ub[1] = m1;
+    }
+}
+
+void launch_ubinit(DevCtl* ctl, const Recs& R, hipStream_t st) {
+    hipLaunchKernelGGL(k_ubinit, dim3(1), dim3(256), 0, st, ctl, R);
 }
 
 void launch_touch(double* r, int B, int32_t* blm, int32_t* posm, uint4* setrec, int nrec, hipStream_t st) {

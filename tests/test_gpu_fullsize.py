@@ -1,0 +1,165 @@
+"""Full-size GPU parity by properties: BASELINE.json c4 (1M partitions, decommission +
+re-replication) and c5 (10M partitions x 4096 brokers), too large for the oracle's plan.
+
+What each test pins without running the reference's O(P.S.B.|A|) search:
+* the stage order of Balance() (balancer.go:34-44) and each first-index stage's
+  partition sequence (steps.go:70-89 RemoveExtraReplicas, :93-113 AddMissingReplicas,
+  :117-143 MoveDisallowedReplicas), derived independently in numpy;
+* the targets a stage may pick (p.Brokers for remove/add; for a disallowed move, a
+  broker of the load map, i.e. one holding replicas: utils.go:81-90);
+* every move() step strictly improves U (steps.go:222) and the next step's su is the
+  previous step's cu (both the exact unbalance of the same state, within 1e-9);
+* the engine's broker loads after the plan equal, bitwise, getBrokerLoad
+  (utils.go:92-105) of the replayed final state, folded here in partition order.
+"""
+import numpy as np
+import pytest
+
+from kafkabalancer_amd import engine as E
+from kafkabalancer_amd import synth
+
+from helpers import oracle_loads, rel_close
+
+
+def fold_loads(state_flat, off, w, nc):
+    """getBrokerLoad (utils.go:92-105) over a flat partition-major replica array:
+    contributions in partition order, slot order (np.add.at is unbuffered and applies
+    the updates in index order, so each broker's sum is the reference's sequential fold)."""
+    lens = np.diff(off)
+    contrib = np.repeat(w, lens)
+    first = off[:-1][lens > 0]
+    contrib[first] = w[lens > 0] * (lens[lens > 0] + nc[lens > 0]).astype(np.float64)
+    ids = state_flat
+    size = int(ids.max()) + 1 if len(ids) else 1
+    acc = np.zeros(size)
+    np.add.at(acc, ids, contrib)
+    present = np.zeros(size, bool)
+    present[ids] = True
+    return {int(b): float(acc[b]) for b in np.nonzero(present)[0]}
+
+
+def test_fold_loads_matches_sequential_fold():
+    rng = np.random.default_rng(7)
+    P = 3000
+    lens = rng.integers(1, 5, P)
+    off = np.zeros(P + 1, np.int64)
+    off[1:] = np.cumsum(lens)
+    ids = rng.integers(1, 60, int(off[-1]))
+    w = rng.uniform(1.0, 1e6, P) ** -1.1
+    nc = rng.integers(0, 3, P)
+    got = fold_loads(ids, off, w, nc)
+    want = oracle_loads([ids[off[i]:off[i + 1]].tolist() for i in range(P)], w.tolist(), nc.tolist())
+    assert got == want
+
+
+def replay(cl, changes):
+    """Apply a plan (applied semantics: utils.go:166-202 without the aliasing) to the
+    cluster's replica lists; returns (flat, off)."""
+    touched = {}
+    for c in changes:
+        p = c["pidx"]
+        r = touched.get(p)
+        if r is None:
+            r = cl.replica_ids[cl.replica_off[p]:cl.replica_off[p + 1]].tolist()
+            touched[p] = r
+        if c["kind"] == "replace":
+            assert r[c["slot"]] == c["from_"]
+            r[c["slot"]] = c["to"]
+        elif c["kind"] == "remove":
+            assert r[c["slot"]] == c["from_"]
+            del r[c["slot"]]
+        elif c["kind"] == "add":
+            r.append(c["to"])
+        else:
+            raise AssertionError(c)
+    lens = np.diff(cl.replica_off).copy()
+    for p, r in touched.items():
+        lens[p] = len(r)
+    off = np.zeros(cl.n + 1, np.int64)
+    off[1:] = np.cumsum(lens)
+    flat = np.empty(int(off[-1]), np.int64)
+    # untouched partitions keep their slices
+    keep = np.ones(cl.n, bool)
+    keep[list(touched)] = False
+    seg = np.repeat(keep, lens)
+    flat[seg] = cl.replica_ids[np.repeat(keep, np.diff(cl.replica_off))]
+    for p, r in touched.items():
+        flat[off[p]:off[p + 1]] = r
+    return flat, off
+
+
+def check_loads(eng, cl, changes):
+    flat, off = replay(cl, changes)
+    w = np.where(cl.weight == 0, 1.0, cl.weight) if cl.weight[0] == 0 else cl.weight
+    want = fold_loads(flat, off, w, cl.num_consumers)
+    got = eng.loads()
+    bad = [(b, got.get(b), l) for b, l in want.items() if got.get(b) != l]
+    assert not bad, bad[:5]
+
+
+def check_moves(changes):
+    for a, b in zip(changes, changes[1:]):
+        assert rel_close(b["su"], a["cu"]), (a, b)
+    for c in changes:
+        assert c["cu"] < c["su"], c
+
+
+@pytest.mark.gpu
+def test_c4_full_size():
+    """c4: 1M partitions on brokers 1..1000, -broker-ids 1..1200 minus 951..1000,
+    300 partitions want 2 replicas, 300 want 4: 300 removes, 300 adds, then the
+    disallowed replicas move, first partition first."""
+    cl, cfg, desc = synth.config("c4")
+    k = desc["remove"]
+    steps = 2 * k + 150
+    eng = E.Engine(cl, cfg)
+    ch, err = eng.plan(steps)
+    assert err is None, err
+    assert len(ch) == steps
+    nr = cl.num_replicas
+    allowed = np.zeros(1201, bool)
+    allowed[cfg["brokers"]] = True
+    # stage 1: RemoveExtraReplicas, first partition with NumReplicas < len(Replicas)
+    rem = ch[:k]
+    assert all(c["step"] == "RemoveExtraReplicas" and c["kind"] == "remove" for c in rem)
+    assert [c["pidx"] for c in rem] == np.nonzero(nr == 2)[0].tolist()
+    assert all(allowed[c["from_"]] for c in rem)          # picked from p.Brokers
+    # stage 2: AddMissingReplicas
+    add = ch[k:2 * k]
+    assert all(c["step"] == "AddMissingReplicas" and c["kind"] == "add" for c in add)
+    assert [c["pidx"] for c in add] == np.nonzero(nr == 4)[0].tolist()
+    for c in add:
+        p = c["pidx"]
+        assert allowed[c["to"]]
+        assert c["to"] not in cl.replica_ids[cl.replica_off[p]:cl.replica_off[p + 1]].tolist()
+    # stage 3: MoveDisallowedReplicas, partitions in order, one step per disallowed replica
+    dis = ch[2 * k:]
+    reps = cl.replica_ids.reshape(-1, 3)
+    ndis = (~allowed[reps]).sum(axis=1)
+    want = np.repeat(np.arange(cl.n), ndis)[:len(dis)].tolist()
+    assert all(c["step"] == "MoveDisallowedReplicas" and c["kind"] == "replace" for c in dis)
+    assert [c["pidx"] for c in dis] == want
+    held = np.zeros(1201, bool)
+    held[cl.replica_ids] = True
+    for c in dis:
+        assert not allowed[c["from_"]]
+        assert allowed[c["to"]] and held[c["to"]]            # new brokers are never targets
+    check_loads(eng, cl, ch)
+    eng.close()
+
+
+@pytest.mark.gpu
+def test_c5_full_size():
+    """c5: 10M partitions x 4096 brokers (the widest broker table), auto allowed lists:
+    MoveNonLeaders only, each step improving, loads exact after the plan."""
+    cl, cfg, _ = synth.config("c5")
+    eng = E.Engine(cl, cfg)
+    ch, err = eng.plan(12)
+    assert err is None, err
+    assert len(ch) == 12
+    assert all(c["step"] == "MoveNonLeaders" and c["kind"] == "replace" and c["slot"] >= 1 for c in ch)
+    check_moves(ch)
+    st = eng.stats()
+    assert st["n_brokers"] == 4096
+    check_loads(eng, cl, ch)
+    eng.close()
