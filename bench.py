@@ -151,6 +151,7 @@ def main():
                      "traffic_source": "profiles/pmc_traffic.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE per launch)"},
         "kernels_us_per_step": {k: 1e3 * v[0] / max(v[1], 1) for k, v in tk.items()},
         "kernel_timing_steps": kt_steps,
+        "engine_events": {k: st1[k] - st0[k] for k in ("retries", "refreshes", "exact_halts", "exact_folds")},
     }
     if args.stamps:
         st = eng.stamps()

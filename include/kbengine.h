@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define KB_ABI_VERSION 2
+#define KB_ABI_VERSION 3
 
 /* step indices == position in the reference's steps table (balancer.go:34-44) */
 enum kb_step {
@@ -133,6 +133,8 @@ typedef struct {
     int64_t refreshes;              /* exact refolds of the approximate loads (k_refresh) */
     int64_t exact_halts;            /* steps that needed exact loads to decide */
     int64_t scan_workgroups;        /* k_scan workgroups (one record each) */
+    int64_t retries;                /* steps re-scanned with the census bound tightened to the
+                                       step minimum after a near-tie spill overflow (ABI 3) */
 } kb_stats;
 
 typedef struct kb_engine kb_engine;

@@ -102,6 +102,7 @@ struct kb_engine {
     int64_t klaunch[TK_N] = {0, 0, 0};
     int64_t refreshes = 0;
     int dbg_scan = 0;
+    bool ub_mode = false;          // a step re-scanned: enqueue the conditional bound pass per scan
     std::string last_err;
 };
 
@@ -529,6 +530,7 @@ static void fill_scan_args(kb_engine* e, ScanArgs& s) {
     s.R = scan_recs(e->recs, (int)e->nscan); s.cont = e->cont; s.cont_cap = e->cont_cap;
     s.listwg = e->integral ? 0 : 1;
     s.dbg = e->dbg_scan;
+    s.ubpass = 0;
     s.L = e->L;
 }
 
@@ -597,8 +599,9 @@ static void enqueue_ubinit(kb_engine* e) {
     fill_scan_args(e, s);
     s.listwg = 0;
     s.dbg |= 1;
+    s.ubpass = 1;
     launch_scan(s, e->rc_dev, e->lds_sets, e->scan_lds, e->st);
-    launch_ubinit(e->ctl, scan_recs(e->recs, (int)e->nscan), e->st);
+    launch_ubinit(e->ctl, scan_recs(e->recs, (int)e->nscan), e->allow_leader, e->st);
 }
 
 static void enqueue_step(kb_engine* e) {
@@ -728,7 +731,9 @@ static int run_steps(kb_engine* e, int64_t max_steps) {
         if (done >= max_steps) break;
         const int64_t pairs = std::min<int64_t>(kStepBatch, max_steps - done + (prepped ? 0 : 1));
         for (int64_t s = 0; s < pairs; s++) {
-            if (s == 1 && !prepped) enqueue_ubinit(e);   // pair 0 ran the full prep
+            // pair 0 ran the full prep; once a step had to re-scan (no surviving best
+            // keys bound the next minimum), every scan gets the conditional bound pass
+            if ((s == 1 && !prepped) || (e->ub_mode && (s > 0 || prepped))) enqueue_ubinit(e);
             enqueue_pair(e);
         }
         mark(e, -1);
@@ -737,6 +742,7 @@ static int run_steps(kb_engine* e, int64_t max_steps) {
         HIPCHK(hipStreamSynchronize(e->st));
         harvest(e);
         const DevCtl& c = *e->h_ctl;
+        if (c.total_retries > 0) e->ub_mode = true;
         if (c.halted == H_DONE) break;
         if (c.halted == H_NEED_EXACT || (c.want_refresh && c.steps - steps0 < max_steps)) {
             const int logpos = c.logpos;
@@ -855,6 +861,7 @@ extern "C" int kb_engine_stats(kb_engine* e, kb_stats* o) {
     o->refreshes = e->refreshes;
     o->exact_halts = (int64_t)c.total_exact_halts;
     o->scan_workgroups = e->nscan;
+    o->retries = (int64_t)c.total_retries;
     return KB_OK;
 }
 
@@ -917,6 +924,7 @@ extern "C" int kb_engine_bench_scan(kb_engine* e, int iters, double* avg_us) {
     hipEvent_t a, b;
     HIPCHK(hipEventCreate(&a));
     HIPCHK(hipEventCreate(&b));
+    if (e->ub_mode) enqueue_ubinit(e);                // an open census bound: close it first
     enqueue_scan(e);                                  // warm
     // KB_PROBE_INTERLEAVE (diagnostic): 1 = an empty one-workgroup kernel between the
     // scans, 2 = one that rewrites the scan's tables (as k_step does); each scan is

@@ -454,7 +454,8 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
     const int heavy = ctl->heavy, nblm = ctl->nblm;
     const bool tk_on = ctl->tk_on != 0;
     __syncthreads();
-    if (!run || (a.dbg & 4)) return;
+    const bool ub_open = ubN == HUGE_VAL || (a.allow_leader && ubL == HUGE_VAL);
+    if (!run || (a.dbg & 4) || (a.ubpass && !ub_open)) return;
     // Lower-bound prune.  The source delta f(r_s - delta) - f(r_s) decreases and the
     // target delta f(r_t + delta) - f(r_t) increases with the relative load (f is
     // convex), so every candidate of a partition with weight w scores
@@ -2423,7 +2424,9 @@ __global__ __launch_bounds__(1024) void k_touch(double* r, int B, int32_t* blm, 
 // brokers, tiny weights) that overflows the spill buffer.  The minima of a
 // census-free scan of the same state are the step minimum g itself, so ub = g is
 // valid for the census gate (tL <= ub + 12 eps) and the prune (LB > ub + 16 eps).
-__global__ __launch_bounds__(256) void k_ubinit(DevCtl* ctl, Recs R) {
+// Only a bound that is +inf is set (the records are this pass's only when a bound
+// was open: otherwise the bound pass returned at once and they are stale).
+__global__ __launch_bounds__(256) void k_ubinit(DevCtl* ctl, Recs R, int allow_leader) {
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const bool run = ctl->halted == H_RUN && ctl->prepped && ctl->steps < ctl->budget;
     if (!run) return;                            // uniform over the workgroup
@@ -2445,13 +2448,16 @@ __global__ __launch_bounds__(256) void k_ubinit(DevCtl* ctl, Recs R) {
         }
         m0 = s_m[0][0] < m0 ? s_m[0][0] : m0;
         m1 = s_m[1][0] < m1 ? s_m[1][0] : m1;
-        if (m0 < ctl->ub[0]) ctl->ub[0] = m0;
-        if (m1 < ctl->ub[1]) ctl->ub[1] = m1;
+        const bool open1 = ctl->ub[1] == HUGE_VAL, open0 = allow_leader && ctl->ub[0] == HUGE_VAL;
+        if (open0 || open1) {                    // the bound pass ran on this state
+            if (open0) ctl->ub[0] = m0;
+            if (open1) ctl->ub[1] = m1;
+        }
     }
 }
 
-void launch_ubinit(DevCtl* ctl, const Recs& R, hipStream_t st) {
-    hipLaunchKernelGGL(k_ubinit, dim3(1), dim3(256), 0, st, ctl, R);
+void launch_ubinit(DevCtl* ctl, const Recs& R, int allow_leader, hipStream_t st) {
+    hipLaunchKernelGGL(k_ubinit, dim3(1), dim3(256), 0, st, ctl, R, allow_leader);
 }
 
 void launch_touch(double* r, int B, int32_t* blm, int32_t* posm, uint4* setrec, int nrec, hipStream_t st) {

@@ -33,6 +33,8 @@ struct ScanArgs {
     Contender* cont;          // spill buffer
     uint32_t cont_cap;
     int listwg;               // 1: the last workgroup applies the pending list op
+    int ubpass;               // 1: census-free bound pass (k_ubinit follows); returns at once
+                              //    unless a relevant upper bound is +inf
     int dbg;                  // diagnostic only (KB_DEBUG_SCAN): 1 = skip the census
     Lists L;
 };
@@ -100,7 +102,7 @@ int scan_blocks_per_cu(int rc, bool lds_sets, size_t lds_bytes);
 void launch_step(const StepArgs& a, hipStream_t st);
 int step_static_lds();
 // diagnostic: one workgroup rewrites the given tables in place (n = 0: nothing)
-void launch_ubinit(DevCtl* ctl, const Recs& R, hipStream_t st);
+void launch_ubinit(DevCtl* ctl, const Recs& R, int allow_leader, hipStream_t st);
 void launch_touch(double* r, int B, int32_t* blm, int32_t* posm, uint4* setrec, int nrec, hipStream_t st);
 void launch_listop(DevCtl* ctl, const Lists& L, hipStream_t st);
 void launch_refresh(const RefreshArgs& a, hipStream_t st);
