@@ -1050,7 +1050,8 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
         // anything else takes the general path below
         __shared__ int s_fast;
         if (tid == 0) {
-            int fast = !C.list_overflow && !s_fm && !a.rebalance && !(s_flags & 1u) && !a.exact_unb;
+            const bool census_off = C.ub[0] == -HUGE_VAL || C.ub[1] == -HUGE_VAL;
+            int fast = !C.list_overflow && !s_fm && !a.rebalance && !(s_flags & 1u) && !a.exact_unb && !census_off;
             Decision d;
             d.status = 0; d.step = -1; d.kind = 0; d.slot = -1; d.part = -1; d.from = -1; d.to = -1;
             d.su = U0h; d.cu = U0h; d.w = 0.0; d.exact = 0; d.err = E_NONE; d.err_broker = -1; d.pad = 0;
@@ -1243,6 +1244,8 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
                 if (tid == 0) {
                     if (s_first[F_EMPTY_ELIG] != NONE32) {
                         D.status = -1; D.step = step; D.err = E_PANIC; D.part = s_first[F_EMPTY_ELIG]; s_done = 1;
+                    } else if (a.use_spill && (C.ub[0] == -HUGE_VAL || C.ub[1] == -HUGE_VAL)) {
+                        s_retry = 1;                 // census was off (after a first-index stage)
                     } else if (s_flags & 1u) {
                         // near-tie spill overflow.  If the scan's census gate ran on a loose
                         // upper bound (ub > g: no surviving best keys, e.g. 4096 brokers with
@@ -1381,8 +1384,15 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
 
         if (s_retry) {
             if (tid == 0) {
-                C.ub[0] = C.ub[0] < s_g[0] ? C.ub[0] : s_g[0];
-                C.ub[1] = C.ub[1] < s_g[1] ? C.ub[1] : s_g[1];
+                if (C.ub[0] == -HUGE_VAL || C.ub[1] == -HUGE_VAL) {
+                    // the scan pruned every wave: its minima are not the step's; open the
+                    // bound (the host's bound pass, or a full census, closes it)
+                    C.ub[0] = HUGE_VAL;
+                    C.ub[1] = HUGE_VAL;
+                } else {
+                    C.ub[0] = C.ub[0] < s_g[0] ? C.ub[0] : s_g[0];
+                    C.ub[1] = C.ub[1] < s_g[1] ? C.ub[1] : s_g[1];
+                }
                 C.ncont = 0;
                 C.cont_overflow = 0;
                 C.total_retries++;
@@ -1726,7 +1736,10 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
                 if (!(ep > 1e-300)) ep = 1e-300;
                 C.S = S; C.avg = avg; C.inv_avg = iav; C.U0 = U0;
                 C.V = V; C.eps = ep; C.E = E; C.nblm = nblm;
-                C.ub[0] = ub0; C.ub[1] = ub1;
+                // after a first-index stage (Remove/Add/Disallowed) the next step is most
+                // likely one too: no census (ub = -inf; k_step re-scans if move() is reached)
+                const bool sup = a.use_spill && do_res && D.status == 1 && D.step >= 3 && D.step <= 5;
+                C.ub[0] = sup ? -HUGE_VAL : ub0; C.ub[1] = sup ? -HUGE_VAL : ub1;
                 C.want_refresh = (epsl > epsf || C.ndirty >= 256) ? 1 : 0;
                 C.ncont = 0;
                 C.cont_overflow = 0;
@@ -2027,7 +2040,8 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
         if (!(ep > 1e-300)) ep = 1e-300;
         C.S = S; C.avg = avg; C.inv_avg = iav; C.U0 = U0;
         C.V = V; C.eps = ep; C.E = E; C.nblm = nblm;
-        C.ub[0] = ub0; C.ub[1] = ub1;
+        const bool sup = a.use_spill && do_res && !full && D.status == 1 && D.step >= 3 && D.step <= 5;
+        C.ub[0] = sup ? -HUGE_VAL : ub0; C.ub[1] = sup ? -HUGE_VAL : ub1;
         C.want_refresh = (epsl > epsf || C.ndirty >= 256) ? 1 : 0;
         C.ncont = 0;
         C.cont_overflow = 0;
