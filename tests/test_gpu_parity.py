@@ -166,6 +166,23 @@ def test_scaled_configs(variant):
     check_plan(pl, cfg, 12)
 
 
+@pytest.mark.parametrize("allow_leader", [False, True])
+def test_stage_transition_into_move(allow_leader):
+    """RemoveExtraReplicas / AddMissingReplicas steps, then move(): the scans after a
+    first-index stage skip the near-tie census (ub = -inf) and the first move() step
+    re-scans with the bound opened (k_step retry); the plan must not notice."""
+    nr = np.zeros(2000, np.int64)
+    nr[[11, 700]] = 2
+    nr[[5, 1300, 1999]] = 4
+    cl = synth.make_cluster(2000, 40, 3, "zipf", seed=41, with_names=True, num_replicas=nr)
+    cfg = default_cfg(allow_leader=allow_leader, min_unbalance=0.0)
+    pl = synth.to_plist(cl)
+    ech = check_plan(pl, cfg, 12)
+    steps = [c["step"] for c in ech]
+    assert steps[:5] == ["RemoveExtraReplicas"] * 2 + ["AddMissingReplicas"] * 3
+    assert all(s in ("MoveLeaders", "MoveNonLeaders") for s in steps[5:]) and len(steps) == 12
+
+
 def test_many_brokers_sorting():
     """4096-entry broker table (c5 width) with explicit broker ids, tiny P for the oracle."""
     cl = synth.make_cluster(120, 4096, 3, "int", seed=5, with_names=True)
