@@ -103,6 +103,23 @@ __device__ __forceinline__ double fold_lds(const double* x, int n, double acc = 
     return acc;
 }
 
+// Sequential fold of term_x(x[k], avg) in order.  The terms of a batch are
+// independent (their IEEE divisions overlap); only the adds form the chain.
+constexpr int TERM_BATCH = 16;
+__device__ __forceinline__ double fold_terms_lds(const double* x, int n, double avg) {
+    double U = 0.0;
+    int k = 0;
+    for (; k + TERM_BATCH <= n; k += TERM_BATCH) {
+        double t[TERM_BATCH];
+#pragma unroll
+        for (int i = 0; i < TERM_BATCH; i++) t[i] = term_x(x[k + i], avg);
+#pragma unroll
+        for (int i = 0; i < TERM_BATCH; i++) U += t[i];
+    }
+    for (; k < n; k++) U += term_x(x[k], avg);
+    return U;
+}
+
 // getUnbalanceBL (utils.go:119-147) of the bl order with bl[ps] = Ls and
 // bl[pt] = Lt (steps.go:185,207): two sequential folds, the reference's order.
 __device__ double exact_unbalance_lds(const double* Lm, int n, int ps, int pt, double Ls, double Lt) {
@@ -1196,9 +1213,7 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
                 if (tid == 0) {
                     const double S = fold_lds(s_Lm, nblm0);
                     const double avg = S / (double)nblm0;
-                    double U = 0.0;
-                    for (int k = 0; k < nblm0; k++) U += term_x(s_Lm[k], avg);
-                    s_sux = U;
+                    s_sux = fold_terms_lds(s_Lm, nblm0, avg);
                     atomicAdd(&C.total_folds, 1ull);
                 }
                 __syncthreads();
