@@ -251,6 +251,9 @@ static int addpl(or_plist *pl, int64_t pidx, int64_t b, int sem, or_result *res,
 
 /* ------------------------------------------------------------- the steps */
 
+static int g_threads = 1;                 /* see or_set_threads (move_impl) */
+void or_set_threads(int n) { g_threads = n < 1 ? 1 : n; }
+
 static int validate_weights(or_plist *pl, or_result *res) {      /* steps.go:7-23 */
     char ps[512], m[700];
     int has = pl->parts[0].weight != 0;
@@ -368,7 +371,32 @@ static int move_disallowed(or_plist *pl, int sem, or_result *res) { /* steps.go:
     int64_t nbl; bload *bl = get_bl(&m, &nbl);
     int64_t *A = (int64_t *)malloc((size_t)(nbl ? nbl : 1) * sizeof(int64_t));
     int rc = 0;
-    for (int64_t i = 0; i < pl->n && rc == 0; i++) {
+    int64_t i_start = 0;
+    if (g_threads > 1 && pl->n > 1) {
+        /* the first partition holding a replica outside getBrokerListByLoadBL's list
+         * (every earlier one passes untouched); the loop below starts there */
+        int64_t first = pl->n;
+#pragma omp parallel num_threads(g_threads)
+        {
+            int64_t *A2 = (int64_t *)malloc((size_t)(nbl ? nbl : 1) * sizeof(int64_t));
+            int64_t mine = pl->n;
+#pragma omp for schedule(static)
+            for (int64_t i = 0; i < pl->n; i++) {
+                if (i >= mine) continue;
+                const or_partition *p = &pl->parts[i];
+                int64_t na = 0;
+                for (int64_t k = 0; k < nbl; k++)
+                    if (in_list(p->brokers.a, p->brokers.len, bl[k].id)) A2[na++] = bl[k].id;
+                for (int64_t r = 0; r < p->replicas.len; r++)
+                    if (!in_list(A2, na, p->replicas.a[r])) { mine = i; break; }
+            }
+#pragma omp critical
+            if (mine < first) first = mine;
+            free(A2);
+        }
+        i_start = first;
+    }
+    for (int64_t i = i_start; i < pl->n && rc == 0; i++) {
         or_partition *p = &pl->parts[i];
         int64_t na = 0;                       /* getBrokerListByLoadBL (utils.go:81-90) */
         for (int64_t k = 0; k < nbl; k++)
@@ -410,9 +438,16 @@ static int distribute_leaders(or_plist *pl, const or_config *cfg, int sem, or_re
     if (!(su < cfg->min_unbalance)) {
         if (n == 0) { set_err(res, 6, "panic: index out of range"); free(bl); return -1; }
         int64_t heavy = bl[n - 1].id;
+        /* pp is built over EVERY partition first (steps.go:257-262): p.Replicas[0]
+         * panics on any empty list, wherever it sits relative to the first pick */
+        for (int64_t i = 0; i < pl->n; i++)
+            if (pl->parts[i].replicas.len == 0) {
+                set_err(res, 6, "panic: index out of range");
+                free(bl);
+                return -1;
+            }
         for (int64_t i = 0; i < pl->n; i++) {
             or_partition *p = &pl->parts[i];
-            if (p->replicas.len == 0) { set_err(res, 6, "panic: index out of range"); rc = -1; break; }
             if (p->replicas.a[0] != heavy) continue;
             if (p->num_replicas < cfg->min_replicas) continue;
             rc = replacepl(pl, i, p->replicas.a[0], bl[0].id, sem, res, 6, OR_REPLACE);
@@ -424,45 +459,92 @@ static int distribute_leaders(or_plist *pl, const or_config *cfg, int sem, or_re
     return rc;
 }
 
-/* move (steps.go:210-297).  limit < 0 => all partitions. */
-static int move_impl(or_plist *pl, const or_config *cfg, int leaders, int sem, or_result *res,
-                     int64_t limit, int64_t *ncand, double *cu_out) {
-    int64_t n; bload *bl = loads_with_cfg(pl, cfg, &n);
-    double su = unbalance_bl(bl, n), cu = su;
-    int64_t cp = -1, cr = 0, cb = 0, cnt = 0;
-    int64_t np = limit < 0 || limit > pl->n ? pl->n : limit;
-    for (int64_t i = 0; i < np; i++) {
+/* Threads used by move() and MoveDisallowedReplicas' first-hit search (default 1:
+ * the plain sequential restatement).  With T > 1 the partitions are split into T
+ * contiguous chunks in order; every chunk runs the reference's own loop on a
+ * private copy of bl, and the chunk results are merged in chunk order, which
+ * yields exactly the sequential result: move() keeps the FIRST strict minimum in
+ * (partition, slot, bl) order starting from cu = su (steps.go:163,211), i.e. the
+ * lexicographic minimum of (u, iteration index) over the candidates with u < su,
+ * and a panic is the one the sequential loop meets first.  Used to generate the
+ * large golden plans (tests/golden/gen_scale.py); tests/test_oracle.py checks it
+ * against T = 1. */
+
+/* one chunk [i0, i1) of move()'s partition loop on bl (restored on return).
+ * Returns 0, or the step error (1 = slice bounds panic, 2 = assertion) with the
+ * partition in *ep. */
+static int move_chunk(const or_plist *pl, const or_config *cfg, int leaders, bload *bl, int64_t n,
+                      int64_t i0, int64_t i1, double *cu, int64_t *cp, int64_t *cr, int64_t *cb,
+                      int64_t *cnt, int64_t *ep) {
+    for (int64_t i = i0; i < i1; i++) {
         const or_partition *p = &pl->parts[i];
         if (p->num_replicas < cfg->min_replicas) continue;
         int64_t lo = 1, hi = p->replicas.len;
         if (leaders) { lo = 0; hi = 1; }
-        if (p->replicas.len < lo || p->replicas.len < hi) {   /* Go slice bounds panic */
-            set_err(res, leaders ? 7 : 8, "panic: slice bounds out of range");
-            free(bl); return -1;
-        }
+        if (p->replicas.len < lo || p->replicas.len < hi) { *ep = i; return 1; }  /* Go slice bounds panic */
         for (int64_t s = lo; s < hi; s++) {
             int64_t r = p->replicas.a[s];
             int64_t ridx = -1; double rload = 0;
             for (int64_t k = 0; k < n; k++)
                 if (bl[k].id == r) { ridx = k; rload = bl[k].load; bl[k].load -= p->weight; }
-            if (ridx == -1) {
-                set_err(res, leaders ? 7 : 8, "assertion failed: replica not in broker loads");
-                free(bl); return -1;
-            }
+            if (ridx == -1) { *ep = i; return 2; }
             for (int64_t k = 0; k < n; k++) {
                 if (!in_list(p->brokers.a, p->brokers.len, bl[k].id)) continue;
                 if (in_list(p->replicas.a, p->replicas.len, bl[k].id)) continue;
                 double bload_ = bl[k].load;
                 bl[k].load += p->weight;
                 double u = unbalance_bl(bl, n);
-                cnt++;
-                if (u < cu) { cu = u; cp = i; cr = r; cb = bl[k].id; }
+                (*cnt)++;
+                if (u < *cu) { *cu = u; *cp = i; *cr = r; *cb = bl[k].id; }
                 bl[k].load = bload_;
             }
             bl[ridx].load = rload;
         }
     }
+    return 0;
+}
+
+/* move (steps.go:145-232).  limit < 0 => all partitions. */
+static int move_impl(or_plist *pl, const or_config *cfg, int leaders, int sem, or_result *res,
+                     int64_t limit, int64_t *ncand, double *cu_out) {
+    int64_t n; bload *bl = loads_with_cfg(pl, cfg, &n);
+    double su = unbalance_bl(bl, n), cu = su;
+    int64_t cp = -1, cr = 0, cb = 0, cnt = 0;
+    int64_t np = limit < 0 || limit > pl->n ? pl->n : limit;
+    int err = 0;
+    int T = g_threads;
+    if (T > np) T = np > 0 ? (int)np : 1;
+    if (T <= 1) {
+        int64_t ep = -1;
+        err = move_chunk(pl, cfg, leaders, bl, n, 0, np, &cu, &cp, &cr, &cb, &cnt, &ep);
+    } else {
+        double *tcu = (double *)malloc((size_t)T * sizeof(double));
+        int64_t *tv = (int64_t *)malloc((size_t)T * 5 * sizeof(int64_t));
+        int *terr = (int *)calloc((size_t)T, sizeof(int));
+#pragma omp parallel for num_threads(T) schedule(static, 1)
+        for (int t = 0; t < T; t++) {
+            bload *b2 = (bload *)malloc((size_t)(n ? n : 1) * sizeof(bload));
+            if (n) memcpy(b2, bl, (size_t)n * sizeof(bload));
+            int64_t i0 = np * t / T, i1 = np * (t + 1) / T;
+            int64_t *v = tv + 5 * t;     /* cp, cr, cb, cnt, ep */
+            tcu[t] = su; v[0] = -1; v[1] = v[2] = v[3] = 0; v[4] = -1;
+            terr[t] = move_chunk(pl, cfg, leaders, b2, n, i0, i1, &tcu[t], &v[0], &v[1], &v[2], &v[3], &v[4]);
+            free(b2);
+        }
+        for (int t = 0; t < T && !err; t++) {
+            int64_t *v = tv + 5 * t;
+            cnt += v[3];
+            if (terr[t]) { err = terr[t]; break; }          /* the first panic in order */
+            if (v[0] >= 0 && tcu[t] < cu) { cu = tcu[t]; cp = v[0]; cr = v[1]; cb = v[2]; }
+        }
+        free(tcu); free(tv); free(terr);
+    }
     free(bl);
+    if (err) {
+        set_err(res, leaders ? 7 : 8, err == 1 ? "panic: slice bounds out of range"
+                                                : "assertion failed: replica not in broker loads");
+        return -1;
+    }
     if (ncand) *ncand = cnt;
     if (cu_out) *cu_out = cu;
     if (limit >= 0) return 0;

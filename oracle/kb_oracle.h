@@ -92,6 +92,10 @@ void or_format_float(double x, char *buf);
 
 void or_free(void *p);
 
+/* Worker threads of move() / MoveDisallowedReplicas' search (default 1).  Any
+ * count gives the identical result (chunked in order, merged in order). */
+void or_set_threads(int n);
+
 /* Build a partition list from flat arrays.  Brokers lists are deduplicated
  * into sets; partitions with the same set_idx share one slice (as FillDefaults
  * makes them share in Go).  set_idx < 0 => nil Brokers. rep_nil may be NULL. */

@@ -80,6 +80,8 @@ def lib():
         L.or_unbalance.restype = C.c_double
         L.or_format_float.argtypes = [C.c_double, C.c_char_p]
         L.or_free.argtypes = [C.c_void_p]
+        L.or_set_threads.argtypes = [C.c_int]
+        L.or_set_threads.restype = None
         _lib = L
     return _lib
 
@@ -250,6 +252,11 @@ def move_sample(opl, cfg, leaders, max_parts):
     cu = C.c_double()
     n = lib().or_move_sample(opl.pl, C.byref(make_cfg(cfg)), int(leaders), max_parts, C.byref(cu))
     return n, cu.value
+
+
+def set_threads(n):
+    """Worker threads of the oracle's move() (identical results for any n)."""
+    lib().or_set_threads(int(n))
 
 
 def format_float(x):

@@ -140,6 +140,9 @@ def balance(pl, cfg):
         su = unbalance(bl)
         if not su < cfg["min_unbalance"]:
             heavy = bl[-1][0]
+            # pp is built over every partition first (steps.go:257-262)
+            if any(not p["replicas"] for p in pl):
+                raise StepError("ReassignLeaders: panic")
             for i, p in enumerate(pl):
                 if p["replicas"][0] != heavy or p["num_replicas"] < cfg["min_replicas"]:
                     continue

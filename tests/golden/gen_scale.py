@@ -1,0 +1,115 @@
+"""Generate the large-scale golden plans tests/golden/scale_<name>.json from the CPU
+oracle (oracle/kb_oracle.c, threaded move(): identical results for any thread count,
+tests/test_oracle.py::test_threaded_oracle_matches_sequential).
+
+These pin the engine's parity far beyond what the oracle can replay inside a test:
+c3-shaped (1000 brokers, 256 allowed sets of 64, Zipf weights, -allow-leader and
+without), a 4096-broker auto-list case in both weight modes (Zipf and the uniform
+exact-tie worst case) and a c4-shaped broker add/remove case that runs through
+RemoveExtraReplicas, AddMissingReplicas and MoveDisallowedReplicas into move().
+
+Each fixture stores the synth parameters, a SHA-256 of the generated input arrays
+(the GPU test regenerates the input and checks it first), the change list
+[step, pidx, kind, from, to, slot] and su / cu of every step as exact floats.
+
+Run:  python tests/golden/gen_scale.py [case ...]   (all cases: ~20 min on 8 cores)
+"""
+import hashlib
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+
+from oracle import oracle as O  # noqa: E402
+
+from kafkabalancer_amd import synth  # noqa: E402
+
+
+def c4_cfg():
+    return dict(O.default_cfg(), min_unbalance=0.0,
+                brokers=[b for b in range(1, 241) if not 196 <= b <= 200])
+
+
+def c4_nr(P, seed):
+    rng = np.random.default_rng(seed)
+    nr = np.zeros(P, np.int64)
+    pick = rng.choice(P, size=60, replace=False)
+    nr[pick[:30]] = 2
+    nr[pick[30:]] = 4
+    return nr
+
+
+# name -> (make_cluster kwargs, cfg, steps)
+CASES = {
+    "c3s_leader": (dict(P=20000, B=1000, rf=3, weights="zipf", nsets=256, set_size=64, seed=0x5EED1003),
+                   dict(O.default_cfg(), allow_leader=True, min_unbalance=0.0), 200),
+    "c3s_nonleader": (dict(P=20000, B=1000, rf=3, weights="zipf", nsets=256, set_size=64, seed=0x5EED2003),
+                      dict(O.default_cfg(), min_unbalance=0.0), 200),
+    "b4096_zipf": (dict(P=3000, B=4096, rf=3, weights="zipf", seed=0x5EED1005),
+                   dict(O.default_cfg(), min_unbalance=0.0), 12),
+    "b4096_uniform": (dict(P=3000, B=4096, rf=3, weights="uniform", seed=0x5EED2005),
+                      dict(O.default_cfg(), min_unbalance=0.0), 12),
+    "c4s": (dict(P=20000, B=200, rf=3, weights="zipf", seed=0x5EED1004, nr_seed=0x5EED1104),
+            c4_cfg(), 1700),
+}
+
+
+def build(params):
+    kw = dict(params)
+    nr_seed = kw.pop("nr_seed", None)
+    P = kw.pop("P")
+    B = kw.pop("B")
+    nr = c4_nr(P, nr_seed) if nr_seed is not None else None
+    return synth.make_cluster(P, B, kw.pop("rf"), kw.pop("weights"), nsets=kw.pop("nsets", 0),
+                              set_size=kw.pop("set_size", 0), seed=kw.pop("seed"), with_names=True,
+                              num_replicas=nr)
+
+
+def input_hash(cl):
+    h = hashlib.sha256()
+    for a in (cl.replica_ids, cl.replica_off, cl.weight, cl.num_replicas, cl.set_ids, cl.set_off, cl.set_idx):
+        if a is not None:
+            h.update(np.ascontiguousarray(a).tobytes())
+    return h.hexdigest()
+
+
+def generate(name, threads):
+    params, cfg, steps = CASES[name]
+    cl = build(params)
+    O.set_threads(threads)
+    o = O.OraclePL(synth.to_plist(cl))
+    changes, su, cu, err = [], [], [], None
+    t0 = time.time()
+    for k in range(steps):
+        r = O.balance(o, cfg, O.SEM_APPLIED)
+        if r["status"] == 0:
+            break
+        if r["status"] < 0:
+            err = r["err"]
+            break
+        changes.append([r["step"], r["pidx"], r["kind"], r["from_"], r["to"], r["slot"]])
+        su.append(r["su"])
+        cu.append(r["cu"])
+        if k % 20 == 0:
+            print(name, k, r["step"], "%.0fs" % (time.time() - t0), flush=True)
+    # final replicas of every partition some change touched
+    touched = sorted({c[1] for c in changes})
+    doc = {"name": name, "generator": "tests/golden/gen_scale.py (oracle/kb_oracle.c, %d threads)" % threads,
+           "params": params, "cfg": cfg, "steps": steps, "input_sha256": input_hash(cl),
+           "changes": changes, "su": su, "cu": cu, "err": err,
+           "final": {str(i): o.replicas(i) for i in touched}}
+    with open(os.path.join(HERE, "scale_%s.json" % name), "w") as f:
+        json.dump(doc, f, separators=(",", ":"))
+    print("wrote", name, len(changes), "changes in %.0fs" % (time.time() - t0), flush=True)
+
+
+if __name__ == "__main__":
+    names = sys.argv[1:] or list(CASES)
+    for n in names:
+        generate(n, os.cpu_count() or 1)

@@ -198,28 +198,42 @@ def test_full_size_properties():
     eng = E.Engine(cl, cfg)
     ch1, err = eng.plan(40)
     assert err is None and len(ch1) == 40
-    # the reported unbalance values are the exact folds (within 1e-9) of the state they scored
-    loads0 = None
     # determinism: a second engine on the same input produces the identical plan
     eng2 = E.Engine(cl, cfg)
     ch2, _ = eng2.plan(40)
     assert [tuple(sorted(c.items())) for c in ch1] == [tuple(sorted(c.items())) for c in ch2]
-    # loads stay the exact partition-ordered fold of the final state
-    state = eng.state() if cl.n <= 2000 else None
+    # loads stay the exact partition-ordered fold (getBrokerLoad, utils.go:92-105) of
+    # the replayed final state
     got = eng.loads()
     reps = cl.replica_ids.reshape(-1, 3).copy()
     for c in ch1:
         row = reps[c["pidx"]]
         row[c["slot"]] = c["to"]
-    w = cl.weight
-    want = oracle_loads(reps.tolist(), w.tolist(), [0] * cl.n)
+    want = oracle_loads(reps.tolist(), cl.weight.tolist(), [0] * cl.n)
     for b, l in want.items():
         assert got[b] == l, (b, got[b], l)
-    # su of step k+1 equals the exact unbalance of the state after step k
-    assert rel_close(eng.unbalance(), eng.unbalance())
-    del loads0, state
+    # the engine's unbalance is the oracle's getUnbalanceBL fold (utils.go:119-147) of
+    # those loads in getBL order (utils.go:107-117), bit for bit
+    bl = sorted(want.items(), key=lambda kv: (kv[1], kv[0]))
+    u_exact = O.unbalance(np.array([l for _, l in bl]))
+    assert eng.unbalance() == u_exact
+    # and the next step starts from it: su of step 41 is that fold (exact, or within 1e-9)
+    ch3, err = eng.plan(1)
+    assert err is None and len(ch3) == 1
+    if ch3[0]["exact"]:
+        assert ch3[0]["su"] == u_exact
+    assert rel_close(ch3[0]["su"], u_exact)
     eng.close()
     eng2.close()
+
+
+def test_distribute_leaders_empty_partition_after_pick():
+    """distributeLeaders builds pp over every partition (steps.go:257-262): an empty
+    Replicas anywhere panics, even after an eligible heavy-leader partition."""
+    from test_oracle import EMPTY_AFTER_PICK
+    for sem in ("applied", "go"):
+        check_plan(EMPTY_AFTER_PICK, default_cfg(rebalance_leaders=True, min_unbalance=0.0), 3, sem)
+        check_plan(EMPTY_AFTER_PICK, default_cfg(min_unbalance=0.0), 3, sem)
 
 
 # ------------------------------------- lower-bound prune of the scan (k_scan)

@@ -78,6 +78,28 @@ def test_c1_predicted_plans():
     assert code == 99     # the 6th move is foo2/0, which then flips forever
 
 
+EMPTY_AFTER_PICK = {"version": 1, "partitions": [
+    {"topic": "t", "partition": 0, "replicas": [1, 2], "weight": 5.0},
+    {"topic": "t", "partition": 1, "replicas": [2, 3], "weight": 1.0},
+    {"topic": "t", "partition": 2, "replicas": [], "weight": 1.0}]}
+
+
+def test_distribute_leaders_empty_partition_after_pick_panics():
+    """distributeLeaders builds pp over EVERY partition (steps.go:257-262) before it
+    picks, so p.Replicas[0] panics on an empty list even when an eligible
+    heavy-leader partition (P0) comes first."""
+    cfg = default_cfg(rebalance_leaders=True, min_unbalance=0.0)
+    for sem in (O.SEM_APPLIED, O.SEM_GO):
+        r = O.balance(O.OraclePL(EMPTY_AFTER_PICK), cfg, sem)
+        assert r["status"] == -1 and r["err"].startswith("ReassignLeaders: panic"), r
+    with pytest.raises(pyref.StepError, match="panic"):
+        pyref.balance(pyref.normalize(EMPTY_AFTER_PICK), cfg)
+    # without -rebalance-leader the step is skipped and move() only reads slots of
+    # eligible partitions (P2 has NumReplicas 0 < MinReplicas): no panic
+    r = O.balance(O.OraclePL(EMPTY_AFTER_PICK), default_cfg(min_unbalance=0.0), O.SEM_APPLIED)
+    assert r["status"] >= 0, r
+
+
 def _pyref_plan(plist, cfg, steps):
     pl = pyref.normalize(plist)
     out = []
@@ -123,6 +145,35 @@ def test_oracle_vs_pyref(seed):
         assert oerr is not None
         if "panic" not in perr:
             assert perr == oerr
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_threaded_oracle_matches_sequential(seed):
+    """or_set_threads(T): chunked move() / Disallowed search, merged in order --
+    the identical plan, unbalance bits and errors as T = 1."""
+    rng = random.Random(500 + seed)
+    pl = random_plist(rng, rng.choice([40, 90, 200]), rng.choice([3, 6, 12]),
+                      rng.choice(["uniform", "int", "zipf"]), rng.choice(["none", "some", "all"]),
+                      rng.random() < 0.4, rng.random() < 0.3)
+    cfg = default_cfg(allow_leader=rng.random() < 0.5, rebalance_leaders=rng.random() < 0.2,
+                      min_replicas=rng.choice([1, 2, 3]), min_unbalance=rng.choice([0.0, 0.01]))
+
+    def run(threads):
+        O.set_threads(threads)
+        try:
+            o = O.OraclePL(pl)
+            out = []
+            for _ in range(20):
+                r = O.balance(o, cfg, O.SEM_APPLIED)
+                out.append((r["status"], r["step"], r.get("pidx"), r.get("from_"), r.get("to"),
+                            r.get("su"), r.get("cu"), r["err"]))
+                if r["status"] != 1:
+                    break
+            return out, o.state()
+        finally:
+            O.set_threads(1)
+
+    assert run(1) == run(5)
 
 
 def test_golden_plans_reproduce():
