@@ -103,6 +103,15 @@ struct kb_engine {
     int64_t refreshes = 0;
     int dbg_scan = 0;
     bool ub_mode = false;          // a step re-scanned: enqueue the conditional bound pass per scan
+    // persistent plan launch (k_plan): plan_nscan scan workgroups + one resolver
+    bool persist = false;
+    int plan_nscan = 0;
+    size_t plan_lds = 0;
+    SyncBlk* sync = nullptr;
+    SyncBlk* h_sync = nullptr;         // pinned
+    int64_t plan_launches = 0, plan_aborts = 0;
+    uint32_t list_slack = 1024;        // free entries per broker list (doubled on every re-layout)
+    int64_t relists = 0;
     std::string last_err;
 };
 
@@ -401,6 +410,7 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
     std::vector<uint32_t> hls, hll, hlc, hle;
     if (!e->integral) {
         uint32_t slack = cfg->list_slack > 0 ? (uint32_t)cfg->list_slack : 1024u;
+        e->list_slack = slack;
         hls.resize(e->B); hll.resize(e->B); hlc.resize(e->B);
         uint64_t off = 0;
         for (int64_t b = 0; b < e->B; b++) {
@@ -448,6 +458,16 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
         e->step_lds_bytes = step_lds((int)e->B, e->NP2, e->sb_lds ? sbw : 0).total;
         if (st_lds + e->step_lds_bytes > lim) { e->last_err = "too many brokers for k_step's LDS"; *out = e; return KB_ERR_UNSUPPORTED; }
     }
+    {
+        // k_plan: every scan workgroup, the resolver and one spare CU stay resident
+        // together (one workgroup per CU); both roles share the dynamic LDS
+        const bool whole = e->shard_begin == 0 && e->shard_end == n;
+        e->plan_nscan = (int)std::min<int64_t>(e->ntiles, std::max(ncu - 2, 1));
+        e->plan_lds = std::max(e->scan_lds, (size_t)e->step_lds_bytes);
+        const int st_plan = plan_static_lds(e->rc_dev, e->lds_sets);
+        e->persist = whole && e->ntiles > 0 && st_plan >= 0 && st_plan + e->plan_lds <= 160 * 1024;
+        if (const char* v = getenv("KB_PERSIST")) if (*v == '0') e->persist = false;      // A/B and fallback
+    }
     HIPCHK(hipStreamCreateWithFlags(&e->st, hipStreamNonBlocking));
     e->own_st = true;
     HIPCHK(dalloc(&e->w, e->Ppad));
@@ -474,6 +494,8 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
     e->logcap = 1024;
     HIPCHK(dalloc(&e->log, e->logcap));
     HIPCHK(hipHostMalloc((void**)&e->h_ctl, sizeof(DevCtl), hipHostMallocDefault));
+    HIPCHK(dalloc(&e->sync, 1));
+    HIPCHK(hipHostMalloc((void**)&e->h_sync, sizeof(SyncBlk), hipHostMallocDefault));
     HIPCHK(hipMemcpy(e->w, hw.data(), hw.size() * 8, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(e->meta, hm.data(), hm.size() * 4, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(e->rep, hr.data(), hr.size() * 2, hipMemcpyHostToDevice));
@@ -528,6 +550,7 @@ static void fill_scan_args(kb_engine* e, ScanArgs& s) {
     s.setbits = e->setbits; s.setrec = e->setrec; s.r = e->r; s.blm = e->blm; s.posm = e->posm;
     s.allow_leader = e->allow_leader; s.rebalance = e->rebalance; s.sem_go = e->sem == KB_SEM_GO;
     s.R = scan_recs(e->recs, (int)e->nscan); s.cont = e->cont; s.cont_cap = e->cont_cap;
+    s.ncont = &e->ctl->ncont; s.cont_ovf = &e->ctl->cont_overflow;
     s.listwg = e->integral ? 0 : 1;
     s.dbg = e->dbg_scan;
     s.ubpass = 0;
@@ -549,6 +572,7 @@ static void fill_step_args(kb_engine* e, StepArgs& a, const Recs& R, int use_spi
     a.integral = e->integral ? 1 : 0; a.exact_unb = e->exact_unb;
     a.minrep = e->minrep; a.min_unbalance = e->min_unb; a.wmax = e->wmax;
     a.log = e->log; a.L = e->L;
+    a.sync = nullptr;
 }
 
 static const int kStepBatch = 64;
@@ -618,11 +642,60 @@ static void enqueue_pair(kb_engine* e) {
     enqueue_step(e);
 }
 
+// Lay the per-broker partition lists out again from the device's partition words
+// (partition order, the getBrokerLoad fold order) with twice the slack: a list ran
+// out of room (ctl.list_overflow).  Every applied change is already in the
+// partition words, so a pending list edit is dropped with the old lists.
+static int relist(kb_engine* e) {
+    const int64_t P = e->P;
+    std::vector<uint16_t> hr((size_t)e->rc_dev * e->Ppad);
+    std::vector<uint32_t> hm((size_t)e->Ppad);
+    HIPCHK(hipMemcpy(hr.data(), e->rep, hr.size() * 2, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(hm.data(), e->meta, hm.size() * 4, hipMemcpyDeviceToHost));
+    std::vector<uint32_t> cnt(e->B, 0);
+    for (int64_t i = 0; i < P; i++) {
+        const int nr = (int)meta_nrep(hm[i]);
+        for (int k = 0; k < nr && k < e->rc_dev; k++) cnt[hr[(size_t)k * e->Ppad + i]]++;
+    }
+    e->list_slack = e->list_slack < (1u << 30) ? 2 * e->list_slack : e->list_slack;
+    std::vector<uint32_t> hls(e->B), hll(e->B, 0), hlc(e->B);
+    uint64_t off = 0;
+    for (int64_t b = 0; b < e->B; b++) { hls[b] = (uint32_t)off; hlc[b] = cnt[b] + e->list_slack; off += hlc[b]; }
+    if (off >= (1ull << 32)) { e->last_err = "broker lists exceed 2^32 entries"; return KB_ERR_CAPACITY; }
+    std::vector<uint32_t> hle(off ? off : 1, 0);
+    for (int64_t i = 0; i < P; i++) {
+        const int nr = (int)meta_nrep(hm[i]);
+        for (int k = 0; k < nr && k < e->rc_dev; k++) {
+            const int b = hr[(size_t)k * e->Ppad + i];
+            hle[hls[b] + hll[b]++] = (uint32_t)i;
+        }
+    }
+    uint32_t* nent = nullptr;
+    HIPCHK(dalloc(&nent, hle.size()));
+    hipFree(e->L.lent);
+    e->L.lent = nent;
+    HIPCHK(hipMemcpy(e->L.lent, hle.data(), hle.size() * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(e->L.lstart, hls.data(), hls.size() * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(e->L.llen, hll.data(), hll.size() * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(e->L.lcap, hlc.data(), hlc.size() * 4, hipMemcpyHostToDevice));
+    e->relists++;
+    return KB_OK;
+}
+
 // exact refolds of the approximate loads (k_refresh), then a full prep
 static int refresh(kb_engine* e) {
     if (e->integral) return KB_OK;
     mark(e, -1);
     launch_listop(e->ctl, e->L, e->st);
+    HIPCHK(hipMemcpyAsync(e->h_ctl, e->ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, e->st));
+    HIPCHK(hipStreamSynchronize(e->st));
+    if (e->h_ctl->list_overflow) {
+        if (relist(e) != KB_OK) return KB_ERR_HIP;
+        DevCtl c = *e->h_ctl;
+        c.list_overflow = 0;
+        c.pending_list = 0;
+        HIPCHK(hipMemcpy(e->ctl, &c, sizeof c, hipMemcpyHostToDevice));
+    }
     RefreshArgs ra;
     ra.ctl = e->ctl; ra.w = e->w; ra.rep = e->rep; ra.meta = e->meta; ra.nc = e->nc;
     ra.load = e->load; ra.lerr = e->lerr; ra.eb = e->eb; ra.bfl = e->bfl; ra.B = (int)e->B;
@@ -714,15 +787,104 @@ static int pending_result(kb_engine* e, kb_change* o) {
     return e->pending;
 }
 
+// grow the device step log to hold max_steps entries (the new buffer first: a failed
+// allocation leaves the old one and its capacity in place)
+static int ensure_log(kb_engine* e, int64_t max_steps) {
+    if (max_steps <= e->logcap) return KB_OK;
+    const int cap = (int)std::min<int64_t>(max_steps, 1 << 30);
+    ChangeDev* nl = nullptr;
+    if (dalloc(&nl, cap) != hipSuccess) {
+        e->last_err = "cannot allocate the step log";
+        return KB_ERR_HIP;
+    }
+    hipFree(e->log);
+    e->log = nl;
+    e->logcap = cap;
+    return KB_OK;
+}
+
+// persistent plan: launches of k_plan (each up to PLAN_MAX_STEPS steps; a launch
+// whose plan already halted exits at once), a few per host round trip; between
+// round trips the host refolds the loads exactly when a step asked for it.  A
+// launch that gave up (a bounded spin ran out, e.g. workgroups not co-resident)
+// leaves a consistent state behind: the remaining steps then run as (k_scan, k_step)
+// launches.  Returns the log entries written, or < 0.
+static int run_steps_plan(kb_engine* e, int64_t max_steps, bool* fell_back) {
+    *fell_back = false;
+    const int steps0 = e->h_ctl->steps;
+    PlanArgs p;
+    p.sync = e->sync;
+    p.nscan = e->plan_nscan;
+    p.max_steps = PLAN_MAX_STEPS;
+    p.timeout_ticks = 200000000ull;                  // 2 s of the 100 MHz wall clock per wait
+    p.dbg = 0;
+    if (const char* v = getenv("KB_PLAN_DBG")) p.dbg = atoi(v);                    // diagnostic
+    for (;;) {
+        const int64_t done = e->h_ctl->steps - steps0;
+        if (done >= max_steps) break;
+        // the arguments of every round (a refresh may have laid the broker lists out anew)
+        ScanArgs s;
+        fill_scan_args(e, s);
+        s.nscan = e->plan_nscan;
+        s.R = scan_recs(e->recs, e->plan_nscan);
+        s.ncont = &e->sync->ncont; s.cont_ovf = &e->sync->cont_overflow;
+        s.listwg = 0;
+        StepArgs t;
+        fill_step_args(e, t, s.R, 1);
+        t.sync = e->sync;
+        const int64_t need = (max_steps - done + PLAN_MAX_STEPS - 1) / PLAN_MAX_STEPS;
+        const int nl = (int)std::min<int64_t>(need, 4);
+        for (int i = 0; i < nl; i++) {
+            HIPCHK(hipMemsetAsync(e->sync, 0, SYNC_ZERO_BYTES, e->st));
+            launch_plan(s, t, p, e->rc_dev, e->lds_sets, e->plan_lds, e->st);
+            HIPCHK(hipGetLastError());
+            e->plan_launches++;
+        }
+        HIPCHK(hipMemcpyAsync(e->h_ctl, e->ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, e->st));
+        HIPCHK(hipMemcpyAsync(e->h_sync, e->sync, sizeof(SyncBlk), hipMemcpyDeviceToHost, e->st));
+        HIPCHK(hipStreamSynchronize(e->st));
+        const DevCtl& c = *e->h_ctl;
+        if (e->h_sync->abort) {
+            e->plan_aborts++;
+            *fell_back = true;
+            return 0;
+        }
+        if (c.halted == H_DONE) break;
+        if (c.halted == H_NEED_EXACT || (c.want_refresh && c.steps - steps0 < max_steps)) {
+            if (refresh(e) != KB_OK) return KB_ERR_HIP;
+            continue;
+        }
+    }
+    return KB_OK;
+}
+
 // run up to max_steps Balance() calls device-resident; returns the number of
 // log entries written (changes + the terminating no-change / error)
 static int run_steps(kb_engine* e, int64_t max_steps) {
-    if (max_steps > e->logcap) {
-        hipFree(e->log);
-        e->logcap = (int)std::min<int64_t>(max_steps, 1 << 30);
-        HIPCHK(dalloc(&e->log, e->logcap));
-    }
+    if (ensure_log(e, max_steps) != KB_OK) return KB_ERR_HIP;
     if (reset_ctl(e, max_steps) != KB_OK) return KB_ERR_HIP;
+    if (e->persist) {
+        HIPCHK(hipEventRecord(e->ev0, e->st));
+        bool fb = false;
+        const int rc = run_steps_plan(e, max_steps, &fb);
+        if (rc < 0) return rc;
+        if (!fb) {
+            HIPCHK(hipEventRecord(e->ev1, e->st));
+            HIPCHK(hipStreamSynchronize(e->st));
+            float ms = 0;
+            hipEventElapsedTime(&ms, e->ev0, e->ev1);
+            e->last_ms = ms;
+            HIPCHK(hipMemcpy(e->h_ctl, e->ctl, sizeof(DevCtl), hipMemcpyDeviceToHost));
+            return (int)std::min<int64_t>(e->h_ctl->logpos, e->logcap);
+        }
+        // a launch gave up: continue with per-step launches from the state it left
+        fprintf(stderr, "kbengine: persistent plan launch gave up (workgroups not co-resident?); "
+                        "continuing with per-step launches\n");
+        e->persist = false;
+        const int left = (int)(e->h_ctl->budget - e->h_ctl->steps);
+        if (left <= 0) return (int)std::min<int64_t>(e->h_ctl->logpos, e->logcap);
+        max_steps = left;
+    }
     const int steps0 = e->h_ctl->steps;
     bool prepped = e->h_ctl->prepped != 0;
     HIPCHK(hipEventRecord(e->ev0, e->st));
@@ -862,6 +1024,8 @@ extern "C" int kb_engine_stats(kb_engine* e, kb_stats* o) {
     o->exact_halts = (int64_t)c.total_exact_halts;
     o->scan_workgroups = e->nscan;
     o->retries = (int64_t)c.total_retries;
+    o->plan_launches = e->plan_launches;
+    o->plan_aborts = e->plan_aborts;
     return KB_OK;
 }
 
@@ -981,6 +1145,8 @@ extern "C" void kb_engine_destroy(kb_engine* e) {
                     e->L.lstart, e->L.llen, e->L.lcap, e->L.lent};
     for (void* p : ptrs) if (p) hipFree(p);
     if (e->h_ctl) hipHostFree(e->h_ctl);
+    if (e->h_sync) hipHostFree(e->h_sync);
+    if (e->sync) hipFree(e->sync);
     if (e->ev0) hipEventDestroy(e->ev0);
     if (e->ev1) hipEventDestroy(e->ev1);
     for (auto v : e->tev) hipEventDestroy(v);

@@ -301,9 +301,15 @@ static int cmp_i64(const void *x, const void *y) {
 static void fill_defaults(or_plist *pl, const or_config *cfg) {   /* steps.go:39-66 */
     if (pl->parts[0].weight == 0)
         for (int64_t i = 0; i < pl->n; i++) pl->parts[i].weight = 1.0;
+    int any_nil = 0;
+    for (int64_t i = 0; i < pl->n && !any_nil; i++) any_nil = pl->parts[i].brokers.a == NULL;
+    if (!any_nil) goto num_replicas;
     or_slice brokers;
     if (!cfg->brokers_nil) {
-        brokers.a = cfg->brokers; brokers.len = cfg->nbrokers; brokers.cap = cfg->nbrokers;
+        /* Go shares cfg.Brokers' backing array (alive for the whole run); the caller's
+         * or_config may not outlive this call, so the list owns a copy */
+        brokers = sl_make(cfg->nbrokers, cfg->nbrokers);
+        if (cfg->nbrokers) memcpy(brokers.a, cfg->brokers, (size_t)cfg->nbrokers * sizeof(int64_t));
     } else {                                          /* getBrokerList (utils.go:49-64) */
         lmap m; lm_init(&m, 64);
         for (int64_t i = 0; i < pl->n; i++)
@@ -318,6 +324,7 @@ static void fill_defaults(or_plist *pl, const or_config *cfg) {   /* steps.go:39
     }
     for (int64_t i = 0; i < pl->n; i++)
         if (pl->parts[i].brokers.a == NULL) pl->parts[i].brokers = brokers;
+num_replicas:
     for (int64_t i = 0; i < pl->n; i++)
         if (pl->parts[i].num_replicas == 0) pl->parts[i].num_replicas = pl->parts[i].replicas.len;
 }
