@@ -465,8 +465,11 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
         e->plan_nscan = (int)std::min<int64_t>(e->ntiles, std::max(ncu - 2, 1));
         e->plan_lds = std::max(e->scan_lds, (size_t)e->step_lds_bytes);
         const int st_plan = plan_static_lds(e->rc_dev, e->lds_sets);
-        e->persist = whole && e->ntiles > 0 && st_plan >= 0 && st_plan + e->plan_lds <= 160 * 1024;
-        if (const char* v = getenv("KB_PERSIST")) if (*v == '0') e->persist = false;      // A/B and fallback
+        // opt-in (KB_PERSIST=1): parity-green but slower than the two-launch step so far
+        // (DESIGN.md "Persistent plan kernel": the resolver's loop spills registers)
+        const bool fits = whole && e->ntiles > 0 && st_plan >= 0 && st_plan + e->plan_lds <= 160 * 1024;
+        e->persist = false;
+        if (const char* v = getenv("KB_PERSIST")) e->persist = fits && *v == '1';
     }
     HIPCHK(hipStreamCreateWithFlags(&e->st, hipStreamNonBlocking));
     e->own_st = true;
