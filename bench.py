@@ -3,17 +3,25 @@
 Workload (N=1): BASELINE.json configs[2] -- synthetic 1M partitions x 1000
 brokers, RF3, Zipf weights, 256 allowed-broker sets of 64, -allow-leader,
 -min-unbalance 0 (the metric's "1M partitions x 1k brokers").  A step is one
-Balance() call (balancer.go:49-65) executed device-resident by
-kb_engine_plan; `value` counts the candidates the reference would score
-(SURVEY.md 8d metric 1) over the timed steps.
+Balance() call (balancer.go:49-65) executed device-resident by kb_engine_plan;
+`value` counts the candidates the reference would score (SURVEY.md 8d metric 1)
+over the timed steps, per wall second.
 
-Multi-GPU (torchrun): weak scaling, every rank holds the full cluster state
-(N x 1M partitions, replicated) and scans its own 1M-partition shard; one
-all-gather of a fixed-size summary per step combines the ranks.
+Roofline: the dominant streaming kernel is k_scan; `achieved` =
+its algorithmic bytes per launch / its in-plan duration (device clock: earliest
+scan-workgroup start to latest end, per step).  The isolated figure (HIP events
+around back-to-back launches on the final state) and the whole-step fraction
+(8d bytes per step / ms_per_step / 8 TB/s) are reported beside it.  `traffic` is
+the rocprofv3 PMC figure for the same workload (profiles/pmc_traffic.json, keyed by
+workload).
+
+Multi-GPU (torchrun): kafkabalancer_amd.dist.bench_main (c5: a fixed 10M partitions
+sharded N ways, strong scaling; other workloads weak by default).
 """
 import argparse
 import json
 import os
+import platform
 import sys
 import time
 
@@ -25,23 +33,34 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
 def cpu_baseline(cl, cfg, seconds=12.0):
-    """The oracle (C restatement of steps.go move(), single thread) on a bounded
-    sample: the first k partitions of the same cluster, leader step (the step
-    the reference runs first with -allow-leader)."""
+    """The reference's algorithm on the host: the oracle (C restatement of steps.go
+    move(), single thread like the Go balancer) on a bounded sample -- the first k
+    partitions of the same cluster, leader step (the step the reference runs first with
+    -allow-leader) -- plus the engine's own algorithm on the CPU (tools/cpu_engine,
+    OpenMP) over whole steps of the same plan."""
     from oracle import oracle as O
     P = cl.n
-    blob = b"t"
-    toff = np.zeros(P + 1, np.int64)
-    toff[1:] = 1
-    opl = O.OraclePL.from_soa(blob * 1, np.zeros(P + 1, np.int64), np.arange(P, dtype=np.int64),
+    opl = O.OraclePL.from_soa(b"t", np.zeros(P + 1, np.int64), np.arange(P, dtype=np.int64),
                               cl.replica_ids, cl.replica_off, np.where(cl.weight == 0, 1.0, cl.weight),
-                              np.where(cl.num_replicas == 0, 3, cl.num_replicas),
+                              np.where(cl.num_replicas == 0, np.diff(cl.replica_off), cl.num_replicas),
                               cl.set_ids, cl.set_off, cl.set_idx, cl.num_consumers)
+    leaders = bool(cfg.get("allow_leader"))
     k = 16
     while True:
         t0 = time.perf_counter()
-        n, _ = O.move_sample(opl, cfg, True, k)
+        n, _ = O.move_sample(opl, cfg, leaders, k)
         dt = time.perf_counter() - t0
         if dt > seconds / 8 or k >= P:
             break
@@ -49,21 +68,68 @@ def cpu_baseline(cl, cfg, seconds=12.0):
     k2 = min(P, int(k * seconds / max(dt, 1e-6)))
     if k2 > k:
         t0 = time.perf_counter()
-        n, _ = O.move_sample(opl, cfg, True, k2)
+        n, _ = O.move_sample(opl, cfg, leaders, k2)
         dt = time.perf_counter() - t0
         k = k2
-    return {"value": n / dt, "unit": "candidates/s", "cores": 1, "kind": "port",
-            "sample": "oracle move(leaders) over the first %d of %d partitions: %d candidates in %.1f s "
-                      "(reference Go not buildable: no Go toolchain)" % (k, P, n, dt)}
+    out = {"value": n / dt, "unit": "candidates/s", "cores": 1, "kind": "port",
+           "sample": "oracle move(%s) over the first %d of %d partitions: %d candidates in %.1f s "
+                     "(extrapolated per candidate; reference Go not buildable: no Go toolchain)"
+                     % ("leaders" if leaders else "non-leaders", k, P, n, dt),
+           "cpu_model": cpu_model(), "nproc": os.cpu_count()}
+    # the engine's algorithm on the CPU (O(1) deltas + exact verification, OpenMP)
+    try:
+        sys.path.insert(0, os.path.join(ROOT, "tools", "cpu_engine"))
+        import cpu_engine
+        threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+        ce = cpu_engine.CpuEngine(cl, cfg, threads=threads)
+        c0 = ce.candidates()
+        t0 = time.perf_counter()
+        steps = 0
+        while steps < 200 and time.perf_counter() - t0 < seconds:
+            if ce.step() is None:
+                break
+            steps += 1
+        dt = time.perf_counter() - t0
+        out["optimised_cpu"] = {"value": (ce.candidates() - c0) / dt, "unit": "candidates/s",
+                                "ms_per_step": 1e3 * dt / max(steps, 1), "cores": threads, "steps": steps,
+                                "kind": "engine algorithm on the host (tools/cpu_engine, OpenMP)"}
+        ce.close()
+    except (ImportError, OSError, ValueError) as ex:
+        out["optimised_cpu"] = {"skipped": str(ex)}
+    return out
 
 
-def pmc_traffic(kernel):
+def pmc_traffic(workload, kernel):
     """HBM-side bytes per launch from the committed rocprofv3 PMC passes (tools/pmc_bench.sh)."""
     try:
         with open(os.path.join(ROOT, "profiles", "pmc_traffic.json")) as f:
-            return json.load(f)[kernel]["traffic_bytes_per_launch"]
-    except (OSError, KeyError, ValueError):
+            d = json.load(f)
+        return d[workload][kernel]["traffic_bytes_per_launch"]
+    except (OSError, KeyError, ValueError, TypeError):
         return None
+
+
+def bytes_8d(cl, changes, nsets, B, rmax, full_steps):
+    """SURVEY.md 8(d) algorithmic bytes of the timed steps: a full-scan step reads
+    P*(8 w + 4*Rmax rep + 1 nrep + 1 want + 4 aset) + 12 B + nsets*ceil(B/64)*8; an
+    early-exit stage (Remove / Add / Disallowed, steps.go:81,105,135) reads the fields
+    of every fully scanned earlier stage over all P plus its own up to the hit."""
+    P = cl.n
+    tables = 12 * B + nsets * ((B + 63) // 64) * 8
+    per = 8 + 4 * rmax + 1 + 1 + 4
+    total = 0
+    for c in changes:
+        h = c["pidx"] + 1
+        if c["step"] == "RemoveExtraReplicas":
+            total += 2 * h + tables
+        elif c["step"] == "AddMissingReplicas":
+            total += 2 * P + 2 * h + tables
+        elif c["step"] == "MoveDisallowedReplicas":
+            total += 4 * P + (4 * rmax + 1 + 4) * h + tables
+        else:
+            total += P * per + tables
+    total += (full_steps - len(changes)) * (P * per + tables)
+    return total
 
 
 def main():
@@ -73,6 +139,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--workload", default="c3")
     ap.add_argument("--scale", type=float, default=1.0)
+    ap.add_argument("--scaling", default=None, choices=[None, "weak", "strong"],
+                    help="multi-GPU: weak (every rank adds a full cluster) or strong (one cluster "
+                         "sharded N ways; default for c5)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--stamps", action="store_true",
@@ -108,13 +177,10 @@ def main():
     steps = len(changes) + (0 if len(changes) == args.steps else 1)
     cand = st1["candidates"] - st0["candidates"]
     dev_s = st1["device_ms"] / 1e3
-    # per-kernel durations, outside the headline timing above (instrumentation
-    # between the launches adds its own gaps):
-    #  * device clock: every scan workgroup stamps its start/end, k_step folds the
-    #    interval (earliest start .. latest end) -- a second stretch of the same plan;
-    #  * HIP events on the engine's stream around 200 back-to-back k_scan launches
-    #    on the plan's final state: dispatch-inclusive, the interval rocprofv3
-    #    reports.  `achieved` uses this (the conservative) one.
+    ms_per_step = 1e3 * wall / max(steps, 1)
+    # per-kernel durations over a second stretch of the same plan (device clock: every
+    # scan workgroup stamps its start/end, k_step folds the interval), outside the
+    # headline timing above
     eng.set_timing(True)
     kt_steps = min(args.steps, 200)
     _, err = eng.plan(kt_steps)
@@ -123,9 +189,16 @@ def main():
     scan_ms, scan_n = tk["scan"]
     scan_clock_us = 1e3 * scan_ms / max(scan_n, 1)
     eng.set_timing(False)
-    scan_avg_us = eng.bench_scan(200)
+    scan_iso_us = eng.bench_scan(200)
     bytes_scan = st1["scan_bytes"]
-    achieved = bytes_scan / (scan_avg_us * 1e-6) / 1e9
+    achieved = bytes_scan / (scan_clock_us * 1e-6) / 1e9
+    rmax = st1["max_replicas"]
+    b8d = bytes_8d(cl, changes, st1["n_sets"], st1["n_brokers"], rmax, steps)
+    whole_gbs = b8d / max(wall, 1e-12) / 1e9
+    early_exit = any(c["step"] in ("RemoveExtraReplicas", "AddMissingReplicas", "MoveDisallowedReplicas")
+                     for c in changes)
+    weights = "Zipf-like weights w = r^-1.1, r ~ U[1, 1e6]" if desc.get("weights") == "zipf" else \
+        "weights absent (FillDefaults -> 1.0: uniform, exact ties)"
     out = {
         "metric": "candidate moves scored/sec (+ ms per reassignment step)",
         "value": cand / wall,
@@ -133,22 +206,30 @@ def main():
         "n_gpus": 1,
         "steps": steps,
         "warmup": args.warmup,
-        "ms_per_step": 1e3 * wall / max(steps, 1),
+        "ms_per_step": ms_per_step,
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic (numpy PCG64 seed 0x5EED0003), Zipf weights r^-1.1",
+        "data": "synthetic (numpy PCG64 seed 0x5EED000%s), %s" % (args.workload[-1], weights),
         "config": dict(desc, parallelism="single-gpu", device_ms_per_step=1e3 * dev_s / max(steps, 1)),
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic("k_scan"),
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(args.workload, "k_scan"),
                      "kernel": "k_scan", "bytes_per_launch": bytes_scan,
-                     "avg_launch_us": scan_avg_us,
-                     "timing": "HIP events on the engine stream around 200 back-to-back k_scan launches "
-                               "(dispatch-inclusive, as rocprofv3 kernel-trace)",
-                     "avg_launch_us_device_clock": scan_clock_us,
-                     "frac_device_clock": bytes_scan / (scan_clock_us * 1e-6) / 1e9 / HBM_PEAK_GBS,
-                     "traffic_source": "profiles/pmc_traffic.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE per launch)"},
+                     "bytes_per_launch_def": "engine layout: per partition 8 w + 4 meta + 2*%d rep" % rmax,
+                     "avg_launch_us": scan_clock_us,
+                     "timing": "in-plan device clock (earliest scan workgroup start .. latest end), "
+                               "%d steps" % scan_n,
+                     "avg_launch_us_isolated": scan_iso_us,
+                     "frac_isolated": bytes_scan / (scan_iso_us * 1e-6) / 1e9 / HBM_PEAK_GBS,
+                     "isolated_timing": "HIP events around 200 back-to-back k_scan launches on the final state",
+                     "traffic_source": "profiles/pmc_traffic.json[%s] (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE "
+                                       "per launch)" % args.workload,
+                     "whole_step": {"bytes_8d_per_step": b8d / max(steps, 1), "achieved": whole_gbs,
+                                    "frac": whole_gbs / HBM_PEAK_GBS,
+                                    "def": "SURVEY.md 8(d) algorithmic bytes of the timed steps / wall time"
+                                           + (" (early-exit stages counted to their hit: ms_per_step is "
+                                              "the headline, GB/s informational)" if early_exit else "")}},
         "kernels_us_per_step": {k: 1e3 * v[0] / max(v[1], 1) for k, v in tk.items()},
         "kernel_timing_steps": kt_steps,
         "engine_events": {k: st1[k] - st0[k] for k in ("retries", "refreshes", "exact_halts", "exact_folds")},

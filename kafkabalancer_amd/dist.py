@@ -143,8 +143,10 @@ def bench_main(args, world, rank, local):
     local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dist.init_process_group(backend)
-    # weak scaling: 1M partitions per GPU (c3 shape), the same seed on every rank
-    cl, cfg, desc = synth.config(args.workload, scale=args.scale * world)
+    # strong scaling (c5 default, BASELINE configs[4]): one cluster of the configured size
+    # sharded N ways; weak: every rank adds a full cluster's worth of partitions
+    scaling = getattr(args, "scaling", None) or ("strong" if args.workload == "c5" else "weak")
+    cl, cfg, desc = synth.config(args.workload, scale=args.scale * (world if scaling == "weak" else 1))
     begin, end = shard_bounds(cl.n, world, rank)
     eng = E.Engine(cl, cfg, device=local, shard=(begin, end))
     eng.set_stream(torch.cuda.current_stream().cuda_stream)
@@ -184,10 +186,11 @@ def bench_main(args, world, rank, local):
             "warmup": args.warmup,
             "ms_per_step": 1e3 * wall / steps,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": scaling,
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic (numpy PCG64), Zipf weights r^-1.1",
+            "data": "synthetic (numpy PCG64), %s" % ("Zipf weights r^-1.1" if desc.get("weights") == "zipf"
+                                                      else "uniform weights"),
             "config": dict(desc, parallelism="partition-sharded x%d, replicated broker state, "
                                               "1 all-gather per step" % world),
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": 8000.0, "unit": "GB/s",

@@ -9,6 +9,7 @@ from collections import defaultdict
 
 tag = sys.argv[1] if len(sys.argv) > 1 else "pmcb"
 out = sys.argv[2] if len(sys.argv) > 2 else None
+workload = sys.argv[3] if len(sys.argv) > 3 else "c3"
 
 
 def per_kernel(counter):
@@ -42,7 +43,16 @@ doc["method"] = ("rocprofv3 --kernel-trace --pmc FETCH_SIZE, then --pmc WRITE_SI
                  "dispatches after the first 10; FETCH_SIZE doubled per MI355X_MICROARCH.md (gfx950 reports half "
                  "of 16-B/lane streaming reads); KB = 1024 B. k_step's reads are not 16-B streaming, so its "
                  "doubled figure is an upper estimate.")
-s = json.dumps(doc, indent=1)
+method = doc.pop("method")
+merged = {}
+if out:
+    try:
+        merged = json.load(open(out))
+    except (OSError, ValueError):
+        merged = {}
+merged[workload] = doc
+merged["method"] = method + " Keyed by bench workload."
+s = json.dumps(merged, indent=1)
 if out:
     open(out, "w").write(s + "\n")
 print(s)
