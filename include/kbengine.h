@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define KB_ABI_VERSION 4
+#define KB_ABI_VERSION 5
 
 /* step indices == position in the reference's steps table (balancer.go:34-44) */
 enum kb_step {
@@ -135,9 +135,6 @@ typedef struct {
     int64_t scan_workgroups;        /* k_scan workgroups (one record each) */
     int64_t retries;                /* steps re-scanned with the census bound tightened to the
                                        step minimum after a near-tie spill overflow (ABI 3) */
-    int64_t plan_launches;          /* persistent k_plan launches (ABI 4) */
-    int64_t plan_aborts;            /* k_plan launches that gave up waiting (the plan went on
-                                       with per-step launches) */
 } kb_stats;
 
 typedef struct kb_engine kb_engine;

@@ -103,13 +103,6 @@ struct kb_engine {
     int64_t refreshes = 0;
     int dbg_scan = 0;
     bool ub_mode = false;          // a step re-scanned: enqueue the conditional bound pass per scan
-    // persistent plan launch (k_plan): plan_nscan scan workgroups + one resolver
-    bool persist = false;
-    int plan_nscan = 0;
-    size_t plan_lds = 0;
-    SyncBlk* sync = nullptr;
-    SyncBlk* h_sync = nullptr;         // pinned
-    int64_t plan_launches = 0, plan_aborts = 0;
     uint32_t list_slack = 1024;        // free entries per broker list (doubled on every re-layout)
     int64_t relists = 0;
     std::string last_err;
@@ -458,19 +451,6 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
         e->step_lds_bytes = step_lds((int)e->B, e->NP2, e->sb_lds ? sbw : 0).total;
         if (st_lds + e->step_lds_bytes > lim) { e->last_err = "too many brokers for k_step's LDS"; *out = e; return KB_ERR_UNSUPPORTED; }
     }
-    {
-        // k_plan: every scan workgroup, the resolver and one spare CU stay resident
-        // together (one workgroup per CU); both roles share the dynamic LDS
-        const bool whole = e->shard_begin == 0 && e->shard_end == n;
-        e->plan_nscan = (int)std::min<int64_t>(e->ntiles, std::max(ncu - 2, 1));
-        e->plan_lds = std::max(e->scan_lds, (size_t)e->step_lds_bytes);
-        const int st_plan = plan_static_lds(e->rc_dev, e->lds_sets);
-        // opt-in (KB_PERSIST=1): parity-green but slower than the two-launch step so far
-        // (DESIGN.md "Persistent plan kernel": the resolver's loop spills registers)
-        const bool fits = whole && e->ntiles > 0 && st_plan >= 0 && st_plan + e->plan_lds <= 160 * 1024;
-        e->persist = false;
-        if (const char* v = getenv("KB_PERSIST")) e->persist = fits && *v == '1';
-    }
     HIPCHK(hipStreamCreateWithFlags(&e->st, hipStreamNonBlocking));
     e->own_st = true;
     HIPCHK(dalloc(&e->w, e->Ppad));
@@ -497,8 +477,6 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
     e->logcap = 1024;
     HIPCHK(dalloc(&e->log, e->logcap));
     HIPCHK(hipHostMalloc((void**)&e->h_ctl, sizeof(DevCtl), hipHostMallocDefault));
-    HIPCHK(dalloc(&e->sync, 1));
-    HIPCHK(hipHostMalloc((void**)&e->h_sync, sizeof(SyncBlk), hipHostMallocDefault));
     HIPCHK(hipMemcpy(e->w, hw.data(), hw.size() * 8, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(e->meta, hm.data(), hm.size() * 4, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(e->rep, hr.data(), hr.size() * 2, hipMemcpyHostToDevice));
@@ -575,10 +553,10 @@ static void fill_step_args(kb_engine* e, StepArgs& a, const Recs& R, int use_spi
     a.integral = e->integral ? 1 : 0; a.exact_unb = e->exact_unb;
     a.minrep = e->minrep; a.min_unbalance = e->min_unb; a.wmax = e->wmax;
     a.log = e->log; a.L = e->L;
-    a.sync = nullptr;
 }
 
 static const int kStepBatch = 64;
+static const int64_t kLogChunk = 16384;   // steps per device step log (kb_engine_plan chunks)
 
 static void mark(kb_engine* e, int kind_next) {
     if (!e->time_kernels) return;
@@ -806,88 +784,11 @@ static int ensure_log(kb_engine* e, int64_t max_steps) {
     return KB_OK;
 }
 
-// persistent plan: launches of k_plan (each up to PLAN_MAX_STEPS steps; a launch
-// whose plan already halted exits at once), a few per host round trip; between
-// round trips the host refolds the loads exactly when a step asked for it.  A
-// launch that gave up (a bounded spin ran out, e.g. workgroups not co-resident)
-// leaves a consistent state behind: the remaining steps then run as (k_scan, k_step)
-// launches.  Returns the log entries written, or < 0.
-static int run_steps_plan(kb_engine* e, int64_t max_steps, bool* fell_back) {
-    *fell_back = false;
-    const int steps0 = e->h_ctl->steps;
-    PlanArgs p;
-    p.sync = e->sync;
-    p.nscan = e->plan_nscan;
-    p.max_steps = PLAN_MAX_STEPS;
-    p.timeout_ticks = 200000000ull;                  // 2 s of the 100 MHz wall clock per wait
-    p.dbg = 0;
-    if (const char* v = getenv("KB_PLAN_DBG")) p.dbg = atoi(v);                    // diagnostic
-    for (;;) {
-        const int64_t done = e->h_ctl->steps - steps0;
-        if (done >= max_steps) break;
-        // the arguments of every round (a refresh may have laid the broker lists out anew)
-        ScanArgs s;
-        fill_scan_args(e, s);
-        s.nscan = e->plan_nscan;
-        s.R = scan_recs(e->recs, e->plan_nscan);
-        s.ncont = &e->sync->ncont; s.cont_ovf = &e->sync->cont_overflow;
-        s.listwg = 0;
-        StepArgs t;
-        fill_step_args(e, t, s.R, 1);
-        t.sync = e->sync;
-        const int64_t need = (max_steps - done + PLAN_MAX_STEPS - 1) / PLAN_MAX_STEPS;
-        const int nl = (int)std::min<int64_t>(need, 4);
-        for (int i = 0; i < nl; i++) {
-            HIPCHK(hipMemsetAsync(e->sync, 0, SYNC_ZERO_BYTES, e->st));
-            launch_plan(s, t, p, e->rc_dev, e->lds_sets, e->plan_lds, e->st);
-            HIPCHK(hipGetLastError());
-            e->plan_launches++;
-        }
-        HIPCHK(hipMemcpyAsync(e->h_ctl, e->ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, e->st));
-        HIPCHK(hipMemcpyAsync(e->h_sync, e->sync, sizeof(SyncBlk), hipMemcpyDeviceToHost, e->st));
-        HIPCHK(hipStreamSynchronize(e->st));
-        const DevCtl& c = *e->h_ctl;
-        if (e->h_sync->abort) {
-            e->plan_aborts++;
-            *fell_back = true;
-            return 0;
-        }
-        if (c.halted == H_DONE) break;
-        if (c.halted == H_NEED_EXACT || (c.want_refresh && c.steps - steps0 < max_steps)) {
-            if (refresh(e) != KB_OK) return KB_ERR_HIP;
-            continue;
-        }
-    }
-    return KB_OK;
-}
-
 // run up to max_steps Balance() calls device-resident; returns the number of
 // log entries written (changes + the terminating no-change / error)
 static int run_steps(kb_engine* e, int64_t max_steps) {
     if (ensure_log(e, max_steps) != KB_OK) return KB_ERR_HIP;
     if (reset_ctl(e, max_steps) != KB_OK) return KB_ERR_HIP;
-    if (e->persist) {
-        HIPCHK(hipEventRecord(e->ev0, e->st));
-        bool fb = false;
-        const int rc = run_steps_plan(e, max_steps, &fb);
-        if (rc < 0) return rc;
-        if (!fb) {
-            HIPCHK(hipEventRecord(e->ev1, e->st));
-            HIPCHK(hipStreamSynchronize(e->st));
-            float ms = 0;
-            hipEventElapsedTime(&ms, e->ev0, e->ev1);
-            e->last_ms = ms;
-            HIPCHK(hipMemcpy(e->h_ctl, e->ctl, sizeof(DevCtl), hipMemcpyDeviceToHost));
-            return (int)std::min<int64_t>(e->h_ctl->logpos, e->logcap);
-        }
-        // a launch gave up: continue with per-step launches from the state it left
-        fprintf(stderr, "kbengine: persistent plan launch gave up (workgroups not co-resident?); "
-                        "continuing with per-step launches\n");
-        e->persist = false;
-        const int left = (int)(e->h_ctl->budget - e->h_ctl->steps);
-        if (left <= 0) return (int)std::min<int64_t>(e->h_ctl->logpos, e->logcap);
-        max_steps = left;
-    }
     const int steps0 = e->h_ctl->steps;
     bool prepped = e->h_ctl->prepped != 0;
     HIPCHK(hipEventRecord(e->ev0, e->st));
@@ -923,7 +824,7 @@ static int run_steps(kb_engine* e, int64_t max_steps) {
     HIPCHK(hipStreamSynchronize(e->st));
     float ms = 0;
     hipEventElapsedTime(&ms, e->ev0, e->ev1);
-    e->last_ms = ms;
+    e->last_ms += ms;
     HIPCHK(hipMemcpy(e->h_ctl, e->ctl, sizeof(DevCtl), hipMemcpyDeviceToHost));
     return (int)std::min<int64_t>(e->h_ctl->logpos, e->logcap);
 }
@@ -931,6 +832,7 @@ static int run_steps(kb_engine* e, int64_t max_steps) {
 extern "C" int kb_engine_balance(kb_engine* e, kb_change* out) {
     if (!e || !out) return KB_ERR_INVALID;
     if (e->pending) return pending_result(e, out);
+    e->last_ms = 0;
     const int nlog = run_steps(e, 1);
     if (nlog < 0) return nlog;
     if (nlog == 0) { memset(out, 0, sizeof *out); out->status = KB_NOCHANGE; return KB_NOCHANGE; }
@@ -946,17 +848,25 @@ extern "C" int kb_engine_plan(kb_engine* e, int64_t max_steps, kb_change* out, i
     if (e->pending) { if (out) pending_result(e, out); *n_out = 1; return e->pending; }
     for (int k = 0; k < TK_N; k++) { e->kms[k] = 0; e->klaunch[k] = 0; }
     e->tev_used = 0;
-    const int nlog = run_steps(e, max_steps);
-    if (nlog < 0) return nlog;
-    std::vector<ChangeDev> logv((size_t)nlog);
-    if (nlog) HIPCHK(hipMemcpy(logv.data(), e->log, (size_t)nlog * sizeof(ChangeDev), hipMemcpyDeviceToHost));
+    e->last_ms = 0;
+    // chunks of at most kLogChunk steps: the device step log stays bounded whatever
+    // max_steps asks for (the caller's `out` holds max_steps entries)
     int rc = KB_NOCHANGE;
     int64_t k = 0;
-    for (int64_t i = 0; i < nlog; i++) {
-        kb_change tmp;
-        rc = convert(e, logv[i], out ? &out[k] : &tmp);
-        k++;
-        if (rc != KB_CHANGE) break;
+    std::vector<ChangeDev> logv;
+    while (k < max_steps) {
+        const int64_t m = std::min<int64_t>(max_steps - k, kLogChunk);
+        const int nlog = run_steps(e, m);
+        if (nlog < 0) { *n_out = k; return nlog; }
+        logv.resize((size_t)nlog);
+        if (nlog) HIPCHK(hipMemcpy(logv.data(), e->log, (size_t)nlog * sizeof(ChangeDev), hipMemcpyDeviceToHost));
+        for (int64_t i = 0; i < nlog; i++) {
+            kb_change tmp;
+            rc = convert(e, logv[i], out ? &out[k] : &tmp);
+            k++;
+            if (rc != KB_CHANGE) { *n_out = k; return rc; }
+        }
+        if (nlog < m) break;
     }
     *n_out = k;
     return rc;
@@ -1027,8 +937,6 @@ extern "C" int kb_engine_stats(kb_engine* e, kb_stats* o) {
     o->exact_halts = (int64_t)c.total_exact_halts;
     o->scan_workgroups = e->nscan;
     o->retries = (int64_t)c.total_retries;
-    o->plan_launches = e->plan_launches;
-    o->plan_aborts = e->plan_aborts;
     return KB_OK;
 }
 
@@ -1148,8 +1056,6 @@ extern "C" void kb_engine_destroy(kb_engine* e) {
                     e->L.lstart, e->L.llen, e->L.lcap, e->L.lent};
     for (void* p : ptrs) if (p) hipFree(p);
     if (e->h_ctl) hipHostFree(e->h_ctl);
-    if (e->h_sync) hipHostFree(e->h_sync);
-    if (e->sync) hipFree(e->sync);
     if (e->ev0) hipEventDestroy(e->ev0);
     if (e->ev1) hipEventDestroy(e->ev1);
     for (auto v : e->tev) hipEventDestroy(v);

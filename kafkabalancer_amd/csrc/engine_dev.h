@@ -146,38 +146,6 @@ struct ChangeDev {
 // halted codes
 enum { H_RUN = 0, H_DONE = 1, H_NEED_EXACT = 2 };
 
-// ---- persistent plan launch (k_plan, DESIGN.md "Persistent plan kernel") ----
-// One launch runs up to PLAN_MAX_STEPS Balance() steps: scan workgroups and one
-// resolver workgroup hand data to each other through write-through (sc1) stores,
-// L1-bypassing (sc1) loads and one epoch flag / per-shard arrival counters.
-constexpr int PLAN_MAX_STEPS = 256;  // steps per launch (= capacity of a scan WG's patch table)
-constexpr int ARR_SHARDS = 8;        // arrival counters (scan WG b adds to shard b & 7)
-
-// the scan parameters of one epoch, published by the resolver
-struct ScanCtl {
-    double inv_avg, eps, ub[2];
-    int32_t run;                    // 0: the launch ends, every scan WG exits
-    int32_t ubpass;                 // 1: census-free bound pass (minima only)
-    int32_t heavy, nblm;
-    int32_t patch_p;                // partition whose replicas the last step rewrote (-1: none)
-    uint32_t patch_meta;            // its meta word after the step
-    int32_t pad[2];
-    uint16_t patch_rep[MAXR];       // its replica slots after the step
-};
-static_assert(sizeof(ScanCtl) % 16 == 0, "ScanCtl layout");
-
-// zeroed (first SYNC_ZERO_BYTES) before every persistent launch
-struct SyncBlk {
-    uint32_t flag;                  // epoch published by the resolver: 1, 2, ...
-    uint32_t abort;                 // a workgroup gave up waiting (bounded spins)
-    uint32_t ncont, cont_overflow;  // near-tie spill buffer of the running epoch
-    uint32_t arr[ARR_SHARDS];       // scan arrivals per shard, cumulative over epochs
-    uint32_t pad[4];
-    ScanCtl sc;
-};
-constexpr int SYNC_ZERO_BYTES = 64;
-static_assert(offsetof(SyncBlk, sc) == SYNC_ZERO_BYTES, "SyncBlk layout");
-
 struct DevCtl {
     int32_t halted, steps, logpos, logcap;
     int32_t prepped, budget, full_prep, want_refresh;

@@ -44,78 +44,16 @@ namespace kbe {
 __device__ __forceinline__ unsigned long long d2u(double d) { return (unsigned long long)__double_as_longlong(d); }
 __device__ __forceinline__ double u2d(unsigned long long u) { return __longlong_as_double((long long)u); }
 
-// ------------------------------------------- cross-workgroup loads / stores
-// PER = true: data another workgroup of the persistent plan launch reads or wrote
-// (MI355X_MICROARCH.md "inter-workgroup visibility", cdna_hip_programming.md
-// Guideline 16 R1): write-through agent-scope stores and L1-bypassing agent-scope
-// loads (global_{load,store}_* sc1), global address space, never flat.  PER = false:
-// plain accesses (the data crossed a kernel boundary).
-typedef __attribute__((address_space(1))) unsigned long long gu64;
-typedef __attribute__((address_space(1))) uint32_t gu32;
-#define KB_RLX_AGENT __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT
-
-template <bool PER>
-__device__ __forceinline__ unsigned long long ld64(const void* p) {
-    if (PER) return __hip_atomic_load((gu64*)p, KB_RLX_AGENT);
-    return *(const unsigned long long*)p;
-}
-template <bool PER>
-__device__ __forceinline__ uint32_t ld32(const void* p) {
-    if (PER) return __hip_atomic_load((gu32*)p, KB_RLX_AGENT);
-    return *(const uint32_t*)p;
-}
-template <bool PER>
-__device__ __forceinline__ void st64(void* p, unsigned long long v) {
-    if (PER) __hip_atomic_store((gu64*)p, v, KB_RLX_AGENT);
-    else *(unsigned long long*)p = v;
-}
-template <bool PER>
-__device__ __forceinline__ void st32(void* p, uint32_t v) {
-    if (PER) __hip_atomic_store((gu32*)p, v, KB_RLX_AGENT);
-    else *(uint32_t*)p = v;
-}
-template <bool PER>
-__device__ __forceinline__ double ldd(const double* p) { return u2d(ld64<PER>(p)); }
-template <bool PER>
-__device__ __forceinline__ void stdbl(double* p, double v) { st64<PER>(p, d2u(v)); }
-// objects of 8-byte multiples (record headers, keys, 16-B set-record units)
-template <bool PER, typename T>
-__device__ __forceinline__ T ldobj(const T* p) {
-    static_assert(sizeof(T) % 8 == 0, "8-byte words");
-    if (!PER) return *p;
-    T v;
-    unsigned long long* d = (unsigned long long*)&v;
-#pragma unroll
-    for (int i = 0; i < (int)(sizeof(T) / 8); i++) d[i] = ld64<true>((const unsigned long long*)p + i);
-    return v;
-}
-template <bool PER, typename T>
-__device__ __forceinline__ void stobj(T* p, const T& v) {
-    static_assert(sizeof(T) % 8 == 0, "8-byte words");
-    if (!PER) { *p = v; return; }
-    const unsigned long long* s = (const unsigned long long*)&v;
-#pragma unroll
-    for (int i = 0; i < (int)(sizeof(T) / 8); i++) st64<true>((unsigned long long*)p + i, s[i]);
-}
-// every storing wave drains its stores before the barrier that precedes a signal (R1)
-__device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-
-// Bounded spin of one lane until *w >= target (relaxed agent-scope polls, s_sleep
-// between them).  Gives up, raising *abort, once `deadline` (wall clock, 100 MHz)
-// passes or another workgroup raised it: every waiter of the launch then exits.
-__device__ __forceinline__ bool spin_ge(const uint32_t* w, uint32_t target, uint32_t* abort,
-                                     unsigned long long deadline) {
-    for (uint32_t n = 0;; n++) {
-        if (ld32<true>(w) >= target) return true;
-        if ((n & 15) == 15) {
-            if (ld32<true>(abort) || wall_clock64() > deadline) {
-                __hip_atomic_store((gu32*)abort, 1u, KB_RLX_AGENT);
-                return false;
-            }
-        }
-        __builtin_amdgcn_s_sleep(1);
-    }
-}
+// plain loads / stores of objects of 8-byte multiples (record headers, keys,
+// 16-B set-record units): the data crosses kernel boundaries only
+__device__ __forceinline__ uint32_t ld32(const void* p) { return *(const uint32_t*)p; }
+__device__ __forceinline__ void st32(void* p, uint32_t v) { *(uint32_t*)p = v; }
+__device__ __forceinline__ double ldd(const double* p) { return *p; }
+__device__ __forceinline__ void stdbl(double* p, double v) { *p = v; }
+template <typename T>
+__device__ __forceinline__ T ldobj(const T* p) { return *p; }
+template <typename T>
+__device__ __forceinline__ void stobj(T* p, const T& v) { *p = v; }
 
 // reference term (utils.go:136-143): r = L/avg - 1; r>0 ? r*r : r*r/2 (exact ops)
 __device__ __forceinline__ double term_x(double L, double avg) {
@@ -390,14 +328,12 @@ __device__ __forceinline__ void load_parts(const ScanArgs& a, long long base, Pa
     for (int k = 0; k < RC; k++) P.r[k] = *(const uint32_t*)(a.rep + (long long)k * a.Ppad + base);
 }
 
-template <bool PER>
 __device__ __forceinline__ void emit_global(const ScanArgs& a, const Contender& c) {
     uint32_t i = atomicAdd(a.ncont, 1u);
-    if (i < a.cont_cap) stobj<PER>(&a.cont[i], c);
-    else st32<PER>(a.cont_ovf, 1u);
+    if (i < a.cont_cap) stobj(&a.cont[i], c);
+    else st32(a.cont_ovf, 1u);
 }
 
-template <bool PER>
 __device__ __forceinline__ void emit(const ScanArgs& a, const Dedup& T, int kind, int s, int t, double w,
                                      unsigned long long iter) {
     KB_COUNT_WALK(a.ctl, 31, 1);
@@ -405,23 +341,23 @@ __device__ __forceinline__ void emit(const ScanArgs& a, const Dedup& T, int kind
         KB_COUNT_WALK(a.ctl, 30, 1);
         Contender c;
         c.s = s; c.t = t; c.w = w; c.iter = iter; c.kind = kind; c.pad = 0;
-        emit_global<PER>(a, c);
+        emit_global(a, c);
     }
 }
 
 // the 16-B units of a set record: from LDS (LSETS) or from memory
-template <int RC, bool LSETS, bool PER>
+template <int RC, bool LSETS>
 __device__ __forceinline__ void set_record(const ScanArgs& a, const uint4* s_set, uint32_t set,
                                            uint4 (&R)[sr_units(RC)]) {
     constexpr int U = sr_units(RC);
 #pragma unroll
-    for (int u = 0; u < U; u++) R[u] = LSETS ? s_set[set * U + u] : ldobj<PER>(a.setrec + (size_t)set * U + u);
+    for (int u = 0; u < U; u++) R[u] = LSETS ? s_set[set * U + u] : ldobj(a.setrec + (size_t)set * U + u);
 }
 
 // walk every allowed, non-replica target in bl order for one (partition, slot)
 // and emit the ones within 4*eps of the tile minimum g; stop once 8*eps is
 // exceeded (the approximate delta is monotone in the target load up to 2*eps).
-template <int RC, bool PER>
+template <int RC>
 __device__ void walk_targets(const ScanArgs& a, const Dedup& T, const double2* s_rf, const int16_t* s_pos,
                              const uint16_t* s_blm, const uint4 (&R)[sr_units(RC)], int kind, long long p,
                              int slot, int src, const uint32_t (&reps)[RC], int nrep, int set, double w, double ds,
@@ -441,7 +377,7 @@ __device__ void walk_targets(const ScanArgs& a, const Dedup& T, const double2* s
         for (int q = 0; q < RC; q++) isrep |= (q < nrep) && ((int)reps[q] == b);
         if (isrep) continue;
         const double d = ds + dtgt_f(s_rf[b], delta);
-        if (d <= g + 4.0 * eps) emit<PER>(a, T, kind, src, b, w, ib | (unsigned long long)s_pos[b]);
+        if (d <= g + 4.0 * eps) emit(a, T, kind, src, b, w, ib | (unsigned long long)s_pos[b]);
         if (d > g + 8.0 * eps) return;
     }
     if (nl < KR || last < 0) return;              // the set is exhausted
@@ -455,20 +391,20 @@ __device__ void walk_targets(const ScanArgs& a, const Dedup& T, const double2* s
         for (int q = 0; q < RC; q++) isrep |= (q < nrep) && ((int)reps[q] == b);
         if (isrep) continue;
         const double d = ds + dtgt_f(s_rf[b], delta);
-        if (d <= g + 4.0 * eps) emit<PER>(a, T, kind, src, b, w, ib | (unsigned long long)k);
+        if (d <= g + 4.0 * eps) emit(a, T, kind, src, b, w, ib | (unsigned long long)k);
         if (d > g + 8.0 * eps) return;
     }
 }
 
 // first allowed target in bl order that is not a replica (steps.go:192-201):
 // among the first RC+1 entries of the partition's set record
-template <int RC, bool LSETS, bool PER>
+template <int RC, bool LSETS>
 __device__ __forceinline__ int first_target(const ScanArgs& a, const uint4* s_set, uint32_t m,
                                             const uint32_t (&reps)[RC], int nrep, int* nelig) {
     constexpr int U = sr_units(RC);
     constexpr int KT = RC + 1;
     uint4 R[U];
-    set_record<RC, LSETS, PER>(a, s_set, meta_set(m), R);
+    set_record<RC, LSETS>(a, s_set, meta_set(m), R);
     *nelig = (int)rec_u16(R, 0);
     // slots past nrep compare against an id no record holds (ids < MAXB, NONE16 = padding);
     // padding is never a replica, so it is picked only when no valid target precedes it
@@ -497,8 +433,7 @@ __device__ __forceinline__ double dec(unsigned long long e) {
     return u2d(u);
 }
 
-// the control values one scan round runs on (from DevCtl for k_scan, from the
-// epoch's ScanCtl for k_plan)
+// the control values one scan round runs on (from DevCtl)
 struct ScanParams {
     int run;
     double inv_avg, eps, ubL, ubN;
@@ -507,38 +442,12 @@ struct ScanParams {
     int ubpass;                     // census-free round whose minima close an open bound
 };
 
-// replica rewrites of this launch's steps in one scan workgroup's tiles (k_plan):
-// the workgroup's prefetched and streamed partition words may predate them
-// (DESIGN.md "Persistent plan kernel"); applied to every tile after its load
-template <int RC>
-struct PatchTab {
-    int n;
-    const int32_t* p;
-    const uint32_t* meta;
-    const uint16_t* rep;            // [n][RC]
-};
-
-template <int RC>
-__device__ __forceinline__ void apply_patches(const PatchTab<RC>& pt, PartRaw<RC>& P, long long lane_base) {
-    for (int e = 0; e < pt.n; e++) {
-        const long long d = (long long)pt.p[e] - lane_base;
-        if (d != 0 && d != 1) continue;
-        const uint32_t m = pt.meta[e];
-        if (d == 0) P.m.x = m; else P.m.y = m;
-#pragma unroll
-        for (int k = 0; k < RC; k++) {
-            const uint32_t v = pt.rep[e * RC + k];
-            P.r[k] = d == 0 ? ((P.r[k] & 0xFFFF0000u) | v) : ((P.r[k] & 0xFFFFu) | (v << 16));
-        }
-    }
-}
-
-// One scan round of a workgroup over its tiles (tile0 = blockIdx.x, already loaded
-// into A): stage the tables, score, write the workgroup record.  PER: inside the
-// persistent plan launch (tables and records cross workgroups within the launch).
-template <int RC, bool LSETS, bool PER>
+// One scan round of a workgroup over its tiles (its first tile already loaded into
+// A): stage the tables, score, write the workgroup record.
+template <int RC, bool LSETS>
 __device__ __forceinline__ void scan_round(const ScanArgs& a, const ScanParams& q, unsigned char* smem,
-                                           PartRaw<RC>& A, const PatchTab<RC>& pt, unsigned long long t_in,
+                                           PartRaw<RC>& A,
+                                           unsigned long long t_in,
                                            int wg) {
     DevCtl* ctl = a.ctl;
     constexpr int U = sr_units(RC);
@@ -566,10 +475,10 @@ __device__ __forceinline__ void scan_round(const ScanArgs& a, const ScanParams& 
     // the lookup tables (one memory round trip, overlapping the first tile's loads)
     double rlo = HUGE_VAL, rhi = -HUGE_VAL;          // range of the relative loads (prune bound)
     for (int i = tid; i < a.B; i += SCAN_THREADS) {
-        const double r = ldd<PER>(a.r + i);
+        const double r = ldd(a.r + i);
         s_rf[i] = make_double2(r, fsq(r));
-        s_pos[i] = (int16_t)(int32_t)ld32<PER>(a.posm + i);
-        s_blm[i] = (uint16_t)ld32<PER>(a.blm + i);
+        s_pos[i] = (int16_t)(int32_t)ld32(a.posm + i);
+        s_blm[i] = (uint16_t)ld32(a.blm + i);
         rlo = r < rlo ? r : rlo;
         rhi = r > rhi ? r : rhi;
     }
@@ -577,7 +486,7 @@ __device__ __forceinline__ void scan_round(const ScanArgs& a, const ScanParams& 
     rlo = wave_min(rlo);
     rhi = wave_max(rhi);
     if (lane == 0) { s_rr[0][wid] = rlo; s_rr[1][wid] = rhi; }
-    if (LSETS) for (int i = tid; i < a.nsets * U; i += SCAN_THREADS) s_set[i] = ldobj<PER>(a.setrec + i);
+    if (LSETS) for (int i = tid; i < a.nsets * U; i += SCAN_THREADS) s_set[i] = ldobj(a.setrec + i);
     for (int i = tid; i < DEDUP_SCAN; i += SCAN_THREADS) { s_key[i] = NONE32; s_wb[i] = NONE64; s_it[i] = NONE64; }
     if (tid == 0) s_nk = 0;
     if (tid < 2) { s_benc[tid] = NONE64; s_bslot[tid] = NONE32; s_nkk[tid] = 0; }
@@ -588,7 +497,7 @@ __device__ __forceinline__ void scan_round(const ScanArgs& a, const ScanParams& 
     const bool tk_on = q.tk_on != 0;
     __syncthreads();
     const bool ub_open = ubN == HUGE_VAL || (a.allow_leader && ubL == HUGE_VAL);
-    if (!run || (a.dbg & 4) || (!PER && a.ubpass && !ub_open)) return;
+    if (!run || (a.dbg & 4) || (a.ubpass && !ub_open)) return;
     const bool census_off = (a.dbg & 1) || q.ubpass;
     // Lower-bound prune.  The source delta f(r_s - delta) - f(r_s) decreases and the
     // target delta f(r_t + delta) - f(r_t) increases with the relative load (f is
@@ -664,7 +573,7 @@ __device__ __forceinline__ void scan_round(const ScanArgs& a, const ScanParams& 
                 const uint32_t m = P.mt(j);
                 const uint32_t nrep = meta_nrep(m), nin = meta_nin(m), set = meta_set(m);
                 const uint32_t nelig = LSETS ? (uint32_t)((const uint16_t*)(s_set + (size_t)set * U))[0]
-                                             : (ld32<PER>(a.setrec + (size_t)set * U) & 0xFFFFu);
+                                             : (ld32(a.setrec + (size_t)set * U) & 0xFFFFu);
                 const bool ok = base + j < a.shard_end && meta_elig(m) && nrep > 0 && nelig > nin;
                 const uint32_t ne = ok ? nelig - nin : 0u;
                 if (a.allow_leader) cl += ne;
@@ -711,7 +620,7 @@ __device__ __forceinline__ void scan_round(const ScanArgs& a, const ScanParams& 
 #pragma unroll
             for (int k = 0; k < RC; k++) reps[k] = P.rp(k, j);
             int nelig;
-            const int tb0 = first_target<RC, LSETS, PER>(a, s_set, m, reps, nrep, &nelig);
+            const int tb0 = first_target<RC, LSETS>(a, s_set, m, reps, nrep, &nelig);
             const bool ok = base + j < a.shard_end && meta_elig(m) && nrep > 0 && tb0 >= 0;
             const double delta = P.wt(j) * inv_avg;
             const double dt = dtgt_f(s_rf[tb0 >= 0 ? tb0 : 0], delta);
@@ -755,7 +664,7 @@ __device__ __forceinline__ void scan_round(const ScanArgs& a, const ScanParams& 
 #pragma unroll
                 for (int k = 0; k < RC; k++) reps[k] = P.rp(k, j);
                 int nelig;
-                const int tb = first_target<RC, LSETS, PER>(a, s_set, m, reps, nrep, &nelig);
+                const int tb = first_target<RC, LSETS>(a, s_set, m, reps, nrep, &nelig);
                 if (tb < 0) continue;
                 const double delta = P.wt(j) * inv_avg;
                 const double dt = dtgt_f(s_rf[tb], delta);
@@ -781,9 +690,9 @@ __device__ __forceinline__ void scan_round(const ScanArgs& a, const ScanParams& 
                 for (int q2 = 1; q2 < RC; q2++) src = k == q2 ? reps[q2] : src;
                 const int nrep = (int)meta_nrep(m), set = (int)meta_set(m);
                 uint4 R[U];
-                set_record<RC, LSETS, PER>(a, s_set, (uint32_t)set, R);
+                set_record<RC, LSETS>(a, s_set, (uint32_t)set, R);
                 const double ds = dsrc_f(s_rf[src], w * inv_avg);
-                walk_targets<RC, PER>(a, T, s_rf, s_pos, s_blm, R, k ? 1 : 0, base + j, k, (int)src, reps, nrep,
+                walk_targets<RC>(a, T, s_rf, s_pos, s_blm, R, k ? 1 : 0, base + j, k, (int)src, reps, nrep,
                                       set, w, ds, k ? tN : tL, eps, inv_avg, nblm);
             }
         }
@@ -791,8 +700,10 @@ __device__ __forceinline__ void scan_round(const ScanArgs& a, const ScanParams& 
         wgN = tN < wgN ? tN : wgN;
     };
 
-    // ping-pong between two register sets: the next tile's loads are in flight
-    // while the current one is scored
+    // ping-pong between two register sets: A (this workgroup's first tile, issued by
+    // the caller before the tables) and Bq; while one tile is scored, the next one's
+    // loads are in flight.  (Issuing the second tile before the tables as well was
+    // measured slower: 10.6 vs 10.2 us per c3 scan.)
     const long long lane_off = a.shard_begin + (long long)tid * PER_LANE;
     PartRaw<RC> Bq;
     // (the prefetch is unconditional -- a last tile re-loads itself -- so that the
@@ -800,12 +711,10 @@ __device__ __forceinline__ void scan_round(const ScanArgs& a, const ScanParams& 
     for (; tile < a.ntiles; tile += 2 * a.nscan) {
         const int t1 = tile + a.nscan;
         load_parts<RC>(a, lane_off + (long long)(t1 < a.ntiles ? t1 : tile) * TILE, Bq);
-        if (PER) apply_patches<RC>(pt, A, lane_off + (long long)tile * TILE);
         score(A, lane_off + (long long)tile * TILE);
         if (t1 >= a.ntiles) break;
         const int t2 = t1 + a.nscan;
         load_parts<RC>(a, lane_off + (long long)(t2 < a.ntiles ? t2 : t1) * TILE, A);
-        if (PER) apply_patches<RC>(pt, Bq, lane_off + (long long)t1 * TILE);
         score(Bq, lane_off + (long long)t1 * TILE);
     }
     // workgroup record: counts, first-index predicates, minima, near-tie keys
@@ -846,8 +755,8 @@ __device__ __forceinline__ void scan_round(const ScanArgs& a, const ScanParams& 
             atomicMin(&s_benc[c.kind], myenc);
             atomicAdd(&s_nkk[c.kind], 1u);
             const uint32_t k = atomicAdd(&s_nk, 1u);
-            if (k < (uint32_t)TILE_KEYS) stobj<PER>(&keys[k], c);
-            else emit_global<PER>(a, c);
+            if (k < (uint32_t)TILE_KEYS) stobj(&keys[k], c);
+            else emit_global(a, c);
         }
     }
     __syncthreads();
@@ -883,13 +792,13 @@ __device__ __forceinline__ void scan_round(const ScanArgs& a, const ScanParams& 
             if (s_bslot[k] != NONE32) r.best[k] = dedup_entry(T, (int)s_bslot[k]);
             else { r.best[k].s = r.best[k].t = -1; r.best[k].w = 0.0; r.best[k].iter = NONE64; r.best[k].kind = k; r.best[k].pad = 0; }
         }
-        stobj<PER>(hdr, r);
+        stobj(hdr, r);
         if (fm) {
             uint32_t* fo = a.R.f(wg);
 #pragma unroll
-            for (int f = 0; f < NF; f++) st32<PER>(fo + f, fst[f]);
+            for (int f = 0; f < NF; f++) st32(fo + f, fst[f]);
         }
-        if (!PER && tk_on) {                           // the scan's interval (kernel timing)
+        if (tk_on) {                           // the scan's interval (kernel timing)
             atomicMin(&ctl->ts_beg, t_in);
             atomicMax(&ctl->ts_end, wall_clock64());
         }
@@ -904,6 +813,12 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
     DevCtl* ctl = a.ctl;
     if (a.listwg && (int)blockIdx.x == a.nscan) { if (!(a.dbg & 8)) do_list_op(ctl, a.L, &s_li); return; }
     const unsigned long long t_in = wall_clock64();
+    // a conditional bound pass returns at once unless a bound is open: decided before
+    // any partition word is loaded (it runs before every scan once a plan retried)
+    if (a.ubpass) {
+        const double ubL = ctl->ub[0], ubN = ctl->ub[1];
+        if (!(ubN == HUGE_VAL || (a.allow_leader && ubL == HUGE_VAL))) return;
+    }
     // every load that does not depend on the control block goes out first: the
     // first tile's stream, then the lookup tables (one memory round trip)
     PartRaw<RC> A;
@@ -916,76 +831,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
     q.heavy = ctl->heavy; q.nblm = ctl->nblm;
     q.tk_on = ctl->tk_on;
     q.ubpass = 0;
-    PatchTab<RC> pt{0, nullptr, nullptr, nullptr};
-    scan_round<RC, LSETS, false>(a, q, smem, A, pt, t_in, (int)blockIdx.x);
-}
-
-// --------------------------------------------------- persistent plan: scan role
-// Per epoch: prefetch the first tile (the partition words do not depend on the
-// epoch; rewrites of this launch are patched), wait for the resolver's epoch flag,
-// register the epoch's partition patch, run the round on the published tables,
-// publish the record (sc1 stores, drained) and arrive on this workgroup's shard.
-template <int RC, bool LSETS>
-__device__ void plan_scan_role(const ScanArgs& a, const PlanArgs& pa, unsigned char* smem, int wg) {
-    const int tid = threadIdx.x;
-    __shared__ int s_go;
-    __shared__ ScanCtl s_q;
-    __shared__ int32_t s_pp[PLAN_MAX_STEPS];
-    __shared__ uint32_t s_pm[PLAN_MAX_STEPS];
-    __shared__ uint16_t s_pr[PLAN_MAX_STEPS * RC];
-    __shared__ int s_npt;
-    if (tid == 0) s_npt = 0;
-    SyncBlk* sy = pa.sync;
-    for (uint32_t epoch = 1;; epoch++) {
-        PartRaw<RC> A;
-        if (!(pa.dbg & 2) && wg < a.ntiles)
-            load_parts<RC>(a, a.shard_begin + (long long)wg * TILE + (long long)tid * PER_LANE, A);
-        if (tid == 0) {
-            s_go = spin_ge(&sy->flag, epoch, &sy->abort, wall_clock64() + pa.timeout_ticks) ? 1 : 0;
-            if (pa.dbg & 1) { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent"); drain_stores(); }
-        }
-        __syncthreads();
-        if (!s_go) return;
-        if ((pa.dbg & 2) && wg < a.ntiles)
-            load_parts<RC>(a, a.shard_begin + (long long)wg * TILE + (long long)tid * PER_LANE, A);
-        // the epoch's parameters (sc1 loads, after the flag)
-        if (tid < (int)(sizeof(ScanCtl) / 8))
-            ((unsigned long long*)&s_q)[tid] = ld64<true>((const unsigned long long*)&sy->sc + tid);
-        __syncthreads();
-        if (!s_q.run) return;
-        // a rewritten partition in one of this workgroup's tiles joins the patch table
-        if (tid == 0 && s_q.patch_p >= 0) {
-            const long long d = (long long)s_q.patch_p - a.shard_begin;
-            const long long t = d / TILE;
-            if (d >= 0 && t < a.ntiles && (int)(t % a.nscan) == wg) {
-                int e = 0;
-                while (e < s_npt && s_pp[e] != s_q.patch_p) e++;
-                if (e < PLAN_MAX_STEPS) {
-                    s_pp[e] = s_q.patch_p;
-                    s_pm[e] = s_q.patch_meta;
-                    for (int k = 0; k < RC; k++) s_pr[e * RC + k] = s_q.patch_rep[k];
-                    if (e == s_npt) s_npt = e + 1;
-                }
-            }
-        }
-        ScanParams q;
-        q.run = 1;
-        q.inv_avg = s_q.inv_avg; q.eps = s_q.eps;
-        q.ubL = s_q.ub[0]; q.ubN = s_q.ub[1];
-        q.heavy = s_q.heavy; q.nblm = s_q.nblm;
-        q.tk_on = 0;
-        q.ubpass = s_q.ubpass;
-        __syncthreads();
-        PatchTab<RC> pt{s_npt, s_pp, s_pm, s_pr};
-        scan_round<RC, LSETS, true>(a, q, smem, A, pt, 0, wg);
-        // every storing wave drains, then one lane arrives for the workgroup (R1)
-        drain_stores();
-        __syncthreads();
-        if (tid == 0) {
-            if (pa.dbg & 1) { __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent"); drain_stores(); }
-            __hip_atomic_fetch_add((gu32*)&sy->arr[wg & (ARR_SHARDS - 1)], 1u, KB_RLX_AGENT);
-        }
-    }
+    scan_round<RC, LSETS>(a, q, smem, A, t_in, (int)blockIdx.x);
 }
 
 // --------------------------------------------------------------- k_step
@@ -1014,17 +860,17 @@ __device__ __forceinline__ double cont_delta_ld(const double* s_ld, const Conten
 
 // every near-tie contender of `kind` within 4*eps of g: the keys of the
 // records whose minimum is within 8*eps, then the raw spill buffer
-template <bool PER, typename F>
+template <typename F>
 __device__ void for_each_contender(const StepArgs& a, const double* s_ld, uint32_t ncont, int kind, double g,
                                    double eps, double inv_avg, F f) {
     const int nt = blockDim.x;
     for (int i = threadIdx.x; i < a.R.n; i += nt) {
         const RecHdr* h = a.R.h(i);
-        if (!(ldd<PER>(&h->dmin[kind]) <= g + 8.0 * eps)) continue;
+        if (!(ldd(&h->dmin[kind]) <= g + 8.0 * eps)) continue;
         const Contender* keys = a.R.k(i);
-        const int nk = (int)min(ld32<PER>(&h->nkeys), (uint32_t)a.R.cap);
+        const int nk = (int)min(ld32(&h->nkeys), (uint32_t)a.R.cap);
         for (int k = 0; k < nk; k++) {
-            const Contender c = ldobj<PER>(keys + k);
+            const Contender c = ldobj(keys + k);
             if (c.kind != kind) continue;
             if (cont_delta_ld(s_ld, c, inv_avg) <= g + 4.0 * eps) f(c);
         }
@@ -1032,7 +878,7 @@ __device__ void for_each_contender(const StepArgs& a, const double* s_ld, uint32
     if (a.use_spill) {
         const uint32_t n = min(ncont, a.cont_cap);
         for (uint32_t i = threadIdx.x; i < n; i += nt) {
-            const Contender c = ldobj<PER>(a.cont + i);
+            const Contender c = ldobj(a.cont + i);
             if (c.kind != kind) continue;
             if (cont_delta_ld(s_ld, c, inv_avg) <= g + 4.0 * eps) f(c);
         }
@@ -1043,28 +889,20 @@ __device__ void for_each_contender(const StepArgs& a, const double* s_ld, uint32
 // start, stores only at the end): the serial code never waits on a global RMW
 constexpr int CTL_WORDS = (int)(offsetof(DevCtl, stamps) / 4);
 
-// The serial half of one Balance() step (k_step, and the resolver of k_plan):
-// mode STEP_LOAD only stages the state (control block, broker tables, allowed-set
-// words) into LDS; STEP_RUN resolves the scan records (when prepped), applies the
-// change and preps the next step.  PER (k_plan): the state stays in LDS across
-// calls (load_state only on the first), the records and the spill counters come
-// from the scan workgroups of the same launch (sc1 loads), and the tables the
-// scans read (r, bl_move order and positions, set records) are written with sc1
-// stores; s_patch receives the partition the applied change rewrote.
-enum { STEP_LOAD = 0, STEP_RUN = 1 };
-template <bool PER>
-__device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C, bool load_state, int mode,
-                                          int32_t* s_patch) {
+// The serial half of one Balance() step (k_step): stage the control block, the
+// broker tables and the allowed-set words in LDS, resolve the scan records (when
+// prepped), apply the change and prep the next step.
+__device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
     DevCtl* ctl = a.ctl;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     constexpr int NW = STEP_THREADS / 64;
     const unsigned long long t_in = wall_clock64();
     KB_STAMP_BEGIN();
-    if (load_state && tid < CTL_WORDS) ((uint32_t*)&C)[tid] = ((const uint32_t*)ctl)[tid];
+    if (tid < CTL_WORDS) ((uint32_t*)&C)[tid] = ((const uint32_t*)ctl)[tid];
     auto write_back = [&]() {
         KB_STAMP_FLUSH(ctl);
         __syncthreads();
-        if (!PER && tid == 0 && C.tk_on) {
+        if (tid == 0 && C.tk_on) {
             // kernel timing: this launch, and the scan that ran before it (if any)
             C.tk_sum[1] += wall_clock64() - t_in;
             C.tk_n[1]++;
@@ -1109,16 +947,13 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C, bool loa
 
     // ---- one memory round trip: the broker state, the allowed-set words, the control
     // block and (speculatively: the buffer always exists) the first record's header
-    for (int b = tid; load_state && b < B; b += STEP_THREADS) {
+    for (int b = tid; b < B; b += STEP_THREADS) {
         s_ld[b] = a.load[b];
         s_e[b] = a.eb[b];
         s_fl[b] = a.bfl[b];
         s_ord[b] = a.order[b];
     }
-    // the LDS-resident state of k_plan keeps its flags across steps: the previous
-    // prep's touched marks go (a reload from memory never carries them)
-    for (int b = tid; !load_state && b < B; b += STEP_THREADS) s_fl[b] &= (uint8_t)~BF_TOUCHED;
-    if (load_state && a.sb_lds) {
+    if (a.sb_lds) {
         const int nq = a.nsets * a.W64;                   // 16-B loads (the rows are contiguous)
         for (int q = 2 * tid; q < nq; q += 2 * STEP_THREADS) {
             if (q + 1 < nq) *(uint4*)(s_sb + q) = *(const uint4*)(a.setbits + q);
@@ -1130,23 +965,17 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C, bool loa
     uint32_t hflg = 0, hfm = 0, hnk0 = 0, hnk1 = 0;
     Contender hb0, hb1;                              // the record's best keys
     hb0.s = hb1.s = -1;
-    if (mode == STEP_RUN && tid < a.R.n) {
-        const RecHdr h = ldobj<PER>(a.R.h(tid));
+    if (tid < a.R.n) {
+        const RecHdr h = ldobj(a.R.h(tid));
         hd0 = h.dmin[0]; hd1 = h.dmin[1];
         hc0 = h.cand[0]; hc1 = h.cand[1];
         hflg = h.flags & 1u; hfm = h.fmask;
         hnk0 = h.nkk[0]; hnk1 = h.nkk[1];
         hb0 = h.best[0]; hb1 = h.best[1];
     }
-    // the spill counters of the epoch (k_plan: the scan workgroups' atomics)
-    uint32_t sy_nc = 0, sy_ov = 0;
-    if (PER && mode == STEP_RUN && tid == 0) { sy_nc = ld32<true>(&a.sync->ncont); sy_ov = ld32<true>(&a.sync->cont_overflow); }
     dedup_clear(T);
     if (tid < 2) { s_nd[tid] = 0; s_li[tid] = -1; s_kfail[tid] = 0; }
     __syncthreads();                               // the control block copy
-    if (mode == STEP_LOAD) return;
-    if (PER && tid == 0) { C.ncont = sy_nc; C.cont_overflow = sy_ov; }   // read after the next barrier
-    if (tid == 0) s_patch[0] = -1;
     const int halted = C.halted;
     const bool do_res = C.prepped && C.steps < C.budget;
     const double eps = C.eps, inv_avg = C.inv_avg, U0h = C.U0;
@@ -1171,7 +1000,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C, bool loa
         unsigned long long c0 = hc0, c1 = hc1;
         uint32_t flg = hflg, fm = hfm;
         for (int i = tid + STEP_THREADS; i < a.R.n; i += STEP_THREADS) {
-            const RecHdr h = ldobj<PER>(a.R.h(i));
+            const RecHdr h = ldobj(a.R.h(i));
             d0 = h.dmin[0] < d0 ? h.dmin[0] : d0;
             d1 = h.dmin[1] < d1 ? h.dmin[1] : d1;
             c0 += h.cand[0]; c1 += h.cand[1];
@@ -1209,10 +1038,10 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C, bool loa
 #pragma unroll
             for (int q = 0; q < NF; q++) f[q] = NONE32;
             for (int i = tid; i < a.R.n; i += STEP_THREADS) {
-                if (!ld32<PER>(&a.R.h(i)->fmask)) continue;
+                if (!ld32(&a.R.h(i)->fmask)) continue;
                 const uint32_t* fi = a.R.f(i);
 #pragma unroll
-                for (int q = 0; q < NF; q++) f[q] = min(f[q], ld32<PER>(fi + q));
+                for (int q = 0; q < NF; q++) f[q] = min(f[q], ld32(fi + q));
             }
 #pragma unroll
             for (int q = 0; q < NF; q++) {
@@ -1255,13 +1084,13 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C, bool loa
 
         for (int i = tid; (need0 || need1) && i < a.R.n; i += STEP_THREADS) {
             const RecHdr* h = a.R.h(i);
-            const bool q0 = need0 && ldd<PER>(&h->dmin[0]) <= g0 + 8.0 * eps;
-            const bool q1 = need1 && ldd<PER>(&h->dmin[1]) <= g1 + 8.0 * eps;
+            const bool q0 = need0 && ldd(&h->dmin[0]) <= g0 + 8.0 * eps;
+            const bool q1 = need1 && ldd(&h->dmin[1]) <= g1 + 8.0 * eps;
             if (!q0 && !q1) continue;
             const Contender* keys = a.R.k(i);
-            const int nk = (int)min(ld32<PER>(&h->nkeys), (uint32_t)a.R.cap);
+            const int nk = (int)min(ld32(&h->nkeys), (uint32_t)a.R.cap);
             for (int k = 0; k < nk; k++) {
-                const Contender c = ldobj<PER>(keys + k);
+                const Contender c = ldobj(keys + k);
                 if (!(c.kind ? q1 : q0)) continue;
                 if (cont_delta_ld(s_ld, c, inv_avg) <= (c.kind ? g1 : g0) + 4.0 * eps &&
                     dedup_insert(T, c.kind, c.s, c.t, c.w, c.iter) < 0)
@@ -1275,7 +1104,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C, bool loa
         // raw spills of the scan (rare): every thread
         const uint32_t n = min(C.ncont, a.cont_cap);
         for (uint32_t i = tid; i < n; i += STEP_THREADS) {
-            const Contender c = ldobj<PER>(a.cont + i);
+            const Contender c = ldobj(a.cont + i);
             if (cont_delta_ld(s_ld, c, inv_avg) <= s_g[c.kind] + 4.0 * eps &&
                 dedup_insert(T, c.kind, c.s, c.t, c.w, c.iter) < 0)
                 s_kfail[c.kind] = 1;
@@ -1286,7 +1115,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C, bool loa
 
     // ================================================================ resolve
     if (do_res) {
-        if (!PER && pend) {                      // not consumed by a scan: do it here
+        if (pend) {                      // not consumed by a scan: do it here
             do_list_op(ctl, a.L, &s_i);
             if (tid == 0) { C.pending_list = 0; C.list_overflow = ctl->list_overflow; }
             __syncthreads();
@@ -1441,7 +1270,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C, bool loa
             // (every load is exact here, so every error bound is zero)
             double* s_Lm = s_e;
             auto exact_su = [&]() {
-                for (int k = tid; k < nblm0; k += STEP_THREADS) s_Lm[k] = s_ld[(int)ld32<PER>(a.blm + k)];
+                for (int k = tid; k < nblm0; k += STEP_THREADS) s_Lm[k] = s_ld[(int)ld32(a.blm + k)];
                 __syncthreads();
                 if (tid == 0) {
                     const double S = fold_lds(s_Lm, nblm0);
@@ -1555,7 +1384,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C, bool loa
                     sux = s_sux;
                     if (!fail && ndist == 1) {
                         if (tid == 0) {
-                            s_dv[0] = exact_unbalance_lds(s_Lm, nblm0, (int)ld32<PER>(a.posm + cw.s), (int)ld32<PER>(a.posm + cw.t),
+                            s_dv[0] = exact_unbalance_lds(s_Lm, nblm0, (int)ld32(a.posm + cw.s), (int)ld32(a.posm + cw.t),
                                                           s_ld[cw.s] - cw.w, s_ld[cw.t] + cw.w);
                             atomicAdd(&C.total_folds, 1ull);
                         }
@@ -1570,7 +1399,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C, bool loa
                         double bw = 0.0;
                         unsigned long long nf = 0;
                         auto consider = [&](const Contender& c) {
-                            const double u = exact_unbalance_lds(s_Lm, nblm0, (int)ld32<PER>(a.posm + c.s), (int)ld32<PER>(a.posm + c.t),
+                            const double u = exact_unbalance_lds(s_Lm, nblm0, (int)ld32(a.posm + c.s), (int)ld32(a.posm + c.t),
                                                                  s_ld[c.s] - c.w, s_ld[c.t] + c.w);
                             nf++;
                             if (u < bu || (u == bu && c.iter < bi)) { bu = u; bi = c.iter; bs = c.s; bt = c.t; bw = c.w; }
@@ -1579,7 +1408,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C, bool loa
                             for (int h = tid; h < DEDUP_STEP; h += STEP_THREADS)
                                 if (s_key[h] != NONE32 && (int)(s_key[h] >> 30) == kind) consider(dedup_entry(T, h));
                         } else {
-                            for_each_contender<PER>(a, s_ld, C.ncont, kind, g, eps, inv_avg, consider);
+                            for_each_contender(a, s_ld, C.ncont, kind, g, eps, inv_avg, consider);
                         }
                         nf = wave_sum(nf);
                         if (lane == 0 && nf) atomicAdd(&C.total_folds, nf);
@@ -1687,18 +1516,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C, bool loa
                     const uint32_t m = a.meta[p];
                     c = D.w * (double)((int)meta_nrep(m) + a.nc[p]);
                 }
-                // k_plan: the partition's words after the change (the scans' patch), read
-                // in the same round trip
-                uint32_t pm = 0, pr = 0;
-                if (PER) {
-                    if (lane < a.RC) pr = a.rep[(long long)lane * a.Ppad + p];
-                    if (lane == 0) pm = a.meta[p];
-                }
                 if (lane == 0) a.rep[(long long)slot * a.Ppad + p] = (uint16_t)to;
-                if (PER) {
-                    if (lane < a.RC) s_patch[2 + lane] = lane == slot ? to : (int)pr;
-                    if (lane == 0) { s_patch[0] = (int)p; s_patch[1] = (int)pm; }
-                }
                 act = lane < 2;
                 oldc = lane == 0 ? c : 0.0;
                 newc = lane == 0 ? 0.0 : c;
@@ -1754,10 +1572,6 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C, bool loa
                     const uint32_t nmeta = make_meta((uint32_t)nw, meta_want(m), meta_elig(m), bout ? 1u : 0u,
                                                      (uint32_t)__popcll(bin), meta_set(m));
                     if (lane == 0) a.meta[p] = nmeta;
-                    if (PER) {
-                        if (lane < a.RC) s_patch[2 + lane] = lane < nw ? rn : 0xFFFF;
-                        if (lane == 0) { s_patch[0] = (int)p; s_patch[1] = (int)nmeta; }
-                    }
                 }
                 if (state_changed) {
                     // contributions of getBrokerLoad (utils.go:92-105): the leader slot carries
@@ -1889,7 +1703,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C, bool loa
         const bool bkeys = do_res && tid < a.R.n;
         Contender bk0, bk1;
         bk0.s = bk1.s = -1;
-        if (bkeys) { bk0 = ldobj<PER>(&a.R.h(tid)->best[0]); bk1 = ldobj<PER>(&a.R.h(tid)->best[1]); }
+        if (bkeys) { bk0 = ldobj(&a.R.h(tid)->best[0]); bk1 = ldobj(&a.R.h(tid)->best[1]); }
         {
             double sS = 0.0, sE = 0.0;
             int cn = 0;
@@ -1921,7 +1735,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C, bool loa
                     v += ar * (1.0 + ar);
                     rm = ar > rm ? ar : rm;
                 }
-                stdbl<PER>(a.r + b, r);
+                stdbl(a.r + b, r);
             }
             // upper bound of the next step's minimum per kind: the best keys of the scan
             // just resolved whose partition and brokers the applied move did not touch
@@ -2072,8 +1886,8 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C, bool loa
                     if (flag[q]) {
                         if (pos == 0) C.light = b;
                         if (pos == nblm - 1) C.heavy = b;
-                        st32<PER>(a.blm + pos, (uint32_t)b); st32<PER>(a.posm + b, (uint32_t)pos); pos++;
-                    } else st32<PER>(a.posm + b, NONE32);
+                        st32(a.blm + pos, (uint32_t)b); st32(a.posm + b, (uint32_t)pos); pos++;
+                    } else st32(a.posm + b, NONE32);
                 }
             }
             if (tid == 0 && nblm == 0) { C.light = -1; C.heavy = -1; }
@@ -2212,8 +2026,8 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C, bool loa
                     // the first / last bl_move broker: getBL's lightest / heaviest
                     if (pos == 0) C.light = b;
                     if (pos == total - 1) C.heavy = b;
-                    st32<PER>(a.blm + pos, (uint32_t)b); st32<PER>(a.posm + b, (uint32_t)pos); pos++;
-                } else st32<PER>(a.posm + b, NONE32);
+                    st32(a.blm + pos, (uint32_t)b); st32(a.posm + b, (uint32_t)pos); pos++;
+                } else st32(a.posm + b, NONE32);
             }
         }
         if (tid == 0) {
@@ -2234,7 +2048,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C, bool loa
     const bool bkeys = do_res && !full && tid < a.R.n;
     Contender bk0, bk1;
     bk0.s = bk1.s = -1;
-    if (bkeys) { bk0 = ldobj<PER>(&a.R.h(tid)->best[0]); bk1 = ldobj<PER>(&a.R.h(tid)->best[1]); }
+    if (bkeys) { bk0 = ldobj(&a.R.h(tid)->best[0]); bk1 = ldobj(&a.R.h(tid)->best[1]); }
     // approximate S (exact in integral mode: integers below 2^52), total load error E
     double sS = 0.0, sE = 0.0;
     for (int b = tid; b < B; b += STEP_THREADS)
@@ -2257,7 +2071,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C, bool loa
             v += ar * (1.0 + ar);
             rm = ar > rm ? ar : rm;
         }
-        stdbl<PER>(a.r + b, r);
+        stdbl(a.r + b, r);
     }
     su = wave_sum(su); v = wave_sum(v); rm = wave_max(rm);
     // upper bound of the next step's minimum per kind: the near-tie keys of the scan
@@ -2373,7 +2187,6 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C, bool loa
         const int nwords = (a.nsets + 31) / 32;
         const unsigned long long lt = (1ull << lane) - 1ull;
         // each wave builds its records in LDS, then writes them as whole 16-B units
-        // (k_plan: write-through stores the scan workgroups read)
         constexpr int MAXU = sr_units(MAXR);
         __shared__ __align__(16) uint16_t s_rs[NW][G][8 * MAXU];
         if (tid == 0) s_cursor = 0;
@@ -2478,7 +2291,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C, bool loa
                 if (lane < ng * a.units) {
                     const int j = lane / a.units, u = lane - j * a.units;
                     const int set = s_mlist[g + j];
-                    stobj<PER>(a.setrec + (size_t)set * a.units + u, *(const uint4*)&s_rs[wid][j][8 * u]);
+                    stobj(a.setrec + (size_t)set * a.units + u, *(const uint4*)&s_rs[wid][j][8 * u]);
                 }
                 __builtin_amdgcn_wave_barrier();
             }
@@ -2493,142 +2306,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C, bool loa
 
 __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
     __shared__ DevCtl C;
-    __shared__ int32_t s_patch[2 + MAXR];
-    step_body<false>(a, C, true, STEP_RUN, s_patch);
-}
-
-// --------------------------------------------------- persistent plan: resolver
-// The serial half of every step of the launch, with the state resident in LDS:
-//   (prep) -> [bound pass: publish ubpass, wait, close the open bound]
-//          -> publish the epoch (ScanCtl + flag) -> pending list op (overlaps
-//             the scans) -> wait for every scan workgroup -> resolve + apply + prep
-// until the plan halts, needs exact loads, has used its budget or this launch's
-// PLAN_MAX_STEPS; then a run = 0 epoch sends every scan workgroup home.
-// (scan workgroup w = blockIdx.x - 1 arrives on shard w & 7)
-__device__ void plan_resolver_role(const StepArgs& a, const PlanArgs& pa) {
-    __shared__ DevCtl C;
-    __shared__ int32_t s_patch[2 + MAXR];
-    __shared__ int s_go, s_li;
-    constexpr int NW = STEP_THREADS / 64;
-    __shared__ double s_um[2][NW];
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    SyncBlk* sy = pa.sync;
-    uint32_t epoch = 0;
-    unsigned long long t_pub = 0, t_arr = 0;
-    if (tid == 0) s_patch[0] = -1;
-
-    // the epoch's scan parameters and the last step's partition rewrite (sc1), the
-    // spill counters reset, every storing wave drained, then the flag (R1)
-    auto publish = [&](int run, int ubpass) {
-        epoch++;
-        if (tid == 0) {
-            ScanCtl q;
-            q.inv_avg = C.inv_avg; q.eps = C.eps; q.ub[0] = C.ub[0]; q.ub[1] = C.ub[1];
-            q.run = run; q.ubpass = ubpass; q.heavy = C.heavy; q.nblm = C.nblm;
-            q.patch_p = s_patch[0]; q.patch_meta = (uint32_t)s_patch[1]; q.pad[0] = q.pad[1] = 0;
-            for (int k = 0; k < MAXR; k++) q.patch_rep[k] = (uint16_t)(k < a.RC ? s_patch[2 + k] : 0xFFFF);
-            stobj<true>(&sy->sc, q);
-            st32<true>(&sy->ncont, 0u);
-            st32<true>(&sy->cont_overflow, 0u);
-            s_patch[0] = -1;                               // the scans register it with this epoch
-        }
-        drain_stores();
-        __syncthreads();
-        if (tid == 0) {
-            if (pa.dbg & 1) { __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent"); drain_stores(); }
-            __hip_atomic_store((gu32*)&sy->flag, epoch, KB_RLX_AGENT);
-        }
-        t_pub = wall_clock64();
-    };
-    // wave 0, one lane per arrival shard; false once a spin gave up (the launch aborts)
-    auto wait_arrivals = [&]() -> bool {
-        if (wid == 0) {
-            bool ok = true;
-            if (lane < ARR_SHARDS && lane < pa.nscan) {
-                const uint32_t nk = (uint32_t)((pa.nscan - 1 - lane) / ARR_SHARDS + 1);
-                ok = spin_ge(&sy->arr[lane], epoch * nk, &sy->abort, wall_clock64() + pa.timeout_ticks);
-            }
-            const bool all = __ballot(!ok) == 0;
-            if (lane == 0) {
-                s_go = all ? 1 : 0;
-                if (pa.dbg & 1) { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent"); drain_stores(); }
-            }
-        }
-        __syncthreads();
-        t_arr = wall_clock64();
-        if (tid == 0 && C.tk_on) { C.tk_sum[0] += t_arr - t_pub; C.tk_n[0]++; }
-        return s_go != 0;
-    };
-    // a census-free round's minima close an open bound (k_ubinit's rule)
-    auto close_bound = [&]() {
-        double m0 = HUGE_VAL, m1 = HUGE_VAL;
-        for (int i = tid; i < a.R.n; i += STEP_THREADS) {
-            const RecHdr* h = a.R.h(i);
-            const double d0 = ldd<true>(&h->dmin[0]), d1 = ldd<true>(&h->dmin[1]);
-            m0 = d0 < m0 ? d0 : m0;
-            m1 = d1 < m1 ? d1 : m1;
-        }
-        m0 = wave_min(m0);
-        m1 = wave_min(m1);
-        if (lane == 0) { s_um[0][wid] = m0; s_um[1][wid] = m1; }
-        __syncthreads();
-        if (wid == 0) {
-            m0 = wave_min(lane < NW ? s_um[0][lane] : HUGE_VAL);
-            m1 = wave_min(lane < NW ? s_um[1][lane] : HUGE_VAL);
-            if (lane == 0) {
-                if (C.ub[1] == HUGE_VAL) C.ub[1] = m1;
-                if (a.allow_leader && C.ub[0] == HUGE_VAL) C.ub[0] = m0;
-            }
-        }
-        __syncthreads();
-    };
-
-    // one call site of the (large) step body: the state load, the prep of a fresh
-    // state, and every step's resolve + apply + prep
-    bool loaded = false, body = false;
-    int steps0 = 0;
-    for (;;) {
-        if (!loaded || body) {
-            step_body<true>(a, C, !loaded, loaded ? STEP_RUN : STEP_LOAD, s_patch);
-            if (!loaded) {
-                loaded = true;
-                steps0 = C.steps;
-                body = C.halted == H_RUN && !C.prepped;      // a fresh state: the prep first
-                continue;
-            }
-            body = false;
-            if (tid == 0 && C.tk_on && t_arr) {
-                C.tk_sum[1] += wall_clock64() - t_arr; C.tk_n[1]++;
-                a.ctl->tk_sum[0] = C.tk_sum[0]; a.ctl->tk_n[0] = C.tk_n[0];
-                a.ctl->tk_sum[1] = C.tk_sum[1]; a.ctl->tk_n[1] = C.tk_n[1];
-            }
-        }
-        const bool stop = C.halted != H_RUN || !C.prepped || C.steps >= C.budget || C.want_refresh ||
-                          C.steps - steps0 >= pa.max_steps;
-        if (stop) { publish(0, 0); break; }
-        if (C.ub[1] == HUGE_VAL || (a.allow_leader && C.ub[0] == HUGE_VAL)) {
-            publish(1, 1);
-            if (!wait_arrivals()) break;
-            close_bound();
-        }
-        publish(1, 0);
-        if (C.pending_list) {
-            // the per-broker list edit of the applied change, while the scans run
-            do_list_op(&C, a.L, &s_li);
-            if (tid == 0) { a.ctl->pending_list = C.pending_list; a.ctl->list_overflow = C.list_overflow; }
-        }
-        if (!wait_arrivals()) break;
-        body = true;
-    }
-}
-
-template <int RC, bool LSETS>
-__global__ __launch_bounds__(SCAN_THREADS) void k_plan(ScanArgs s, StepArgs t, PlanArgs p) {
-    extern __shared__ __align__(16) unsigned char smem[];
-    static_assert(SCAN_THREADS == STEP_THREADS, "one workgroup size for both roles");
-    // workgroup 0 resolves (dispatched first: it is resident whenever any scan is)
-    if (blockIdx.x == 0) plan_resolver_role(t, p);
-    else if ((int)blockIdx.x <= p.nscan) plan_scan_role<RC, LSETS>(s, p, smem, (int)blockIdx.x - 1);
+    step_body(a, C);
 }
 
 // ------------------------------------------------------------- k_listop
@@ -2896,48 +2574,6 @@ int step_static_lds() {
     hipFuncAttributes fa;
     if (hipFuncGetAttributes(&fa, (const void*)k_step) != hipSuccess) return -1;
     return (int)fa.sharedSizeBytes;
-}
-
-template <int RC>
-static void launch_plan_rc(const ScanArgs& s, const StepArgs& t, const PlanArgs& p, bool lds_sets, size_t lds,
-                           hipStream_t st) {
-    if (lds_sets) hipLaunchKernelGGL((k_plan<RC, true>), dim3(p.nscan + 1), dim3(SCAN_THREADS), lds, st, s, t, p);
-    else hipLaunchKernelGGL((k_plan<RC, false>), dim3(p.nscan + 1), dim3(SCAN_THREADS), lds, st, s, t, p);
-}
-
-void launch_plan(const ScanArgs& s, const StepArgs& t, const PlanArgs& p, int rc, bool lds_sets, size_t lds,
-                 hipStream_t st) {
-    switch (rc) {
-        case 1: launch_plan_rc<1>(s, t, p, lds_sets, lds, st); break;
-        case 2: launch_plan_rc<2>(s, t, p, lds_sets, lds, st); break;
-        case 3: launch_plan_rc<3>(s, t, p, lds_sets, lds, st); break;
-        case 4: launch_plan_rc<4>(s, t, p, lds_sets, lds, st); break;
-        case 6: launch_plan_rc<6>(s, t, p, lds_sets, lds, st); break;
-        case 8: launch_plan_rc<8>(s, t, p, lds_sets, lds, st); break;
-        case 12: launch_plan_rc<12>(s, t, p, lds_sets, lds, st); break;
-        default: launch_plan_rc<16>(s, t, p, lds_sets, lds, st); break;
-    }
-}
-
-template <int RC>
-static int plan_lds_rc(bool lds_sets) {
-    hipFuncAttributes fa;
-    const void* f = lds_sets ? (const void*)k_plan<RC, true> : (const void*)k_plan<RC, false>;
-    if (hipFuncGetAttributes(&fa, f) != hipSuccess) return -1;
-    return (int)fa.sharedSizeBytes;
-}
-
-int plan_static_lds(int rc, bool lds_sets) {
-    switch (rc) {
-        case 1: return plan_lds_rc<1>(lds_sets);
-        case 2: return plan_lds_rc<2>(lds_sets);
-        case 3: return plan_lds_rc<3>(lds_sets);
-        case 4: return plan_lds_rc<4>(lds_sets);
-        case 6: return plan_lds_rc<6>(lds_sets);
-        case 8: return plan_lds_rc<8>(lds_sets);
-        case 12: return plan_lds_rc<12>(lds_sets);
-        default: return plan_lds_rc<16>(lds_sets);
-    }
 }
 
 void launch_step(const StepArgs& a, hipStream_t st) {

@@ -32,7 +32,7 @@ struct ScanArgs {
     Recs R;                   // this scan's workgroup records (scan_recs layout)
     Contender* cont;          // spill buffer
     uint32_t cont_cap;
-    uint32_t* ncont;          // its fill counter and overflow flag (DevCtl's, or SyncBlk's in k_plan)
+    uint32_t* ncont;          // its fill counter and overflow flag (DevCtl's)
     uint32_t* cont_ovf;
     int listwg;               // 1: the last workgroup applies the pending list op
     int ubpass;               // 1: census-free bound pass (k_ubinit follows); returns at once
@@ -74,16 +74,6 @@ struct StepArgs {
     double min_unbalance, wmax;
     ChangeDev* log;
     Lists L;
-    SyncBlk* sync;            // k_plan: spill counters of the epoch (nullptr in k_step)
-};
-
-struct PlanArgs {
-    SyncBlk* sync;
-    int nscan;                // scan workgroups 1..nscan; workgroup 0 resolves
-    int max_steps;            // steps this launch may take (<= PLAN_MAX_STEPS)
-    unsigned long long timeout_ticks;   // bound of every spin (100 MHz wall clock)
-    int dbg;                  // diagnostic (KB_PLAN_DBG): 1 = agent release/acquire fences around
-                              // every hand-off, 2 = no first-tile prefetch before the epoch flag
 };
 
 struct RefreshArgs {
@@ -112,10 +102,6 @@ struct SumArgs {
 void launch_scan(const ScanArgs& a, int rc, bool lds_sets, size_t lds_bytes, hipStream_t st);
 int scan_blocks_per_cu(int rc, bool lds_sets, size_t lds_bytes);
 void launch_step(const StepArgs& a, hipStream_t st);
-// persistent plan launch: a.nscan scan workgroups + 1 resolver
-void launch_plan(const ScanArgs& s, const StepArgs& t, const PlanArgs& p, int rc, bool lds_sets,
-                 size_t lds_bytes, hipStream_t st);
-int plan_static_lds(int rc, bool lds_sets);
 int step_static_lds();
 // diagnostic: one workgroup rewrites the given tables in place (n = 0: nothing)
 void launch_ubinit(DevCtl* ctl, const Recs& R, int allow_leader, hipStream_t st);

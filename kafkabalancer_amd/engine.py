@@ -61,8 +61,7 @@ class kb_stats(C.Structure):
                 ("exact_folds", C.c_int64), ("scan_bytes", C.c_int64), ("device_ms", C.c_double),
                 ("n_brokers", C.c_int64), ("n_sets", C.c_int64), ("integral", C.c_int32),
                 ("max_replicas", C.c_int32), ("refreshes", C.c_int64), ("exact_halts", C.c_int64),
-                ("scan_workgroups", C.c_int64), ("retries", C.c_int64),
-                ("plan_launches", C.c_int64), ("plan_aborts", C.c_int64)]
+                ("scan_workgroups", C.c_int64), ("retries", C.c_int64)]
 
 
 _lib = None
@@ -119,7 +118,7 @@ def lib():
         L.kb_engine_sharded_resolve.restype = C.c_int
         L.kb_engine_sharded_collect.argtypes = [vp, C.POINTER(kb_change), C.c_int64, P64]
         L.kb_engine_sharded_collect.restype = C.c_int
-        if L.kb_abi_version() != 4:
+        if L.kb_abi_version() != 5:
             raise ImportError("libkbengine.so ABI mismatch")
         _lib = L
     return _lib

@@ -163,21 +163,30 @@ StepResult Planner::Step() {
 }
 
 std::vector<StepResult> Planner::Plan(int64_t n) {
+    // in chunks: the change buffer stays bounded whatever -max-reassign asks for
+    // (the reference loops until no change, kafkabalancer.go:177-233)
+    constexpr int64_t kChunk = 4096;
     std::vector<StepResult> out;
-    if (n <= 0) return out;
-    std::vector<kb_change> chs((size_t)n);
-    int64_t got = 0;
-    int rc = kb_engine_plan(eng_, n, chs.data(), &got);
-    for (int64_t i = 0; i < got; i++) {
-        int s = chs[(size_t)i].status;
-        int r = s == KB_CHANGE ? KB_CHANGE : (s == KB_NOCHANGE ? KB_NOCHANGE : rc);
-        out.push_back(apply(chs[(size_t)i], r));
-        if (r != KB_CHANGE) break;
-    }
-    if (got == 0 && rc < 0) {
-        kb_change z{};
-        z.status = rc;
-        out.push_back(apply(z, rc));
+    std::vector<kb_change> chs((size_t)std::min<int64_t>(std::max<int64_t>(n, 0), kChunk));
+    while (n > 0) {
+        const int64_t m = std::min<int64_t>(n, kChunk);
+        int64_t got = 0;
+        int rc = kb_engine_plan(eng_, m, chs.data(), &got);
+        for (int64_t i = 0; i < got; i++) {
+            int s = chs[(size_t)i].status;
+            int r = s == KB_CHANGE ? KB_CHANGE : (s == KB_NOCHANGE ? KB_NOCHANGE : rc);
+            out.push_back(apply(chs[(size_t)i], r));
+            if (r != KB_CHANGE) return out;
+        }
+        if (got == 0) {
+            if (rc < 0) {
+                kb_change z{};
+                z.status = rc;
+                out.push_back(apply(z, rc));
+            }
+            return out;
+        }
+        n -= got;
     }
     return out;
 }

@@ -105,6 +105,10 @@ CLI_VARIANTS = [
     (["-broker-ids=1,2,3,4,5,6", "-max-reassign=20"], dict(max_reassign=20, cfg=dict(brokers=[1, 2, 3, 4, 5, 6]))),
     (["-rebalance-leader", "-min-unbalance=0", "-max-reassign=6", "-complete-partition=false"],
      dict(max_reassign=6, complete_partition=False, cfg=dict(rebalance_leaders=True, min_unbalance=0.0))),
+    # a budget far beyond any plan: the planner runs in bounded chunks until no change
+    # (non-leader moves: -allow-leader plans can cycle forever, as in the reference)
+    (["-min-unbalance=0", "-max-reassign=1000000000", "-complete-partition=false"],
+     dict(max_reassign=1000000000, complete_partition=False, cfg=dict(min_unbalance=0.0))),
 ]
 
 

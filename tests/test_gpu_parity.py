@@ -303,37 +303,3 @@ def test_candidate_count_first_step():
         nin = inset[rows].sum(axis=1)
         want += int(((n_elig - nin) * 2).sum())
     assert cand == want
-
-
-# ------------------------------------- persistent plan kernel (KB_PERSIST=1)
-
-@pytest.mark.parametrize("variant", ["c1", "c3s", "c4s"])
-def test_persistent_plan_matches_oracle(variant, monkeypatch):
-    """The opt-in persistent launch (k_plan: scan workgroups + one resolver handing off
-    through write-through stores and an epoch flag) produces the oracle's plan."""
-    monkeypatch.setenv("KB_PERSIST", "1")
-    if variant == "c1":
-        pl = golden("test.json")
-        cfg = default_cfg(allow_leader=True)
-        steps = 12
-    elif variant == "c3s":
-        cl = synth.make_cluster(6000, 300, 3, "zipf", nsets=24, set_size=32, seed=11, with_names=True)
-        pl = synth.to_plist(cl)
-        cfg = default_cfg(allow_leader=True, min_unbalance=0.0)
-        steps = 12
-    else:
-        nr = np.zeros(6000, np.int64)
-        nr[[5, 900, 3000]] = 2
-        nr[[7, 1500, 4500]] = 4
-        cl = synth.make_cluster(6000, 300, 3, "zipf", seed=12, with_names=True, num_replicas=nr)
-        pl = synth.to_plist(cl)
-        cfg = default_cfg(min_unbalance=0.0, brokers=[b for b in range(1, 361) if not 280 <= b <= 300])
-        steps = 12
-    eng = E.Engine(pl, cfg)
-    ech, eerr = eng.plan(steps)
-    och, oerr, opl = oracle_plan(pl, cfg, steps)
-    assert_same_plan(ech, eerr, och, oerr)
-    assert eng.state() == opl.state()
-    st = eng.stats()
-    assert st["plan_launches"] >= 1 and st["plan_aborts"] == 0
-    eng.close()

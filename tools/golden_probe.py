@@ -23,4 +23,4 @@ print(json.dumps({"case": name, "env": {k: v for k, v in os.environ.items() if k
                   "ngot": len(got), "nwant": min(len(g["changes"]), steps), "diverge": div,
                   "at": [got[div], g["changes"][div]] if div is not None else None,
                   "err": str(err) if err else None,
-                  "stats": {k: st[k] for k in ("steps", "refreshes", "exact_halts", "retries", "plan_launches", "plan_aborts")}}))
+                  "stats": {k: st[k] for k in ("steps", "refreshes", "exact_halts", "retries")}}))
