@@ -20,6 +20,10 @@ def lib():
                                  C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]
         L.kb_cli_run.restype = C.c_int
         L.kb_cli_free.argtypes = [C.c_void_p]
+        L.kb_codec_roundtrip.argtypes = [C.c_char_p, C.c_size_t, C.c_int, C.POINTER(C.c_void_p),
+                                         C.POINTER(C.c_size_t), C.POINTER(C.c_double), C.POINTER(C.c_double),
+                                         C.POINTER(C.c_int64)]
+        L.kb_codec_roundtrip.restype = C.c_int
         _lib = L
     return _lib
 
@@ -37,3 +41,24 @@ def run(args, stdin=None, fail_output=False):
     lib().kb_cli_free(out)
     lib().kb_cli_free(err)
     return rc, o, e
+
+
+CODEC_DEFAULT, CODEC_DOM, CODEC_FAST = 0, 1, 2
+
+
+def codec_roundtrip(data, mode=CODEC_DEFAULT):
+    """Decode JSON `data` like GetPartitionListFromReader and encode it again like
+    WritePartitionList (codecs.go:15-27, 84-93).  Returns (rc, bytes, t_parse_s,
+    t_encode_s, n_partitions): rc 0 = encoded bytes, 1 = the error text, 2 = the
+    one-pass decoder gave up (mode CODEC_FAST only)."""
+    out = C.c_void_p()
+    olen = C.c_size_t()
+    tp, te = C.c_double(), C.c_double()
+    n = C.c_int64()
+    rc = lib().kb_codec_roundtrip(data, len(data), mode, C.byref(out), C.byref(olen), C.byref(tp), C.byref(te),
+                                  C.byref(n))
+    o = b""
+    if out.value:
+        o = C.string_at(out.value, olen.value)
+        lib().kb_cli_free(out)
+    return rc, o, tp.value, te.value, n.value

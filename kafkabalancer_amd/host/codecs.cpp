@@ -14,7 +14,9 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
 #include <set>
+#include <thread>
 #include <utility>
 
 namespace kbh {
@@ -43,25 +45,42 @@ static void shortest(double x, std::string& digits, int& e10) {
     while (digits.size() > 1 && digits.back() == '0') digits.pop_back();
 }
 
-std::string GoFloat(double x) {
-    if (x == 0) return std::signbit(x) ? "-0" : "0";
-    std::string d;
-    int e10;
-    shortest(x, d, e10);
-    std::string o = x < 0 ? "-" : "";
-    double a = std::fabs(x);
+// Go encoding/json float64 text appended to o (strconv 'f' / -1, 'e' outside
+// [1e-6, 1e21) with a negative exponent's leading zero removed)
+void GoFloatAppend(std::string& o, double x) {
+    if (x == 0) { o += std::signbit(x) ? "-0" : "0"; return; }
+    char buf[40];
+    auto r = std::to_chars(buf, buf + sizeof buf, std::fabs(x), std::chars_format::scientific);
+    // shortest round-trip digits d[0..nd) and decimal exponent e10 of d[0]
+    char d[24];
+    int nd = 0;
+    const char* q = buf;
+    for (; q < r.ptr && *q != 'e'; q++) if (*q != '.') d[nd++] = *q;
+    while (nd > 1 && d[nd - 1] == '0') nd--;
+    int e10 = 0;
+    std::from_chars(q + 1 + (q[1] == '+' ? 1 : 0), r.ptr, e10);
+    if (x < 0) o += '-';
+    const double a = std::fabs(x);
     if (a < 1e-6 || a >= 1e21) {
         o += d[0];
-        if (d.size() > 1) o += "." + d.substr(1);
-        o += "e";
-        if (e10 < 0) o += "-" + std::to_string(-e10);          // e-07 -> e-7 cleanup
-        else { o += "+"; if (e10 < 10) o += "0"; o += std::to_string(e10); }
-        return o;
+        if (nd > 1) { o += '.'; o.append(d + 1, (size_t)(nd - 1)); }
+        o += 'e';
+        if (e10 < 0) { o += '-'; e10 = -e10; }              // e-07 -> e-7 (Go's cleanup)
+        else { o += '+'; if (e10 < 10) o += '0'; }
+        char eb[8];
+        auto er = std::to_chars(eb, eb + sizeof eb, e10);
+        o.append(eb, er.ptr);
+        return;
     }
-    int point = e10 + 1;
-    if (point <= 0) o += "0." + std::string((size_t)-point, '0') + d;
-    else if (point >= (int)d.size()) o += d + std::string((size_t)(point - (int)d.size()), '0');
-    else o += d.substr(0, (size_t)point) + "." + d.substr((size_t)point);
+    const int point = e10 + 1;
+    if (point <= 0) { o += "0."; o.append((size_t)-point, '0'); o.append(d, (size_t)nd); }
+    else if (point >= nd) { o.append(d, (size_t)nd); o.append((size_t)(point - nd), '0'); }
+    else { o.append(d, (size_t)point); o += '.'; o.append(d + point, (size_t)(nd - point)); }
+}
+
+std::string GoFloat(double x) {
+    std::string o;
+    GoFloatAppend(o, x);
     return o;
 }
 
@@ -388,6 +407,185 @@ struct Decoder {
     }
 };
 
+// ---- fast path: well-formed documents of the PartitionList shape ----------
+// One pass, no DOM: values go straight into the PartitionList.  Whatever it does not
+// handle exactly like the DOM parser + Decoder above -- escapes in strings,
+// non-integer literals in integer fields, unknown keys, values of unexpected kinds,
+// syntax errors, out-of-range numbers -- makes it give up, and the caller runs the
+// DOM path, which produces the reference's result or error text.  (The DOM path
+// holds a node per number; at c3 size -- 1M partitions with 64-broker lists, ~280 MB
+// of JSON -- that is tens of GB.)
+struct Fast {
+    const char* p;
+    const char* e;
+    void ws() { while (p < e && (*p == ' ' || *p == '\t' || *p == '\n' || *p == '\r')) p++; }
+    bool lit(char c) {
+        ws();
+        if (p < e && *p == c) { p++; return true; }
+        return false;
+    }
+    bool null_lit() {
+        ws();
+        if (e - p >= 4 && memcmp(p, "null", 4) == 0) { p += 4; return true; }
+        return false;
+    }
+    // a string without escapes or control bytes (raw bytes >= 0x80 are copied, as
+    // the DOM parser does)
+    bool raw_str(const char*& s, size_t& n) {
+        ws();
+        if (p >= e || *p != '"') return false;
+        s = ++p;
+        while (p < e && *p != '"' && *p != '\\' && (unsigned char)*p >= 0x20) p++;
+        if (p >= e || *p != '"') return false;
+        n = (size_t)(p - s);
+        p++;
+        return true;
+    }
+    bool key(const char*& s, size_t& n) { return raw_str(s, n) && lit(':'); }
+    // an integer literal in int64 range (strtoll's accepted set for JSON integers)
+    bool i64(int64_t& v) {
+        ws();
+        bool neg = false;
+        if (p < e && *p == '-') { neg = true; p++; }
+        if (p >= e) return false;
+        uint64_t m = 0;
+        if (*p == '0') p++;
+        else if (*p >= '1' && *p <= '9') {
+            int nd = 0;
+            while (p < e && *p >= '0' && *p <= '9') {
+                if (++nd > 19) return false;
+                m = m * 10 + (uint64_t)(*p - '0');
+                p++;
+            }
+            if (nd == 19 && m > (neg ? 9223372036854775808ull : 9223372036854775807ull)) return false;
+        } else return false;
+        if (p < e && (*p == '.' || *p == 'e' || *p == 'E')) return false;   // type error (DOM)
+        v = neg ? (int64_t)(0 - m) : (int64_t)m;
+        return true;
+    }
+    // a JSON number (the DOM grammar), converted like strtod; any range issue -> give up
+    bool f64(double& v) {
+        ws();
+        const char* s = p;
+        if (p < e && *p == '-') p++;
+        if (p >= e) return false;
+        if (*p == '0') p++;
+        else if (*p >= '1' && *p <= '9') { while (p < e && *p >= '0' && *p <= '9') p++; }
+        else return false;
+        if (p < e && *p == '.') {
+            p++;
+            if (p >= e || !(*p >= '0' && *p <= '9')) return false;
+            while (p < e && *p >= '0' && *p <= '9') p++;
+        }
+        if (p < e && (*p == 'e' || *p == 'E')) {
+            p++;
+            if (p < e && (*p == '+' || *p == '-')) p++;
+            if (p >= e || !(*p >= '0' && *p <= '9')) return false;
+            while (p < e && *p >= '0' && *p <= '9') p++;
+        }
+        auto r = std::from_chars(s, p, v);
+        return r.ec == std::errc() && r.ptr == p && std::isfinite(v);
+    }
+    std::vector<int64_t> tmp;                          // element staging: one exact allocation per list
+    bool ints(Slice& out) {
+        if (null_lit()) { out = Slice(); return true; }
+        if (!lit('[')) return false;
+        tmp.clear();
+        if (!lit(']')) {
+            for (;;) {
+                int64_t x;
+                if (!i64(x)) return false;
+                tmp.push_back(x);
+                if (lit(',')) continue;
+                if (lit(']')) break;
+                return false;
+            }
+        }
+        out.arr = std::make_shared<std::vector<int64_t>>(tmp.begin(), tmp.end());
+        out.len = tmp.size();
+        return true;
+    }
+    static bool is(const char* s, size_t n, const char* name) {
+        const size_t m = strlen(name);
+        if (n != m) return false;
+        for (size_t i = 0; i < n; i++) if (tolower((unsigned char)s[i]) != name[i]) return false;
+        return true;
+    }
+    bool partition(Partition& q) {
+        if (null_lit()) return true;
+        if (!lit('{')) return false;
+        if (lit('}')) return true;
+        for (;;) {
+            const char* k;
+            size_t n;
+            if (!key(k, n)) return false;
+            bool ok;
+            if (is(k, n, "topic")) {
+                const char* s;
+                size_t m;
+                ok = null_lit() || (raw_str(s, m) && (q.topic.assign(s, m), true));
+            } else if (is(k, n, "partition")) ok = null_lit() || i64(q.partition);
+            else if (is(k, n, "replicas")) ok = ints(q.replicas);
+            else if (is(k, n, "weight")) ok = null_lit() || f64(q.weight);
+            else if (is(k, n, "num_replicas")) ok = null_lit() || i64(q.num_replicas);
+            else if (is(k, n, "brokers")) ok = ints(q.brokers);
+            else if (is(k, n, "num_consumers")) ok = null_lit() || i64(q.num_consumers);
+            else ok = false;
+            if (!ok) return false;
+            if (lit(',')) continue;
+            if (lit('}')) return true;
+            return false;
+        }
+    }
+    bool plist(PartitionList& pl) {
+        if (!lit('{')) return false;
+        if (lit('}')) return true;
+        for (;;) {
+            const char* k;
+            size_t n;
+            if (!key(k, n)) return false;
+            if (is(k, n, "version")) {
+                if (!null_lit() && !i64(pl.version)) return false;
+            } else if (is(k, n, "partitions")) {
+                if (null_lit()) { pl.partitions.clear(); pl.nil_partitions = true; }
+                else {
+                    if (!lit('[')) return false;
+                    pl.partitions.clear();
+                    pl.nil_partitions = false;
+                    // (a reserve from the document size: partition objects are >= 16 bytes)
+                    pl.partitions.reserve(std::min<size_t>((size_t)(e - p) / 64 + 16, 1u << 26));
+                    if (!lit(']')) {
+                        for (;;) {
+                            pl.partitions.emplace_back();
+                            if (!partition(pl.partitions.back())) return false;
+                            if (lit(',')) continue;
+                            if (lit(']')) break;
+                            return false;
+                        }
+                    }
+                }
+            } else return false;
+            if (lit(',')) continue;
+            if (lit('}')) return true;
+            return false;
+        }
+    }
+};
+
+}  // namespace
+
+bool g_codec_dom_only = false;
+
+bool FastDecodePartitionList(const std::string& in, PartitionList* out) {
+    PartitionList pl;
+    Fast f{in.data(), in.data() + in.size(), {}};
+    if (!f.plist(pl)) return false;
+    *out = std::move(pl);
+    return true;
+}
+
+namespace {
+
 // Atoi with the reference's ignored error: value on success, 0 otherwise
 int64_t atoi_go(const std::string& s) {
     if (s.empty()) return 0;
@@ -416,14 +614,17 @@ std::string GetPartitionListFromReader(const std::string& in, bool json,
                                        const std::vector<std::string>& topics, PartitionList* out) {
     PartitionList pl;
     if (json) {
-        Parser ps(in);
-        ps.ws();
-        if (ps.i >= in.size()) return "failed parsing json: EOF";
-        JVal v;
-        if (!ps.value(v, "looking for beginning of value")) return "failed parsing json: " + ps.err;
-        Decoder d;
-        d.plist(v, pl);
-        if (!d.err.empty()) return "failed parsing json: " + d.err;
+        if (g_codec_dom_only || !FastDecodePartitionList(in, &pl)) {
+            pl = PartitionList();
+            Parser ps(in);
+            ps.ws();
+            if (ps.i >= in.size()) return "failed parsing json: EOF";
+            JVal v;
+            if (!ps.value(v, "looking for beginning of value")) return "failed parsing json: " + ps.err;
+            Decoder d;
+            d.plist(v, pl);
+            if (!d.err.empty()) return "failed parsing json: " + d.err;
+        }
         if (pl.version != 1)
             return "wrong partition list version: expected 1, got " + std::to_string((long long)pl.version);
     } else {
@@ -515,38 +716,78 @@ static void json_string(std::string& o, const std::string& s) {
     o += '"';
 }
 
+static void json_int(std::string& o, int64_t v) {
+    char b[24];
+    auto r = std::to_chars(b, b + sizeof b, v);
+    o.append(b, r.ptr);
+}
+
 static void json_ints(std::string& o, const Slice& s) {
     if (s.nil()) { o += "null"; return; }
     o += '[';
     for (size_t i = 0; i < s.len; i++) {
         if (i) o += ',';
-        o += std::to_string((long long)s.at(i));
+        json_int(o, s.at(i));
     }
     o += ']';
 }
 
+static void encode_partition(std::string& o, const Partition& p) {
+    o += "{\"topic\":";
+    json_string(o, p.topic);
+    o += ",\"partition\":";
+    json_int(o, p.partition);
+    o += ",\"replicas\":";
+    json_ints(o, p.replicas);
+    if (p.weight != 0) { o += ",\"weight\":"; GoFloatAppend(o, p.weight); }
+    if (p.num_replicas != 0) { o += ",\"num_replicas\":"; json_int(o, p.num_replicas); }
+    if (!p.brokers.nil() && p.brokers.len > 0) { o += ",\"brokers\":"; json_ints(o, p.brokers); }
+    if (p.num_consumers != 0) { o += ",\"num_consumers\":"; json_int(o, p.num_consumers); }
+    o += '}';
+}
+
+static size_t encode_estimate(const PartitionList& pl, size_t a, size_t b) {
+    size_t est = 0;
+    for (size_t i = a; i < b; i++) {
+        const Partition& p = pl.partitions[i];
+        est += 96 + p.topic.size() + 8 * (p.replicas.len + p.brokers.len);
+    }
+    return est;
+}
+
+// Large lists are encoded in contiguous slices by several threads (the bytes do
+// not depend on the split: every partition's text is independent of the others)
 std::string EncodePartitionList(PartitionList& pl) {
     pl.version = 1;                                           // codecs.go:86
     std::string o = "{\"version\":1,\"partitions\":";
-    if (pl.nil_partitions && pl.partitions.empty()) o += "null";
-    else {
-        o += '[';
-        for (size_t i = 0; i < pl.partitions.size(); i++) {
-            const Partition& p = pl.partitions[i];
-            if (i) o += ',';
-            o += "{\"topic\":";
-            json_string(o, p.topic);
-            o += ",\"partition\":" + std::to_string((long long)p.partition) + ",\"replicas\":";
-            json_ints(o, p.replicas);
-            if (p.weight != 0) o += ",\"weight\":" + GoFloat(p.weight);
-            if (p.num_replicas != 0) o += ",\"num_replicas\":" + std::to_string((long long)p.num_replicas);
-            if (!p.brokers.nil() && p.brokers.len > 0) { o += ",\"brokers\":"; json_ints(o, p.brokers); }
-            if (p.num_consumers != 0) o += ",\"num_consumers\":" + std::to_string((long long)p.num_consumers);
-            o += '}';
+    if (pl.nil_partitions && pl.partitions.empty()) { o += "null}\n"; return o; }
+    const size_t n = pl.partitions.size();
+    unsigned nt = n < 65536 ? 1u : std::thread::hardware_concurrency();
+    if (const char* v = getenv("KB_CODEC_THREADS")) nt = (unsigned)atoi(v);     // tests / benches
+    nt = (unsigned)std::max<size_t>(1, std::min<size_t>({(size_t)nt, 16, n}));
+    std::vector<std::string> part(nt);
+    auto work = [&](unsigned t) {
+        const size_t a = n * t / nt, b = n * (t + 1) / nt;
+        std::string& s = part[t];
+        s.reserve(encode_estimate(pl, a, b));
+        for (size_t i = a; i < b; i++) {
+            if (i) s += ',';
+            encode_partition(s, pl.partitions[i]);
         }
-        o += ']';
+    };
+    if (nt == 1) work(0);
+    else {
+        std::vector<std::thread> th;
+        for (unsigned t = 1; t < nt; t++) th.emplace_back(work, t);
+        work(0);
+        for (auto& x : th) x.join();
     }
-    o += "}\n";
+    size_t tot = o.size() + 3;
+    for (const auto& s : part) tot += s.size();
+    o.reserve(tot);
+    o += '[';
+    for (auto& s : part) { o += s; std::string().swap(s); }
+    o += "]}\n";
     return o;
 }
 
