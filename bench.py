@@ -240,9 +240,11 @@ def main():
         names = ["prep.S+r+ubloop", "step.loads", "res.reduce", "res.pred", "res.move", "res.apply(tail)", "prep.sort", None,
                  "prep.blm+cert", "prep.reduce+eps", "prep.sets", "res.move->apply", "loads.bro+ctl", "loads.rec_reduce", "loads.keys", None, "sets.mark", "eps.sync1", "eps.wave0red", "sets.list", "sets.build", "keys.pre", "keys.insert"]
         counts = {"waves_scored": 7, "waves_gated_in": 15, "emits": 31, "spills": 30, "walks": 29, "walk_steps": 28, "walk_global": 27}
-        print(json.dumps({"k_step_clock_mhz": 100.0 * st[25] / max(st[24], 1),
+        mhz = 100.0 * st[25] / max(st[24], 1)           # shader clock (the phase stamps' unit)
+        names = names + ["loads.broker", None, None, "stamp.overhead", "loads.setbits", "loads.hdr"]
+        print(json.dumps({"k_step_clock_mhz": mhz,
                           "k_step_us": st[24] / 100.0 / n,
-                          "stamps_us_per_step": {k: st[i] / 100.0 / n for i, k in enumerate(names) if k},
+                          "stamps_us_per_step": {k: st[i] / mhz / n for i, k in enumerate(names) if k},
                           "counts_per_step": {k: st[i] / n for k, i in counts.items()},
                           "stats": eng.stats()}))
         return

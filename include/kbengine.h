@@ -135,6 +135,8 @@ typedef struct {
     int64_t scan_workgroups;        /* k_scan workgroups (one record each) */
     int64_t retries;                /* steps re-scanned with the census bound tightened to the
                                        step minimum after a near-tie spill overflow (ABI 3) */
+    int64_t spill_grows;            /* near-tie spill buffer growths (exact ties over many
+                                       brokers; the step ran again, ABI 5) */
 } kb_stats;
 
 typedef struct kb_engine kb_engine;

@@ -84,6 +84,7 @@ struct kb_engine {
     unsigned char* recs = nullptr;
     Contender* cont = nullptr;
     uint32_t cont_cap = 1u << 20;
+    int64_t spill_grows = 0;           // spill buffer growths (grow_spill)
     Lists L{nullptr, nullptr, nullptr, nullptr};
     DevCtl* ctl = nullptr;
     ChangeDev* log = nullptr;
@@ -472,6 +473,7 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
     HIPCHK(dalloc(&e->bset_off, e->B + 1));
     HIPCHK(dalloc(&e->bset_ids, hbi.size()));
     HIPCHK(dalloc(&e->recs, (size_t)std::max<int64_t>(e->nscan, 1) * WGREC_BYTES));
+    if (const char* v = getenv("KB_CONT_CAP")) e->cont_cap = (uint32_t)std::max(1, atoi(v));   // tests: growth path
     HIPCHK(dalloc(&e->cont, e->cont_cap));
     HIPCHK(dalloc(&e->ctl, 1));
     e->logcap = 1024;
@@ -784,6 +786,36 @@ static int ensure_log(kb_engine* e, int64_t max_steps) {
     return KB_OK;
 }
 
+// The near-tie spill buffer overflowed with the census bound already at the step
+// minimum (exact ties over many brokers): 8x the capacity, up to kContMax, and the
+// halted step runs again.  Only past kContMax is it a capacity error.
+static const uint32_t kContMax = 1u << 26;   // 64M candidates (2 GiB)
+static int grow_spill(kb_engine* e) {
+    if (e->cont_cap >= kContMax) {
+        e->last_err = "engine capacity: more than " + std::to_string(kContMax) + " near-tied candidates in one step";
+        return KB_ERR_CAPACITY;
+    }
+    const uint32_t cap = std::min<uint32_t>(kContMax, e->cont_cap * 8u);
+    Contender* nc = nullptr;
+    if (dalloc(&nc, cap) != hipSuccess) {
+        e->last_err = "cannot allocate the near-tie spill buffer";
+        return KB_ERR_CAPACITY;
+    }
+    HIPCHK(hipStreamSynchronize(e->st));
+    hipFree(e->cont);
+    e->cont = nc;
+    e->cont_cap = cap;
+    e->spill_grows++;
+    DevCtl c = *e->h_ctl;
+    c.halted = H_RUN;
+    c.ncont = 0;
+    c.cont_overflow = 0;
+    HIPCHK(hipMemcpyAsync(e->ctl, &c, sizeof c, hipMemcpyHostToDevice, e->st));
+    HIPCHK(hipStreamSynchronize(e->st));
+    *e->h_ctl = c;
+    return KB_OK;
+}
+
 // run up to max_steps Balance() calls device-resident; returns the number of
 // log entries written (changes + the terminating no-change / error)
 static int run_steps(kb_engine* e, int64_t max_steps) {
@@ -810,6 +842,12 @@ static int run_steps(kb_engine* e, int64_t max_steps) {
         const DevCtl& c = *e->h_ctl;
         if (c.total_retries > 0) e->ub_mode = true;
         if (c.halted == H_DONE) break;
+        if (c.halted == H_NEED_SPILL) {
+            // more near-tied candidates than the spill buffer holds: grow it, run the step again
+            const int rc = grow_spill(e);
+            if (rc != KB_OK) return rc;
+            continue;
+        }
         if (c.halted == H_NEED_EXACT || (c.want_refresh && c.steps - steps0 < max_steps)) {
             const int logpos = c.logpos;
             if (refresh(e) != KB_OK) return KB_ERR_HIP;
@@ -937,6 +975,7 @@ extern "C" int kb_engine_stats(kb_engine* e, kb_stats* o) {
     o->exact_halts = (int64_t)c.total_exact_halts;
     o->scan_workgroups = e->nscan;
     o->retries = (int64_t)c.total_retries;
+    o->spill_grows = e->spill_grows;
     return KB_OK;
 }
 

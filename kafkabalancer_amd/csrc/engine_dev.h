@@ -16,6 +16,9 @@ constexpr int SHARD_ALIGN = 1024;   // shard boundaries (multi-GPU) are multiple
 #define KB_STEP_THREADS 1024
 #endif
 constexpr int STEP_THREADS = KB_STEP_THREADS;  // k_step: one workgroup
+#ifndef KB_ABL
+#define KB_ABL 0                    // diagnostic ablation builds only (tools/ablate.sh)
+#endif
 constexpr uint32_t NONE32 = 0xFFFFFFFFu;
 constexpr unsigned long long NONE64 = ~0ull;
 constexpr uint16_t NONE16 = 0xFFFFu;
@@ -144,7 +147,9 @@ struct ChangeDev {
 };
 
 // halted codes
-enum { H_RUN = 0, H_DONE = 1, H_NEED_EXACT = 2 };
+// (H_NEED_SPILL: the near-tie spill buffer overflowed with the census bound already
+// at the step minimum; the host grows the buffer and the step runs again)
+enum { H_RUN = 0, H_DONE = 1, H_NEED_EXACT = 2, H_NEED_SPILL = 3 };
 
 struct DevCtl {
     int32_t halted, steps, logpos, logcap;
@@ -163,7 +168,8 @@ struct DevCtl {
     unsigned long long tk_sum[2], tk_n[2];
     int32_t tk_on, tk_pad;
     // diagnostic phase stamps (builds with -DKB_STAMPS): accumulated
-    // wall_clock64 ticks (100 MHz) per phase of k_step
+    // shader-clock ticks (clock64) per phase of k_step; [24]/[25] the wall-clock
+    // (100 MHz) and shader-clock length of k_step; [26] one stamp's own cost
     unsigned long long stamps[32];
     // the running scan's interval: earliest workgroup start, latest end (atomics;
     // outside the block k_step copies to LDS and back)
@@ -171,32 +177,40 @@ struct DevCtl {
 };
 
 #ifdef KB_STAMPS
-// phase ticks accumulate in LDS (a global read-modify-write per stamp would add
-// a memory round trip to every phase); KB_STAMP_FLUSH adds them to ctl->stamps
+// Wave 0's timeline: thread 0 writes the shader clock of each stamp point to LDS
+// (one s_memtime + one ds_write: no barrier, no read-modify-write, nothing live in
+// registers, so the measured code keeps its synchronisation and, as far as the
+// compiler allows, its register allocation).  At the end thread 0 orders the points
+// by time and charges each one the interval since the previous point (or the start);
+// a point hit twice in one launch keeps its last time.  [24] / [25]: the launch's
+// wall-clock (100 MHz) / shader-clock length; [29] / [30]: the start times.
 #define KB_STAMP_BEGIN()                                                        \
     __shared__ unsigned long long _kb_st[32];                                   \
-    if (threadIdx.x < 32) _kb_st[threadIdx.x] = 0;                              \
-    unsigned long long _kb_t0 = wall_clock64();                                 \
-    const unsigned long long _kb_r0 = _kb_t0, _kb_c0 = clock64()
+    if (threadIdx.x < 29) _kb_st[threadIdx.x] = 0;                              \
+    if (threadIdx.x == 0) { _kb_st[29] = clock64(); _kb_st[30] = wall_clock64(); } \
+    KB_STAMP(ctl, 26)
 #define KB_STAMP(ctl, i)                                                        \
     do {                                                                        \
-        __syncthreads();                                                        \
-        if (threadIdx.x == 0) {                                                 \
-            unsigned long long _t = wall_clock64();                             \
-            _kb_st[i] += _t - _kb_t0;                                           \
-            _kb_t0 = _t;                                                        \
-        }                                                                       \
+        if (threadIdx.x == 0) _kb_st[i] = clock64();                            \
     } while (0)
 #define KB_STAMP_FLUSH(ctl)                                                     \
     do {                                                                        \
         __syncthreads();                                                        \
         if (threadIdx.x == 0) {                                                 \
-            _kb_st[24] += wall_clock64() - _kb_r0;                              \
-            _kb_st[25] += clock64() - _kb_c0;                                   \
+            const unsigned long long _c = clock64(), _w = wall_clock64();       \
+            unsigned long long _d[24];                                          \
+            for (int _i = 0; _i < 24; _i++) {                                   \
+                const unsigned long long _ti = _kb_st[_i];                      \
+                unsigned long long _p = _kb_st[29];                             \
+                for (int _j = 0; _j < 29; _j++)                                 \
+                    if (_j != 24 && _j != 25 && _kb_st[_j] < _ti && _kb_st[_j] > _p) _p = _kb_st[_j]; \
+                _d[_i] = _ti ? _ti - _p : 0;                                    \
+            }                                                                   \
+            for (int _i = 0; _i < 24; _i++) if (_d[_i]) atomicAdd(&(ctl)->stamps[_i], _d[_i]); \
+            atomicAdd(&(ctl)->stamps[24], _w - _kb_st[30]);                     \
+            atomicAdd(&(ctl)->stamps[25], _c - _kb_st[29]);                     \
         }                                                                       \
         __syncthreads();                                                        \
-        if (threadIdx.x < 32 && _kb_st[threadIdx.x])                            \
-            atomicAdd(&(ctl)->stamps[threadIdx.x], _kb_st[threadIdx.x]);        \
     } while (0)
 #define KB_COUNT(ctl, i, v) atomicAdd(&(ctl)->stamps[i], (unsigned long long)(v))
 #else

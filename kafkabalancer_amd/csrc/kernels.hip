@@ -953,6 +953,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
         s_fl[b] = a.bfl[b];
         s_ord[b] = a.order[b];
     }
+    KB_STAMP(ctl, 23);
     if (a.sb_lds) {
         const int nq = a.nsets * a.W64;                   // 16-B loads (the rows are contiguous)
         for (int q = 2 * tid; q < nq; q += 2 * STEP_THREADS) {
@@ -960,6 +961,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
             else s_sb[q] = a.setbits[q];
         }
     }
+    KB_STAMP(ctl, 27);
     double hd0 = HUGE_VAL, hd1 = HUGE_VAL;
     unsigned long long hc0 = 0, hc1 = 0;
     uint32_t hflg = 0, hfm = 0, hnk0 = 0, hnk1 = 0;
@@ -973,6 +975,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
         hnk0 = h.nkk[0]; hnk1 = h.nkk[1];
         hb0 = h.best[0]; hb1 = h.best[1];
     }
+    KB_STAMP(ctl, 28);
     dedup_clear(T);
     if (tid < 2) { s_nd[tid] = 0; s_li[tid] = -1; s_kfail[tid] = 0; }
     __syncthreads();                               // the control block copy
@@ -1328,9 +1331,11 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
                         // upper bound (ub > g: no surviving best keys, e.g. 4096 brokers with
                         // tiny weights), tighten it to the minima g just found and re-run
                         // this step's scan (the state is untouched; the next enqueued pair
-                        // scans again); with ub already at g it is a capacity error
+                        // scans again); with ub already at g the host grows the spill buffer
+                        // and the step runs again (rank summaries: a capacity error)
                         const bool loose = a.use_spill && (C.ub[1] > s_g[1] || (a.allow_leader && C.ub[0] > s_g[0]));
                         if (loose) s_retry = 1;
+                        else if (a.use_spill) s_retry = 2;
                         else { D.status = -1; D.step = step; D.err = E_CONT_OVERFLOW; s_done = 1; }
                     }
                 }
@@ -1460,7 +1465,11 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
         KB_STAMP(ctl, 4);
 
         if (s_retry) {
-            if (tid == 0) {
+            if (tid == 0 && s_retry == 2) {
+                C.halted = H_NEED_SPILL;                // the host grows the spill buffer
+                C.ncont = 0;
+                C.cont_overflow = 0;
+            } else if (tid == 0) {
                 if (C.ub[0] == -HUGE_VAL || C.ub[1] == -HUGE_VAL) {
                     // the scan pruned every wave: its minima are not the step's; open the
                     // bound (the host's bound pass, or a full census, closes it)
@@ -1684,6 +1693,10 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
     // ================================================================== prep
     // (next step): getBL's (load, id) order, bl_move, relative loads, eps, sets
     const bool full = C.full_prep != 0;
+#if KB_ABL & 2
+    // diagnostic timing build (tools/ablate.sh): no incremental prep at all
+    if (!full) { if (tid == 0) C.prepped = 1; write_back(); return; }
+#endif
     const int nT = s_nT;
     bool marked = false;                              // sets already marked (fused path)
     if (!full && a.sb_lds) {
@@ -2104,7 +2117,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
         ub0 = wave_min(in ? s_ubw[0][lane] : HUGE_VAL);
         ub1 = wave_min(in ? s_ubw[1][lane] : HUGE_VAL);
 #ifdef KB_STAMPS
-        if (lane == 0) { const unsigned long long _t = wall_clock64(); _kb_st[18] += _t - _kb_t0; _kb_t0 = _t; }
+        if (lane == 0) KB_STAMP(ctl, 18);
 #endif
       if (lane == 0) {
         const double u = DBL_EPSILON / 2;
@@ -2174,7 +2187,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
     }
     __syncthreads();
     KB_STAMP(ctl, 16);
-    {
+    if (!(KB_ABL & 1) || full) {     // (KB_ABL & 1: diagnostic timing build without the rebuild)
         // marked sets in chunks of the compact list (allowed-set words resident in LDS,
         // or staged per chunk: one round trip); each wave rebuilds four records at a
         // time so their LDS chains overlap

@@ -61,7 +61,7 @@ class kb_stats(C.Structure):
                 ("exact_folds", C.c_int64), ("scan_bytes", C.c_int64), ("device_ms", C.c_double),
                 ("n_brokers", C.c_int64), ("n_sets", C.c_int64), ("integral", C.c_int32),
                 ("max_replicas", C.c_int32), ("refreshes", C.c_int64), ("exact_halts", C.c_int64),
-                ("scan_workgroups", C.c_int64), ("retries", C.c_int64)]
+                ("scan_workgroups", C.c_int64), ("retries", C.c_int64), ("spill_grows", C.c_int64)]
 
 
 _lib = None

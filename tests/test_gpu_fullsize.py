@@ -163,3 +163,22 @@ def test_c5_full_size():
     assert st["n_brokers"] == 4096
     check_loads(eng, cl, ch)
     eng.close()
+
+
+@pytest.mark.gpu
+def test_uniform_4096_full_size():
+    """The exact-tie worst case at the widest broker table: 1M partitions x 4096 brokers,
+    uniform weights (FillDefaults -> 1.0), RF3, -min-unbalance 0.  No capacity error
+    (an overflowing near-tie census grows the spill buffer), each step improving,
+    loads bitwise equal to the replayed plan's getBrokerLoad."""
+    cl = synth.make_cluster(1_000_000, 4096, 3, "uniform", seed=0x5EED4096)
+    cfg = {"allow_leader": False, "rebalance_leaders": False, "min_replicas": 2,
+           "min_unbalance": 0.0, "brokers": None}
+    eng = E.Engine(cl, cfg)
+    ch, err = eng.plan(20)
+    assert err is None, err
+    assert len(ch) == 20
+    assert all(c["step"] == "MoveNonLeaders" for c in ch)
+    check_moves(ch)
+    check_loads(eng, cl, ch)
+    eng.close()

@@ -151,6 +151,32 @@ def test_c2_full_plan():
     assert len(ech) == 100
 
 
+def test_spill_growth_matches_oracle(monkeypatch):
+    """Exact ties overflowing the near-tie spill buffer (a 4-candidate buffer here,
+    KB_CONT_CAP): the host grows it and the step runs again -- same plan as the oracle,
+    no capacity error."""
+    monkeypatch.setenv("KB_CONT_CAP", "4")
+    # three groups of 20 brokers in rings of RF2 partitions (leader 2, follower 1 with
+    # unit weights): every heavy broker carries 12, every light one 6, the rest 9, so
+    # all 400 (heavy, light) moves tie and the census collects far more keys than a
+    # scan workgroup record holds
+    parts = []
+    for g, rings in ((0, 4), (20, 2), (40, 3)):
+        for r in range(rings):
+            for i in range(20):
+                parts.append({"topic": "t%d" % g, "partition": len(parts),
+                              "replicas": [1 + g + i, 1 + g + (i + 1 + r) % 20]})
+    pl = {"version": 1, "partitions": parts}
+    cfg = default_cfg(min_unbalance=0.0)
+    eng = E.Engine(pl, cfg)
+    ech, eerr = eng.plan(25)
+    och, oerr, opl = oracle_plan(pl, cfg, 25)
+    assert_same_plan(ech, eerr, och, oerr)
+    assert eng.state() == opl.state()
+    assert eng.stats()["spill_grows"] >= 1
+    eng.close()
+
+
 @pytest.mark.parametrize("variant", ["c3", "c4"])
 def test_scaled_configs(variant):
     if variant == "c3":
