@@ -142,6 +142,9 @@ def main():
     ap.add_argument("--scaling", default=None, choices=[None, "weak", "strong"],
                     help="multi-GPU: weak (every rank adds a full cluster) or strong (one cluster "
                          "sharded N ways; default for c5)")
+    ap.add_argument("--mode", default="full", choices=["full", "incremental"],
+                    help="incremental: SURVEY 8(f3) rescoring mode (scans read only the blocks a "
+                         "lower-bound certificate keeps); a separate line, not the full-scan roofline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--stamps", action="store_true",
@@ -162,7 +165,8 @@ def main():
     from kafkabalancer_amd import synth
     torch.cuda.set_device(0)
     cl, cfg, desc = synth.config(args.workload, scale=args.scale)
-    eng = E.Engine(cl, cfg, device=0, time_kernels=False)
+    incr = args.mode == "incremental"
+    eng = E.Engine(cl, cfg, device=0, time_kernels=False, incremental=incr)
     if args.warmup:
         _, err = eng.plan(args.warmup)
         assert err is None, err
@@ -183,14 +187,23 @@ def main():
     # headline timing above
     eng.set_timing(True)
     kt_steps = min(args.steps, 200)
+    stk0 = eng.stats()
     _, err = eng.plan(kt_steps)
     assert err is None, err
+    stk1 = eng.stats()
     tk = eng.timings()
     scan_ms, scan_n = tk["scan"]
     scan_clock_us = 1e3 * scan_ms / max(scan_n, 1)
     eng.set_timing(False)
     scan_iso_us = eng.bench_scan(200)
     bytes_scan = st1["scan_bytes"]
+    if incr:
+        # bytes the incremental scans actually read: their blocks' partition words
+        # (+ the 16-B block descriptors), per scan launch of the timing stretch
+        per_part = bytes_scan / max(cl.n, 1)
+        nscans = max(scan_n, 1)
+        blk = stk1["blocks_scanned"] - stk0["blocks_scanned"]
+        bytes_scan = blk * 128 * per_part / nscans + 16 * blk / nscans
     achieved = bytes_scan / (scan_clock_us * 1e-6) / 1e9
     rmax = st1["max_replicas"]
     b8d = bytes_8d(cl, changes, st1["n_sets"], st1["n_brokers"], rmax, steps)
@@ -212,11 +225,15 @@ def main():
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (numpy PCG64 seed 0x5EED000%s), %s" % (args.workload[-1], weights),
-        "config": dict(desc, parallelism="single-gpu", device_ms_per_step=1e3 * dev_s / max(steps, 1)),
+        "config": dict(desc, parallelism="single-gpu", device_ms_per_step=1e3 * dev_s / max(steps, 1),
+                       mode=args.mode),
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(args.workload, "k_scan"),
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None if incr else pmc_traffic(args.workload, "k_scan"),
                      "kernel": "k_scan", "bytes_per_launch": bytes_scan,
-                     "bytes_per_launch_def": "engine layout: per partition 8 w + 4 meta + 2*%d rep" % rmax,
+                     "bytes_per_launch_def": ("engine layout: per partition 8 w + 4 meta + 2*%d rep" % rmax) +
+                                             (" x the blocks the incremental scans read (+16 B per block "
+                                              "descriptor); the full scan reads %d" % st1["scan_bytes"]
+                                              if incr else ""),
                      "avg_launch_us": scan_clock_us,
                      "timing": "in-plan device clock (earliest scan workgroup start .. latest end), "
                                "%d steps" % scan_n,
@@ -231,6 +248,8 @@ def main():
                                            + (" (early-exit stages counted to their hit: ms_per_step is "
                                               "the headline, GB/s informational)" if early_exit else "")}},
         "kernels_us_per_step": {k: 1e3 * v[0] / max(v[1], 1) for k, v in tk.items()},
+        "incremental": ({"blocks_per_scan": (stk1["blocks_scanned"] - stk0["blocks_scanned"]) / max(scan_n, 1),
+                         "blocks_total": (cl.n + 127) // 128} if incr else None),
         "kernel_timing_steps": kt_steps,
         "engine_events": {k: st1[k] - st0[k] for k in ("retries", "refreshes", "exact_halts", "exact_folds")},
     }

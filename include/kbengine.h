@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define KB_ABI_VERSION 5
+#define KB_ABI_VERSION 6
 
 /* step indices == position in the reference's steps table (balancer.go:34-44) */
 enum kb_step {
@@ -137,6 +137,8 @@ typedef struct {
                                        step minimum after a near-tie spill overflow (ABI 3) */
     int64_t spill_grows;            /* near-tie spill buffer growths (exact ties over many
                                        brokers; the step ran again, ABI 5) */
+    int64_t blocks_scanned;         /* incremental mode: 128-partition blocks the scans read
+                                       (kb_engine_set_incremental, ABI 6) */
 } kb_stats;
 
 typedef struct kb_engine kb_engine;
@@ -179,6 +181,14 @@ int kb_engine_timings(kb_engine *e, double *ms, int64_t *launches, int n);
 
 /* Turn the per-kernel events on or off for the following plans (resets the sums). */
 int kb_engine_set_timing(kb_engine *e, int32_t on);
+
+/* Incremental rescoring mode (single GPU, off by default): after a
+ * move() step (MoveLeaders / MoveNonLeaders, steps.go:145-232) the next scan reads only
+ * the partition blocks a lower-bound certificate cannot exclude from the step's
+ * near-tie window, and reuses the last full scan's candidate counts.  Results are
+ * identical to the full scan (same changes, same loads); only the bytes read differ
+ * (kb_stats.blocks_scanned).  Returns KB_OK. */
+int kb_engine_set_incremental(kb_engine *e, int32_t on);
 
 /* Diagnostic: accumulated in-kernel phase stamps (100 MHz ticks) of k_step
  * phases and scan event counts (up to 32 slots, returns the slot count);

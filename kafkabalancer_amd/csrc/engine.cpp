@@ -103,6 +103,9 @@ struct kb_engine {
     int64_t klaunch[TK_N] = {0, 0, 0};
     int64_t refreshes = 0;
     int dbg_scan = 0;
+    int incr = 0;                  // incremental mode (kb_engine_set_incremental)
+    BlockDesc* bdesc = nullptr;    // partition blocks of the shard by wmax descending
+    int64_t nblk = 0;
     bool ub_mode = false;          // a step re-scanned: enqueue the conditional bound pass per scan
     uint32_t list_slack = 1024;        // free entries per broker list (doubled on every re-layout)
     int64_t relists = 0;
@@ -365,6 +368,17 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
         for (int k = 0; k < len[i]; k++) hr[(size_t)k * e->Ppad + i] = dense[c->replica_off[i] - c->replica_off[0] + k];
         hnc[i] = (int32_t)ncon[i];
     }
+    // incremental mode: the shard's 128-partition blocks, heaviest largest weight first
+    std::vector<BlockDesc> hbd;
+    for (int64_t b0 = e->shard_begin; b0 < e->shard_end; b0 += BLK) {
+        BlockDesc d;
+        d.blk = b0 / BLK;
+        d.wmax = 0.0;
+        for (int64_t i = b0; i < std::min<int64_t>(b0 + BLK, e->shard_end); i++) d.wmax = std::max(d.wmax, wt[i]);
+        hbd.push_back(d);
+    }
+    std::stable_sort(hbd.begin(), hbd.end(), [](const BlockDesc& x, const BlockDesc& y) { return x.wmax > y.wmax; });
+    e->nblk = (int64_t)hbd.size();
     std::vector<uint64_t> hsb((size_t)e->nsets * e->W64, 0);
     for (int64_t s = 0; s < e->nsets; s++)
         for (int b : sets[s]) hsb[(size_t)s * e->W64 + (b >> 6)] |= 1ull << (b & 63);
@@ -476,6 +490,8 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
     if (const char* v = getenv("KB_CONT_CAP")) e->cont_cap = (uint32_t)std::max(1, atoi(v));   // tests: growth path
     HIPCHK(dalloc(&e->cont, e->cont_cap));
     HIPCHK(dalloc(&e->ctl, 1));
+    HIPCHK(dalloc(&e->bdesc, std::max<size_t>(hbd.size(), 1)));
+    if (!hbd.empty()) HIPCHK(hipMemcpy(e->bdesc, hbd.data(), hbd.size() * sizeof(BlockDesc), hipMemcpyHostToDevice));
     e->logcap = 1024;
     HIPCHK(dalloc(&e->log, e->logcap));
     HIPCHK(hipHostMalloc((void**)&e->h_ctl, sizeof(DevCtl), hipHostMallocDefault));
@@ -538,6 +554,7 @@ static void fill_scan_args(kb_engine* e, ScanArgs& s) {
     s.dbg = e->dbg_scan;
     s.ubpass = 0;
     s.L = e->L;
+    s.incr = e->incr; s.nblk = (int)e->nblk; s.bdesc = e->bdesc;
 }
 
 static void fill_step_args(kb_engine* e, StepArgs& a, const Recs& R, int use_spill) {
@@ -555,6 +572,7 @@ static void fill_step_args(kb_engine* e, StepArgs& a, const Recs& R, int use_spi
     a.integral = e->integral ? 1 : 0; a.exact_unb = e->exact_unb;
     a.minrep = e->minrep; a.min_unbalance = e->min_unb; a.wmax = e->wmax;
     a.log = e->log; a.L = e->L;
+    a.incr = e->incr && use_spill;
 }
 
 static const int kStepBatch = 64;
@@ -976,6 +994,23 @@ extern "C" int kb_engine_stats(kb_engine* e, kb_stats* o) {
     o->scan_workgroups = e->nscan;
     o->retries = (int64_t)c.total_retries;
     o->spill_grows = e->spill_grows;
+    o->blocks_scanned = (int64_t)c.total_blocks;
+    return KB_OK;
+}
+
+// incremental mode: see include/kbengine.h.  Switching (either way)
+// clears the device's permission flag, so the next scan is a full one and refreshes
+// the cached candidate counts.
+extern "C" int kb_engine_set_incremental(kb_engine* e, int32_t on) {
+    if (!e) return KB_ERR_INVALID;
+    HIPCHK(hipStreamSynchronize(e->st));
+    e->incr = on && e->lds_sets ? 1 : 0;           // (set records in LDS: the incremental scan kernel)
+    DevCtl c;
+    HIPCHK(hipMemcpy(&c, e->ctl, sizeof c, hipMemcpyDeviceToHost));
+    c.incr_ok = 0;
+    c.wskip = 0.0;
+    HIPCHK(hipMemcpy(e->ctl, &c, sizeof c, hipMemcpyHostToDevice));
+    *e->h_ctl = c;
     return KB_OK;
 }
 
@@ -1039,6 +1074,8 @@ extern "C" int kb_engine_bench_scan(kb_engine* e, int iters, double* avg_us) {
     HIPCHK(hipEventCreate(&a));
     HIPCHK(hipEventCreate(&b));
     if (e->ub_mode) enqueue_ubinit(e);                // an open census bound: close it first
+    const int incr = e->incr;
+    e->incr = 0;                                      // (always the full scan)
     enqueue_scan(e);                                  // warm
     // KB_PROBE_INTERLEAVE (diagnostic): 1 = an empty one-workgroup kernel between the
     // scans, 2 = one that rewrites the scan's tables (as k_step does); each scan is
@@ -1075,6 +1112,7 @@ extern "C" int kb_engine_bench_scan(kb_engine* e, int iters, double* avg_us) {
     *avg_us = 1e3 * ms / iters;
     hipEventDestroy(a);
     hipEventDestroy(b);
+    e->incr = incr;
     // forget the spills of the repeated scans
     HIPCHK(hipMemsetAsync(&e->ctl->ncont, 0, 8, e->st));
     HIPCHK(hipStreamSynchronize(e->st));
@@ -1091,7 +1129,7 @@ extern "C" void kb_engine_destroy(kb_engine* e) {
     if (!e) return;
     void* ptrs[] = {e->w, e->rep, e->meta, e->nc, e->load, e->lerr, e->eb, e->bfl, e->cnt,
                     e->setbits, e->setrec, e->order, e->posu, e->blm, e->posm, e->r,
-                    e->bset_off, e->bset_ids, e->recs, e->cont, e->ctl, e->log,
+                    e->bset_off, e->bset_ids, e->recs, e->cont, e->ctl, e->log, e->bdesc,
                     e->L.lstart, e->L.llen, e->L.lcap, e->L.lent};
     for (void* p : ptrs) if (p) hipFree(p);
     if (e->h_ctl) hipHostFree(e->h_ctl);

@@ -27,6 +27,14 @@ constexpr int SUMMARY_KEYS = 1024;  // near-tie keys carried per rank in a summa
 constexpr int DEDUP_STEP = 2048;    // LDS key table of k_step / k_summary
 constexpr int DEDUP_SCAN = 256;     // LDS key table of one k_scan workgroup
 constexpr int TMAX = 2 * MAXR + 4;  // brokers touched by one applied change (bound)
+constexpr int BLK = 128;            // partitions of one wave in a scan tile = one block of
+                                    // the incremental mode (64 lanes x PER_LANE)
+
+// incremental mode: one descriptor per partition block, sorted by wmax descending
+struct BlockDesc {
+    double wmax;                    // largest weight in the block (after FillDefaults)
+    long long blk;                  // block index: partitions [blk * BLK, blk * BLK + BLK)
+};
 constexpr int LDS_SETS_MAX = 65536; // set records staged in LDS when they fit in this
 
 // first-index predicates reduced by the scan (min over partition index)
@@ -167,6 +175,14 @@ struct DevCtl {
     // counts, {k_scan, k_step}; k_step folds in the scan's interval below
     unsigned long long tk_sum[2], tk_n[2];
     int32_t tk_on, tk_pad;
+    // incremental mode (kb_engine_set_incremental): incr_ok = the next scan
+    // may skip every partition block whose largest weight is below wskip (a lower-bound
+    // certificate, see k_step); cand_cache = the candidate counts of the last full scan,
+    // which move() steps leave unchanged
+    int32_t incr_ok, incr_pad;
+    double wskip;
+    unsigned long long cand_cache[2];
+    unsigned long long total_blocks;    // partition blocks the incremental scans read
     // diagnostic phase stamps (builds with -DKB_STAMPS): accumulated
     // shader-clock ticks (clock64) per phase of k_step; [24]/[25] the wall-clock
     // (100 MHz) and shader-clock length of k_step; [26] one stamp's own cost

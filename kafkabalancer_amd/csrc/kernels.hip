@@ -440,15 +440,17 @@ struct ScanParams {
     int heavy, nblm;
     int tk_on;
     int ubpass;                     // census-free round whose minima close an open bound
+    int incr;                       // incremental round: only the blocks with wmax >= wskip
+    double wskip;
 };
 
 // One scan round of a workgroup over its tiles (its first tile already loaded into
 // A): stage the tables, score, write the workgroup record.
-template <int RC, bool LSETS>
+template <int RC, bool LSETS, bool INCR>
 __device__ __forceinline__ void scan_round(const ScanArgs& a, const ScanParams& q, unsigned char* smem,
                                            PartRaw<RC>& A,
                                            unsigned long long t_in,
-                                           int wg) {
+                                           int wg, long long c0_in) {
     DevCtl* ctl = a.ctl;
     constexpr int U = sr_units(RC);
     constexpr int NW = SCAN_THREADS / 64;
@@ -700,23 +702,47 @@ __device__ __forceinline__ void scan_round(const ScanArgs& a, const ScanParams& 
         wgN = tN < wgN ? tN : wgN;
     };
 
-    // ping-pong between two register sets: A (this workgroup's first tile, issued by
-    // the caller before the tables) and Bq; while one tile is scored, the next one's
-    // loads are in flight.  (Issuing the second tile before the tables as well was
-    // measured slower: 10.6 vs 10.2 us per c3 scan.)
-    const long long lane_off = a.shard_begin + (long long)tid * PER_LANE;
+    // ping-pong between two register sets: A and Bq; while one unit is scored, the next
+    // one's loads are in flight.  A unit is one wave's 128 partitions: of this
+    // workgroup's tiles (full round: A was issued by the caller before the tables;
+    // issuing the second tile early as well was measured slower, 10.6 vs 10.2 us per c3
+    // scan), or of the blocks an incremental round reads: the blocks in
+    // descending wmax order, dealt wave-major across the workgroups (the few heavy
+    // blocks land in different workgroups, whose near-tie tables they would otherwise
+    // crowd); a block lighter than wskip holds no candidate within the census window
+    // (k_step's certificate), and every later block is lighter still.
+    // (the unit bases are wave-uniform: scalar registers; the lane adds its offset)
+    const int widu = __builtin_amdgcn_readfirstlane(wid);
+    const long long lofs = (long long)lane * PER_LANE;
+    const long long i0 = (long long)widu * a.nscan + wg, istep = (long long)a.nscan * NW;
+    auto unit = [&](long long k) -> long long {     // base of this wave's k-th unit, or -1
+        if (!INCR || !q.incr) {
+            const long long t = (long long)tile + k * a.nscan;
+            return t < a.ntiles ? a.shard_begin + t * TILE + (long long)widu * BLK : -1;
+        }
+        const long long i = i0 + k * istep;
+        if (i >= a.nblk) return -1;
+        const BlockDesc d = ldobj(a.bdesc + i);
+        return d.wmax >= q.wskip ? d.blk * BLK : -1;
+    };
     PartRaw<RC> Bq;
-    // (the prefetch is unconditional -- a last tile re-loads itself -- so that the
-    // compiler waits for exactly the older tile's loads: vmcnt(N), not vmcnt(0))
-    for (; tile < a.ntiles; tile += 2 * a.nscan) {
-        const int t1 = tile + a.nscan;
-        load_parts<RC>(a, lane_off + (long long)(t1 < a.ntiles ? t1 : tile) * TILE, Bq);
-        score(A, lane_off + (long long)tile * TILE);
-        if (t1 >= a.ntiles) break;
-        const int t2 = t1 + a.nscan;
-        load_parts<RC>(a, lane_off + (long long)(t2 < a.ntiles ? t2 : t1) * TILE, A);
-        score(Bq, lane_off + (long long)t1 * TILE);
+    // (an incremental round's first unit and its loads were issued by the caller)
+    long long c0 = INCR && q.incr ? c0_in : unit(0), nu = 0;
+    // (the prefetch is unconditional -- a last unit re-loads itself -- so that the
+    // compiler waits for exactly the older unit's loads: vmcnt(N), not vmcnt(0))
+    for (long long k = 0; c0 >= 0; k += 2) {
+        const long long c1 = unit(k + 1);
+        load_parts<RC>(a, (c1 >= 0 ? c1 : c0) + lofs, Bq);
+        score(A, c0 + lofs);
+        nu++;
+        if (c1 < 0) break;
+        const long long c2 = unit(k + 2);
+        load_parts<RC>(a, (c2 >= 0 ? c2 : c1) + lofs, A);
+        score(Bq, c1 + lofs);
+        nu++;
+        c0 = c2;
     }
+    if (INCR && q.incr && lane == 0 && nu) atomicAdd(&ctl->total_blocks, (unsigned long long)nu);
     // workgroup record: counts, first-index predicates, minima, near-tie keys
     cL = wave_sum(cL);
     cN = wave_sum(cN);
@@ -806,7 +832,7 @@ __device__ __forceinline__ void scan_round(const ScanArgs& a, const ScanParams& 
     }
 }
 
-template <int RC, bool LSETS>
+template <int RC, bool LSETS, bool INCR>
 __global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
     extern __shared__ __align__(16) unsigned char smem[];
     __shared__ int s_li;
@@ -821,9 +847,17 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
     }
     // every load that does not depend on the control block goes out first: the
     // first tile's stream, then the lookup tables (one memory round trip)
+    // (incremental mode: the control block decides first whether the tiles are read)
     PartRaw<RC> A;
-    if ((int)blockIdx.x < a.ntiles)
-        load_parts<RC>(a, a.shard_begin + (long long)blockIdx.x * TILE + (long long)threadIdx.x * PER_LANE, A);
+    const long long a0 = a.shard_begin + (long long)blockIdx.x * TILE + (long long)threadIdx.x * PER_LANE;
+    if (!INCR && (int)blockIdx.x < a.ntiles) load_parts<RC>(a, a0, A);
+    // incremental kernel: this wave's first block descriptor goes out with the control
+    // block; the block's partition words follow as soon as both are in (two round trips
+    // before the first score, none of them behind the table staging)
+    BlockDesc d0;
+    d0.wmax = -1.0; d0.blk = 0;
+    const long long i0 = (long long)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) * a.nscan + blockIdx.x;
+    if (INCR && i0 < a.nblk) d0 = ldobj(a.bdesc + i0);
     ScanParams q;
     q.run = ctl->halted == H_RUN && ctl->prepped && ctl->steps < ctl->budget;
     q.inv_avg = ctl->inv_avg; q.eps = ctl->eps;
@@ -831,7 +865,15 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
     q.heavy = ctl->heavy; q.nblm = ctl->nblm;
     q.tk_on = ctl->tk_on;
     q.ubpass = 0;
-    scan_round<RC, LSETS>(a, q, smem, A, t_in, (int)blockIdx.x);
+    q.incr = INCR && ctl->incr_ok;
+    q.wskip = INCR ? ctl->wskip : 0.0;
+    long long c0 = -1;
+    if (INCR && !q.incr && (int)blockIdx.x < a.ntiles) load_parts<RC>(a, a0, A);
+    if (INCR && q.incr && d0.wmax >= q.wskip) {
+        c0 = d0.blk * BLK;
+        load_parts<RC>(a, c0 + (long long)(threadIdx.x & 63) * PER_LANE, A);
+    }
+    scan_round<RC, LSETS, INCR>(a, q, smem, A, t_in, (int)blockIdx.x, c0);
 }
 
 // --------------------------------------------------------------- k_step
@@ -883,6 +925,39 @@ __device__ void for_each_contender(const StepArgs& a, const double* s_ld, uint32
             if (cont_delta_ld(s_ld, c, inv_avg) <= g + 4.0 * eps) f(c);
         }
     }
+}
+
+// Incremental mode: the certificate that lets the next scan skip whole
+// partition blocks.  Every candidate of a partition with weight w scores at least
+// LB(w / avg) (scan_round's lower-bound prune, over the range [rlo, rhi] of r[]), and LB
+// is convex with LB(0) = 0.  Find dl > 0 with LB(dl) > thr (thr = the census window
+// ub + 16 eps, the same bound the per-partition prune uses) and LB'(dl) < 0 (with a
+// margin for the rounding of the slope): LB then decreases on [0, dl], so every weight
+// w <= dl * avg scores above the window.  Wave 0 tries a 64 x 64 grid of
+// [0, (rhi - rlo) / 2] (the minimum of LB lies below its midpoint) and keeps the
+// largest certified point.  Returns the weight bound (blocks with wmax below it need no
+// scan), 0 when nothing can be skipped; fl(wskip / avg) <= dl, as the scan computes it.
+__device__ double incr_wskip(double rlo, double rhi, double thr, double avg, double iav, int lane) {
+    if (!(thr < 0.0) || !(rhi > rlo) || !(avg > 0.0) || !(iav > 0.0)) return 0.0;
+    const double fmn = fsq(rlo), fmx = fsq(rhi);
+    auto ok = [&](double dl) {
+        const double lb = (fsq(rhi - dl) - fmx) + (fsq(rlo + dl) - fmn);
+        const double x1 = rhi - dl, x2 = rlo + dl;
+        const double slope = (x2 > 0.0 ? 2.0 * x2 : x2) - (x1 > 0.0 ? 2.0 * x1 : x1);
+        return lb > thr && slope < -1e-14 * (fabs(x1) + fabs(x2));
+    };
+    const double h = 0.5 * (rhi - rlo) / 64.0;
+    const double d1 = h * (double)(lane + 1);
+    unsigned long long bal = __ballot(ok(d1));
+    double best = 0.0;
+    if (bal) best = __shfl(d1, 63 - __clzll(bal));
+    const double d2 = best + (h / 64.0) * (double)(lane + 1);
+    bal = __ballot(ok(d2));
+    if (bal) best = fmax(best, __shfl(d2, 63 - __clzll(bal)));
+    if (!(best > 0.0)) return 0.0;
+    double ws = best * avg;
+    for (int it = 0; it < 16 && ws * iav > best; it++) ws *= 1.0 - 0x1p-50;
+    return ws * iav <= best ? ws : 0.0;
 }
 
 // the control block lives in LDS for the whole k_step (one load round trip at the
@@ -1030,6 +1105,12 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
             c0 = wave_sum(pin ? s_pc[0][lane] : 0ull); c1 = wave_sum(pin ? s_pc[1][lane] : 0ull);
             flg = wave_red_or(pin ? s_pf[NF][lane] : 0u);
             if (lane == 0) {
+                if (a.incr) {
+                    // an incremental scan read only some blocks: the counts are the last
+                    // full scan's (move() steps keep nrep, the in-set replicas and bl_move)
+                    if (C.incr_ok) { c0 = C.cand_cache[0]; c1 = C.cand_cache[1]; }
+                    else { C.cand_cache[0] = c0; C.cand_cache[1] = c1; }
+                }
                 s_g[0] = g0; s_g[1] = g1; s_cand[0] = c0; s_cand[1] = c1;
                 s_flags = flg | (a.use_spill && C.cont_overflow ? 1u : 0u);
                 s_fm = fm;
@@ -1705,7 +1786,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
         // whole prep takes six barriers
         const bool srt = nT > 0;
         constexpr int NQ = (MAXB + STEP_THREADS - 1) / STEP_THREADS;
-        __shared__ double s_fq[2][NW], s_fq2[5][NW];     // F1 / F2 wave partials (distinct: no overwrite race)
+        __shared__ double s_fq[2][NW], s_fq2[7][NW];     // F1 / F2 wave partials (distinct: no overwrite race)
         __shared__ int s_fcnt[NW];
         __shared__ int s_fwc[NW];
         // F1: touched marks; S, E and |bl_move| partials; clears; best keys issued
@@ -1738,7 +1819,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
         const double avg = S / (double)nblm;
         const double iav = 1.0 / avg;
         {
-            double su = 0.0, v = 0.0, rm = 0.0;
+            double su = 0.0, v = 0.0, rm = 0.0, rlo = HUGE_VAL, rhi = -HUGE_VAL;
             for (int b = tid; b < B; b += STEP_THREADS) {
                 double r = 0.0;
                 if (s_fl[b] & (BF_PRESENT | BF_INCFG)) {
@@ -1749,6 +1830,8 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
                     rm = ar > rm ? ar : rm;
                 }
                 stdbl(a.r + b, r);
+                rlo = r < rlo ? r : rlo;                  // the scan's range of r[] (prune bound)
+                rhi = r > rhi ? r : rhi;
             }
             // upper bound of the next step's minimum per kind: the best keys of the scan
             // just resolved whose partition and brokers the applied move did not touch
@@ -1768,7 +1851,11 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
             }
             su = wave_sum(su); v = wave_sum(v); rm = wave_max(rm);
             ub0 = wave_min(ub0); ub1 = wave_min(ub1);
-            if (lane == 0) { s_fq2[0][wid] = su; s_fq2[1][wid] = v; s_fq2[2][wid] = rm; s_fq2[3][wid] = ub0; s_fq2[4][wid] = ub1; }
+            if (a.incr) { rlo = wave_min(rlo); rhi = wave_max(rhi); }
+            if (lane == 0) {
+                s_fq2[0][wid] = su; s_fq2[1][wid] = v; s_fq2[2][wid] = rm; s_fq2[3][wid] = ub0; s_fq2[4][wid] = ub1;
+                s_fq2[5][wid] = rlo; s_fq2[6][wid] = rhi;
+            }
         }
         for (int set = tid; set < a.nsets; set += STEP_THREADS) {
             // a set is marked when it holds a touched broker
@@ -1815,15 +1902,29 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
             const double Rm = wave_max(in ? s_fq2[2][lane] : 0.0);
             const double ub0 = wave_min(in ? s_fq2[3][lane] : HUGE_VAL);
             const double ub1 = wave_min(in ? s_fq2[4][lane] : HUGE_VAL);
+            // (every lane: the incremental certificate below needs eps on the whole wave)
+            const double u = DBL_EPSILON / 2;
+            const double n = (double)nblm;
+            const double R = Rm + a.wmax * iav;
+            const double Ea = E * iav;
+            double epsf = 64.0 * u * ((n + 8.0) * (U0 + 2.0 * V) + 4.0 * (1.0 + R) * (1.0 + R));
+            double epsl = 16.0 * Ea * (V / (n > 0 ? n : 1.0) + R + 1.0) + 4.0 * Ea * Ea;
+            double ep = epsf + epsl;
+            if (!(ep > 1e-300)) ep = 1e-300;
+            // incremental mode: after a move() with bl_move and the first-index predicates
+            // unchanged, the next scan may skip the blocks lighter than wskip
+            double ws = 0.0;
+            const bool inc = a.incr && do_res && D.status == 1 && D.kind == 1 && (D.step == 7 || D.step == 8) &&
+                             nblm == nblm0 && !s_fm && !a.rebalance && !a.sem_go && a.use_spill;
+            if (inc) {
+                const double rlo = wave_min(in ? s_fq2[5][lane] : HUGE_VAL);
+                const double rhi = wave_max(in ? s_fq2[6][lane] : -HUGE_VAL);
+                const double ubP = a.allow_leader ? (ub0 > ub1 ? ub0 : ub1) : ub1;
+                ws = incr_wskip(rlo, rhi, ubP + 16.0 * ep, avg, iav, lane);
+            }
             if (lane == 0) {
-                const double u = DBL_EPSILON / 2;
-                const double n = (double)nblm;
-                const double R = Rm + a.wmax * iav;
-                const double Ea = E * iav;
-                double epsf = 64.0 * u * ((n + 8.0) * (U0 + 2.0 * V) + 4.0 * (1.0 + R) * (1.0 + R));
-                double epsl = 16.0 * Ea * (V / (n > 0 ? n : 1.0) + R + 1.0) + 4.0 * Ea * Ea;
-                double ep = epsf + epsl;
-                if (!(ep > 1e-300)) ep = 1e-300;
+                C.incr_ok = ws > 0.0 ? 1 : 0;
+                C.wskip = ws;
                 C.S = S; C.avg = avg; C.inv_avg = iav; C.U0 = U0;
                 C.V = V; C.eps = ep; C.E = E; C.nblm = nblm;
                 // after a first-index stage (Remove/Add/Disallowed) the next step is most
@@ -2132,6 +2233,8 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
         C.V = V; C.eps = ep; C.E = E; C.nblm = nblm;
         const bool sup = a.use_spill && do_res && !full && D.status == 1 && D.step >= 3 && D.step <= 5;
         C.ub[0] = sup ? -HUGE_VAL : ub0; C.ub[1] = sup ? -HUGE_VAL : ub1;
+        C.incr_ok = 0;                      // (the next scan reads every block)
+        C.wskip = 0.0;
         C.want_refresh = (epsl > epsf || C.ndirty >= 256) ? 1 : 0;
         C.ncont = 0;
         C.cont_overflow = 0;
@@ -2491,8 +2594,10 @@ __global__ __launch_bounds__(1024) void k_summary(SumArgs a) {
 template <int RC>
 static void launch_scan_rc(const ScanArgs& a, bool lds_sets, size_t lds, hipStream_t st) {
     const int grid = a.nscan + (a.listwg ? 1 : 0);
-    if (lds_sets) hipLaunchKernelGGL((k_scan<RC, true>), dim3(grid), dim3(SCAN_THREADS), lds, st, a);
-    else hipLaunchKernelGGL((k_scan<RC, false>), dim3(grid), dim3(SCAN_THREADS), lds, st, a);
+    // (incremental mode: with the set records in LDS only; engine.cpp gates it)
+    if (lds_sets && a.incr) hipLaunchKernelGGL((k_scan<RC, true, true>), dim3(grid), dim3(SCAN_THREADS), lds, st, a);
+    else if (lds_sets) hipLaunchKernelGGL((k_scan<RC, true, false>), dim3(grid), dim3(SCAN_THREADS), lds, st, a);
+    else hipLaunchKernelGGL((k_scan<RC, false, false>), dim3(grid), dim3(SCAN_THREADS), lds, st, a);
 }
 
 void launch_scan(const ScanArgs& a, int rc, bool lds_sets, size_t lds, hipStream_t st) {
@@ -2510,8 +2615,12 @@ void launch_scan(const ScanArgs& a, int rc, bool lds_sets, size_t lds, hipStream
 template <int RC>
 static int scan_occ_rc(bool lds_sets, size_t lds) {
     int n = 0;
-    if (lds_sets) hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_scan<RC, true>, SCAN_THREADS, lds);
-    else hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_scan<RC, false>, SCAN_THREADS, lds);
+    int m = 0;
+    if (lds_sets) {
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_scan<RC, true, false>, SCAN_THREADS, lds);
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&m, k_scan<RC, true, true>, SCAN_THREADS, lds);
+        n = n < m ? n : m;
+    } else hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_scan<RC, false, false>, SCAN_THREADS, lds);
     return n;
 }
 

@@ -39,6 +39,9 @@ struct ScanArgs {
                               //    unless a relevant upper bound is +inf
     int dbg;                  // diagnostic only (KB_DEBUG_SCAN): 1 = skip the census
     Lists L;
+    int incr;                 // incremental mode: block descriptors (DevCtl.incr_ok decides per step)
+    int nblk;
+    const BlockDesc* bdesc;
 };
 
 struct StepArgs {
@@ -74,6 +77,7 @@ struct StepArgs {
     double min_unbalance, wmax;
     ChangeDev* log;
     Lists L;
+    int incr;                 // incremental mode (single GPU): decide DevCtl.incr_ok / wskip
 };
 
 struct RefreshArgs {

@@ -27,7 +27,7 @@ EXPORTS = ["kb_abi_version", "kb_engine_create", "kb_engine_balance", "kb_engine
            "kb_engine_last_error", "kb_engine_destroy", "kb_engine_summary_bytes",
            "kb_engine_step_begin", "kb_engine_step_finish", "kb_engine_set_stream",
            "kb_engine_sharded_reset", "kb_engine_sharded_scan", "kb_engine_sharded_resolve",
-           "kb_engine_sharded_collect"]
+           "kb_engine_sharded_collect", "kb_engine_set_incremental"]
 
 P64 = C.POINTER(C.c_int64)
 PD = C.POINTER(C.c_double)
@@ -61,7 +61,8 @@ class kb_stats(C.Structure):
                 ("exact_folds", C.c_int64), ("scan_bytes", C.c_int64), ("device_ms", C.c_double),
                 ("n_brokers", C.c_int64), ("n_sets", C.c_int64), ("integral", C.c_int32),
                 ("max_replicas", C.c_int32), ("refreshes", C.c_int64), ("exact_halts", C.c_int64),
-                ("scan_workgroups", C.c_int64), ("retries", C.c_int64), ("spill_grows", C.c_int64)]
+                ("scan_workgroups", C.c_int64), ("retries", C.c_int64), ("spill_grows", C.c_int64),
+                ("blocks_scanned", C.c_int64)]
 
 
 _lib = None
@@ -118,7 +119,9 @@ def lib():
         L.kb_engine_sharded_resolve.restype = C.c_int
         L.kb_engine_sharded_collect.argtypes = [vp, C.POINTER(kb_change), C.c_int64, P64]
         L.kb_engine_sharded_collect.restype = C.c_int
-        if L.kb_abi_version() != 5:
+        L.kb_engine_set_incremental.argtypes = [vp, C.c_int32]
+        L.kb_engine_set_incremental.restype = C.c_int
+        if L.kb_abi_version() != 6:
             raise ImportError("libkbengine.so ABI mismatch")
         _lib = L
     return _lib
@@ -217,7 +220,7 @@ class Engine:
     """One device-resident engine over a cluster (kb_engine_*)."""
 
     def __init__(self, cluster, cfg, semantics=KB_SEM_APPLIED, device=0, shard=None, list_slack=0,
-                 exact_unbalance=False, time_kernels=False):
+                 exact_unbalance=False, time_kernels=False, incremental=False):
         L = lib()
         if not isinstance(cluster, ClusterSoA):
             cluster = ClusterSoA.from_plist(cluster)
@@ -252,6 +255,15 @@ class Engine:
             msg = self.last_error() if h.value else "kb_engine_create failed"
             self.close()
             raise EngineError(rc, "%s: %s" % (ERRORS.get(rc, rc), msg))
+        if incremental:
+            self.set_incremental(True)
+
+    def set_incremental(self, on):
+        """Incremental rescoring mode: scans read only the partition blocks
+        a lower-bound certificate cannot exclude; same results as the full scan."""
+        rc = lib().kb_engine_set_incremental(self.h, int(bool(on)))
+        if rc != 0:
+            raise EngineError(rc, self.last_error())
 
     def last_error(self):
         buf = C.create_string_buffer(4096)

@@ -1,0 +1,155 @@
+"""Incremental rescoring mode (kb_engine_set_incremental) on the GPU.
+
+After a move() step the next scan reads only the 128-partition blocks whose largest
+weight clears k_step's lower-bound certificate (incr_wskip in kernels.hip) and reuses
+the last full scan's candidate counts.  The bar is the full scan's: the oracle's
+golden plans bit for bit, the oracle on random cases, and at c3 size the identical
+plan (every field, su / cu bitwise) and candidate count of the full-scan engine.
+"""
+import glob
+import os
+import random
+import sys
+
+import numpy as np
+import pytest
+
+from kafkabalancer_amd import engine as E
+from kafkabalancer_amd import synth
+
+from test_gpu_parity_data import random_plist
+from helpers import assert_same_plan, default_cfg, oracle_plan
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "golden"))
+import gen_scale  # noqa: E402
+from test_golden_scale import FIXTURES, ids, load  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+def _key(changes):
+    return [tuple(sorted(c.items())) for c in changes]
+
+
+@pytest.mark.parametrize("path", FIXTURES, ids=ids)
+def test_incremental_replays_golden_plan(path):
+    """The oracle's large-scale golden plans (tests/golden/scale_*.json)."""
+    g = load(path)
+    cl = gen_scale.build(g["params"])
+    assert gen_scale.input_hash(cl) == g["input_sha256"]
+    eng = E.Engine(cl, dict(g["cfg"]), incremental=True)
+    changes, err = eng.plan(g["steps"])
+    got = [[c["step"], c["pidx"], c["kind"], c["from_"], c["to"], c["slot"]] for c in changes]
+    for i, (a, b) in enumerate(zip(got, g["changes"])):
+        assert a == b, "step %d: engine %s oracle %s" % (i, a, b)
+    assert len(got) == len(g["changes"])
+    assert (err is None) == (g["err"] is None), (err, g["err"])
+    for i, c in enumerate(changes):
+        if c["step"] in ("MoveLeaders", "MoveNonLeaders"):
+            su, cu = g["su"][i], g["cu"][i]
+            scale = max(abs(su), abs(cu), 1e-300)
+            assert abs(c["su"] - su) <= 1e-9 * scale and abs(c["cu"] - cu) <= 1e-9 * scale, i
+    for p, reps in g["final"].items():
+        assert eng.replicas(int(p)) == reps, p
+    eng.close()
+
+
+CASES = []
+for seed in range(16):
+    r = random.Random(500 + seed)
+    CASES.append(dict(seed=seed, P=r.choice([60, 150, 400, 1000]), B=r.choice([4, 6, 10, 25]),
+                      weights=r.choice(["int", "zipf", "zipf"]), sets=r.choice(["none", "some", "all"]),
+                      allow_leader=r.random() < 0.5))
+
+
+@pytest.mark.parametrize("case", CASES, ids=lambda c: "s%d" % c["seed"])
+def test_incremental_random_vs_oracle(case):
+    rng = random.Random(7000 + case["seed"])
+    pl = random_plist(rng, case["P"], case["B"], case["weights"], case["sets"], False, False)
+    cfg = default_cfg(allow_leader=case["allow_leader"], min_unbalance=0.0)
+    eng = E.Engine(pl, cfg, incremental=True)
+    ech, eerr = eng.plan(40)
+    och, oerr, opl = oracle_plan(pl, cfg, 40)
+    assert_same_plan(ech, eerr, och, oerr)
+    if oerr is None:
+        assert eng.state() == opl.state()
+    eng.close()
+
+
+def _both(cl, cfg, steps):
+    full = E.Engine(cl, cfg)
+    fch, ferr = full.plan(steps)
+    fst = full.stats()
+    fld = full.loads()
+    full.close()
+    inc = E.Engine(cl, cfg, incremental=True)
+    ich, ierr = inc.plan(steps)
+    ist = inc.stats()
+    ild = inc.loads()
+    inc.close()
+    return (fch, ferr, fst, fld), (ich, ierr, ist, ild)
+
+
+@pytest.mark.parametrize("variant", ["c3", "c2", "b4096"])
+def test_incremental_equals_full_scan(variant):
+    """Same plan (every field, su / cu bitwise), same loads, same candidate count; and
+    the incremental scans really skip blocks."""
+    if variant == "c3":
+        cl, cfg, _ = synth.config("c3")
+        steps = 120
+    elif variant == "c2":
+        cl, cfg, _ = synth.config("c2")
+        steps = 100
+    else:
+        cl = synth.make_cluster(400000, 4096, 3, "zipf", seed=41)
+        cfg = default_cfg(min_unbalance=0.0)
+        steps = 40
+    (fch, ferr, fst, fld), (ich, ierr, ist, ild) = _both(cl, cfg, steps)
+    assert (ferr is None) == (ierr is None)
+    assert _key(fch) == _key(ich)
+    assert fld == ild
+    assert fst["candidates"] == ist["candidates"] > 0
+    nblk = (cl.n + 127) // 128
+    # (c2: exact ties, little to certify; b4096: no surviving best key bounds the next
+    # minimum after most moves, so the certificate has no window and the scans are full)
+    if variant == "c3":
+        assert 0 < ist["blocks_scanned"] < nblk * steps // 4, (ist["blocks_scanned"], nblk * steps)
+
+
+def test_incremental_switching_mid_plan():
+    """Turning the mode on and off between plans changes nothing."""
+    cl = synth.make_cluster(200000, 500, 3, "zipf", nsets=64, set_size=48, seed=43)
+    cfg = default_cfg(allow_leader=True, min_unbalance=0.0)
+    ref = E.Engine(cl, cfg)
+    want, err = ref.plan(90)
+    assert err is None
+    ref.close()
+    eng = E.Engine(cl, cfg)
+    got = []
+    for on in (False, True, False, True, True, False):
+        eng.set_incremental(on)
+        ch, err = eng.plan(15)
+        assert err is None
+        got += ch
+    assert _key(got) == _key(want)
+    eng.close()
+
+
+def test_incremental_through_first_index_stages():
+    """Remove / Add / Disallowed stages run full scans; move() steps after them go
+    incremental; the plan is the oracle's (scaled c4)."""
+    nr = np.zeros(800, np.int64)
+    nr[[5, 300]] = 2
+    nr[[7, 500]] = 4
+    cl = synth.make_cluster(800, 40, 3, "zipf", seed=12, with_names=True, num_replicas=nr)
+    cfg = default_cfg(min_unbalance=0.0, allow_leader=True, brokers=[b for b in range(1, 46) if b != 40])
+    pl = synth.to_plist(cl)
+    eng = E.Engine(pl, cfg, incremental=True)
+    ech, eerr = eng.plan(120)
+    och, oerr, opl = oracle_plan(pl, cfg, 120)
+    assert_same_plan(ech, eerr, och, oerr)
+    steps = [c["step"] for c in ech]
+    assert "MoveDisallowedReplicas" in steps and steps[-1] in ("MoveLeaders", "MoveNonLeaders")
+    assert eng.state() == opl.state()
+    eng.close()
