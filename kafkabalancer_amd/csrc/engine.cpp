@@ -90,6 +90,10 @@ struct kb_engine {
     ChangeDev* log = nullptr;
     int logcap = 0;
     DevCtl* h_ctl = nullptr;          // pinned
+    bool ctl_mirror = false;          // h_ctl == the device block and the stream is idle
+                                      // (set by run_steps; every other path clears it)
+    ChangeDev* h_log = nullptr;       // pinned copy of the device step log (run_steps)
+    int h_logcap = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     double last_ms = 0;
     int64_t scan_bytes = 0;
@@ -685,6 +689,7 @@ static int relist(kb_engine* e) {
 
 // exact refolds of the approximate loads (k_refresh), then a full prep
 static int refresh(kb_engine* e) {
+    if (e) e->ctl_mirror = false;            // (the device block changes behind the host copy)
     if (e->integral) return KB_OK;
     mark(e, -1);
     launch_listop(e->ctl, e->L, e->st);
@@ -718,8 +723,11 @@ static int refresh(kb_engine* e) {
 }
 
 static int reset_ctl(kb_engine* e, int64_t budget_steps) {
-    HIPCHK(hipMemcpyAsync(e->h_ctl, e->ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, e->st));
-    HIPCHK(hipStreamSynchronize(e->st));
+    if (!e->ctl_mirror) {          // (after a plan, the host copy is current: no round trip)
+        HIPCHK(hipMemcpyAsync(e->h_ctl, e->ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, e->st));
+        HIPCHK(hipStreamSynchronize(e->st));
+    }
+    e->ctl_mirror = false;
     DevCtl c = *e->h_ctl;
     if (c.halted == H_NEED_EXACT) {
         if (refresh(e) != KB_OK) return KB_ERR_HIP;
@@ -731,8 +739,8 @@ static int reset_ctl(kb_engine* e, int64_t budget_steps) {
     c.logcap = e->logcap;
     const long long bud = (long long)c.steps + budget_steps;
     c.budget = bud > 0x7FFFFFFF ? 0x7FFFFFFF : (int32_t)bud;
-    HIPCHK(hipMemcpyAsync(e->ctl, &c, sizeof c, hipMemcpyHostToDevice, e->st));
     *e->h_ctl = c;
+    HIPCHK(hipMemcpyAsync(e->ctl, e->h_ctl, sizeof c, hipMemcpyHostToDevice, e->st));
     return KB_OK;
 }
 
@@ -809,6 +817,7 @@ static int ensure_log(kb_engine* e, int64_t max_steps) {
 // halted step runs again.  Only past kContMax is it a capacity error.
 static const uint32_t kContMax = 1u << 26;   // 64M candidates (2 GiB)
 static int grow_spill(kb_engine* e) {
+    if (e) e->ctl_mirror = false;            // (the device block changes behind the host copy)
     if (e->cont_cap >= kContMax) {
         e->last_err = "engine capacity: more than " + std::to_string(kContMax) + " near-tied candidates in one step";
         return KB_ERR_CAPACITY;
@@ -838,14 +847,23 @@ static int grow_spill(kb_engine* e) {
 // log entries written (changes + the terminating no-change / error)
 static int run_steps(kb_engine* e, int64_t max_steps) {
     if (ensure_log(e, max_steps) != KB_OK) return KB_ERR_HIP;
+    if (e->h_logcap < e->logcap) {
+        if (e->h_log) hipHostFree(e->h_log);
+        e->h_log = nullptr;
+        e->h_logcap = 0;
+        HIPCHK(hipHostMalloc((void**)&e->h_log, (size_t)e->logcap * sizeof(ChangeDev), hipHostMallocDefault));
+        e->h_logcap = e->logcap;
+    }
     if (reset_ctl(e, max_steps) != KB_OK) return KB_ERR_HIP;
     const int steps0 = e->h_ctl->steps;
     bool prepped = e->h_ctl->prepped != 0;
+    bool fresh = false;                 // h_ctl holds the device block after the last batch
     HIPCHK(hipEventRecord(e->ev0, e->st));
     for (;;) {
         const int64_t done = e->h_ctl->steps - steps0;
         if (done >= max_steps) break;
         const int64_t pairs = std::min<int64_t>(kStepBatch, max_steps - done + (prepped ? 0 : 1));
+        const int lp0 = e->h_ctl->logpos;
         for (int64_t s = 0; s < pairs; s++) {
             // pair 0 ran the full prep; once a step had to re-scan (no surviving best
             // keys bound the next minimum), every scan gets the conditional bound pass
@@ -854,8 +872,16 @@ static int run_steps(kb_engine* e, int64_t max_steps) {
         }
         mark(e, -1);
         HIPCHK(hipGetLastError());
+        HIPCHK(hipEventRecord(e->ev1, e->st));
+        // the control block and this batch's log entries (at most one per pair) come
+        // back with one synchronisation
         HIPCHK(hipMemcpyAsync(e->h_ctl, e->ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, e->st));
+        const int64_t ln = std::min<int64_t>(pairs, (int64_t)e->logcap - lp0);
+        if (ln > 0)
+            HIPCHK(hipMemcpyAsync(e->h_log + lp0, e->log + lp0, (size_t)ln * sizeof(ChangeDev),
+                                  hipMemcpyDeviceToHost, e->st));
         HIPCHK(hipStreamSynchronize(e->st));
+        fresh = true;
         harvest(e);
         const DevCtl& c = *e->h_ctl;
         if (c.total_retries > 0) e->ub_mode = true;
@@ -864,24 +890,26 @@ static int run_steps(kb_engine* e, int64_t max_steps) {
             // more near-tied candidates than the spill buffer holds: grow it, run the step again
             const int rc = grow_spill(e);
             if (rc != KB_OK) return rc;
+            fresh = false;
             continue;
         }
         if (c.halted == H_NEED_EXACT || (c.want_refresh && c.steps - steps0 < max_steps)) {
-            const int logpos = c.logpos;
             if (refresh(e) != KB_OK) return KB_ERR_HIP;
-            // refresh() cleared halted; keep the step log position
-            (void)logpos;
+            // refresh() cleared halted; the step log position is kept
             prepped = false;
+            fresh = false;
             continue;
         }
         prepped = c.prepped != 0;
     }
-    HIPCHK(hipEventRecord(e->ev1, e->st));
-    HIPCHK(hipStreamSynchronize(e->st));
     float ms = 0;
     hipEventElapsedTime(&ms, e->ev0, e->ev1);
     e->last_ms += ms;
-    HIPCHK(hipMemcpy(e->h_ctl, e->ctl, sizeof(DevCtl), hipMemcpyDeviceToHost));
+    if (!fresh) {
+        HIPCHK(hipStreamSynchronize(e->st));
+        HIPCHK(hipMemcpy(e->h_ctl, e->ctl, sizeof(DevCtl), hipMemcpyDeviceToHost));
+    }
+    e->ctl_mirror = true;
     return (int)std::min<int64_t>(e->h_ctl->logpos, e->logcap);
 }
 
@@ -892,9 +920,7 @@ extern "C" int kb_engine_balance(kb_engine* e, kb_change* out) {
     const int nlog = run_steps(e, 1);
     if (nlog < 0) return nlog;
     if (nlog == 0) { memset(out, 0, sizeof *out); out->status = KB_NOCHANGE; return KB_NOCHANGE; }
-    ChangeDev d;
-    HIPCHK(hipMemcpy(&d, e->log, sizeof d, hipMemcpyDeviceToHost));
-    return convert(e, d, out);
+    return convert(e, e->h_log[0], out);
 }
 
 extern "C" int kb_engine_plan(kb_engine* e, int64_t max_steps, kb_change* out, int64_t* n_out) {
@@ -909,16 +935,13 @@ extern "C" int kb_engine_plan(kb_engine* e, int64_t max_steps, kb_change* out, i
     // max_steps asks for (the caller's `out` holds max_steps entries)
     int rc = KB_NOCHANGE;
     int64_t k = 0;
-    std::vector<ChangeDev> logv;
     while (k < max_steps) {
         const int64_t m = std::min<int64_t>(max_steps - k, kLogChunk);
         const int nlog = run_steps(e, m);
         if (nlog < 0) { *n_out = k; return nlog; }
-        logv.resize((size_t)nlog);
-        if (nlog) HIPCHK(hipMemcpy(logv.data(), e->log, (size_t)nlog * sizeof(ChangeDev), hipMemcpyDeviceToHost));
-        for (int64_t i = 0; i < nlog; i++) {
+        for (int64_t i = 0; i < nlog; i++) {         // (run_steps copied the log entries)
             kb_change tmp;
-            rc = convert(e, logv[i], out ? &out[k] : &tmp);
+            rc = convert(e, e->h_log[i], out ? &out[k] : &tmp);
             k++;
             if (rc != KB_CHANGE) { *n_out = k; return rc; }
         }
@@ -955,6 +978,7 @@ extern "C" int64_t kb_engine_loads(kb_engine* e, int64_t* ids, double* loads, in
 }
 
 extern "C" double kb_engine_unbalance(kb_engine* e) {
+    if (e) e->ctl_mirror = false;            // (the device block changes behind the host copy)
     if (!e || e->B == 0) return 0.0;
     if (make_exact(e) != KB_OK) return NAN;
     std::vector<double> ld(e->B);
@@ -1002,6 +1026,7 @@ extern "C" int kb_engine_stats(kb_engine* e, kb_stats* o) {
 // clears the device's permission flag, so the next scan is a full one and refreshes
 // the cached candidate counts.
 extern "C" int kb_engine_set_incremental(kb_engine* e, int32_t on) {
+    if (e) e->ctl_mirror = false;            // (the device block changes behind the host copy)
     if (!e) return KB_ERR_INVALID;
     HIPCHK(hipStreamSynchronize(e->st));
     e->incr = on && e->lds_sets ? 1 : 0;           // (set records in LDS: the incremental scan kernel)
@@ -1036,6 +1061,7 @@ extern "C" int kb_engine_timings(kb_engine* e, double* ms, int64_t* launches, in
 }
 
 extern "C" int kb_engine_set_timing(kb_engine* e, int32_t on) {
+    if (e) e->ctl_mirror = false;            // (the device block changes behind the host copy)
     if (!e) return KB_ERR_INVALID;
     HIPCHK(hipStreamSynchronize(e->st));
     e->tev_used = 0;
@@ -1063,6 +1089,7 @@ extern "C" int kb_engine_stamps(kb_engine* e, uint64_t* out, int n) {
 // Diagnostic: average device time of k_scan over `iters` back-to-back launches on
 // the current prepped state (the scan only writes its records and spill buffer).
 extern "C" int kb_engine_bench_scan(kb_engine* e, int iters, double* avg_us) {
+    if (e) e->ctl_mirror = false;            // (the device block changes behind the host copy)
     if (!e || iters < 1 || !avg_us) return KB_ERR_INVALID;
     if (e->pending) return e->pending;
     if (reset_ctl(e, 1) != KB_OK) return KB_ERR_HIP;
@@ -1133,6 +1160,7 @@ extern "C" void kb_engine_destroy(kb_engine* e) {
                     e->L.lstart, e->L.llen, e->L.lcap, e->L.lent};
     for (void* p : ptrs) if (p) hipFree(p);
     if (e->h_ctl) hipHostFree(e->h_ctl);
+    if (e->h_log) hipHostFree(e->h_log);
     if (e->ev0) hipEventDestroy(e->ev0);
     if (e->ev1) hipEventDestroy(e->ev1);
     for (auto v : e->tev) hipEventDestroy(v);
@@ -1145,6 +1173,7 @@ extern "C" void kb_engine_destroy(kb_engine* e) {
 extern "C" int64_t kb_engine_summary_bytes(kb_engine* e) { (void)e; return (int64_t)SUMMARY_BYTES; }
 
 extern "C" int kb_engine_set_stream(kb_engine* e, void* s) {
+    if (e) e->ctl_mirror = false;            // (the device block changes behind the host copy)
     if (!e) return KB_ERR_INVALID;
     if (e->own_st && e->st) hipStreamDestroy(e->st);
     e->st = (hipStream_t)s;
@@ -1153,6 +1182,7 @@ extern "C" int kb_engine_set_stream(kb_engine* e, void* s) {
 }
 
 extern "C" int kb_engine_step_begin(kb_engine* e, void* summary_dev) {
+    if (e) e->ctl_mirror = false;            // (the device block changes behind the host copy)
     if (!e || !summary_dev) return KB_ERR_INVALID;
     if (e->pending) return e->pending;
     if (reset_ctl(e, 1) != KB_OK) return KB_ERR_HIP;
@@ -1169,6 +1199,7 @@ extern "C" int kb_engine_step_begin(kb_engine* e, void* summary_dev) {
 // ---- batched multi-GPU steps: the host enqueues several (scan, summary, all-gather,
 // resolve) rounds without a host round trip; a halted step turns the rest into no-ops
 extern "C" int kb_engine_sharded_reset(kb_engine* e, int64_t budget_steps) {
+    if (e) e->ctl_mirror = false;            // (the device block changes behind the host copy)
     if (!e || budget_steps < 1) return KB_ERR_INVALID;
     if (e->pending) return e->pending;
     if (reset_ctl(e, budget_steps) != KB_OK) return KB_ERR_HIP;
@@ -1178,6 +1209,7 @@ extern "C" int kb_engine_sharded_reset(kb_engine* e, int64_t budget_steps) {
 }
 
 extern "C" int kb_engine_sharded_scan(kb_engine* e, void* summary_dev) {
+    if (e) e->ctl_mirror = false;            // (the device block changes behind the host copy)
     if (!e || !summary_dev) return KB_ERR_INVALID;
     enqueue_scan(e);
     SumArgs s;
@@ -1189,6 +1221,7 @@ extern "C" int kb_engine_sharded_scan(kb_engine* e, void* summary_dev) {
 }
 
 extern "C" int kb_engine_sharded_resolve(kb_engine* e, const void* gathered_dev, int32_t n_ranks) {
+    if (e) e->ctl_mirror = false;            // (the device block changes behind the host copy)
     if (!e || !gathered_dev || n_ranks < 1) return KB_ERR_INVALID;
     StepArgs a;
     fill_step_args(e, a, summary_recs((unsigned char*)gathered_dev, n_ranks), 0);
@@ -1198,6 +1231,7 @@ extern "C" int kb_engine_sharded_resolve(kb_engine* e, const void* gathered_dev,
 }
 
 extern "C" int kb_engine_sharded_collect(kb_engine* e, kb_change* out, int64_t cap, int64_t* n_out) {
+    if (e) e->ctl_mirror = false;            // (the device block changes behind the host copy)
     if (!e || !n_out || cap < 0) return KB_ERR_INVALID;
     *n_out = 0;
     HIPCHK(hipMemcpyAsync(e->h_ctl, e->ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, e->st));
@@ -1226,6 +1260,7 @@ extern "C" int kb_engine_sharded_collect(kb_engine* e, kb_change* out, int64_t c
 }
 
 extern "C" int kb_engine_step_finish(kb_engine* e, const void* gathered_dev, int32_t n_ranks, kb_change* out) {
+    if (e) e->ctl_mirror = false;            // (the device block changes behind the host copy)
     if (!e || !gathered_dev || n_ranks < 1 || !out) return KB_ERR_INVALID;
     if (e->pending) return pending_result(e, out);
     StepArgs a;

@@ -1022,6 +1022,11 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
 
     // ---- one memory round trip: the broker state, the allowed-set words, the control
     // block and (speculatively: the buffer always exists) the first record's header
+#ifndef KB_REP
+#define KB_REP 0                    // diagnostic timing builds: phases run twice (idempotent)
+#endif
+    for (int rep = 0; rep < ((KB_REP & 4) ? 2 : 1); rep++) {
+    if (rep) __syncthreads();
     for (int b = tid; b < B; b += STEP_THREADS) {
         s_ld[b] = a.load[b];
         s_e[b] = a.eb[b];
@@ -1035,6 +1040,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
             if (q + 1 < nq) *(uint4*)(s_sb + q) = *(const uint4*)(a.setbits + q);
             else s_sb[q] = a.setbits[q];
         }
+    }
     }
     KB_STAMP(ctl, 27);
     double hd0 = HUGE_VAL, hd1 = HUGE_VAL;
@@ -1807,6 +1813,12 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
             if (lane == 0) { s_fq[0][wid] = sS; s_fq[1][wid] = sE; s_fcnt[wid] = cn; }
         }
         __syncthreads();
+
+#if KB_ABL & 16
+        if (tid == 0) C.prepped = 1;                  // diagnostic timing build: stop here
+        write_back();
+        return;
+#endif
         // F2: touched old positions; S, avg, r, U0/V/Rm partials; upper bound partials; set marks
         if (srt)
             for (int i = tid; i < B; i += STEP_THREADS) {
@@ -1869,6 +1881,11 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
         }
         __syncthreads();
         KB_STAMP(ctl, 6);
+#if KB_ABL & 8
+        if (tid == 0) C.prepped = 1;                  // diagnostic timing build: stop here
+        write_back();
+        return;
+#endif
         // F3: new positions of the untouched brokers; eps and the control block (wave 0)
         int nb[NQ], np[NQ];
         if (srt) {
@@ -1956,8 +1973,15 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
         }
         __syncthreads();
         KB_STAMP(ctl, 8);
+#if KB_ABL & 4
+        if (tid == 0) C.prepped = 1;                  // diagnostic timing build: stop here
+        write_back();
+        return;
+#endif
         // F5: bl_move = brokers present in the load map or listed in -broker-ids
         // (steps.go:150-157): membership bits, order / position writes, order certification
+        for (int rep = 0; rep < ((KB_REP & 1) ? 2 : 1); rep++) {
+        if (rep) __syncthreads();
         constexpr int PT = MAXB / STEP_THREADS;          // universe positions per thread
         int flag[PT], c = 0;
         const int base = tid * PT;
@@ -2005,6 +2029,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
                 }
             }
             if (tid == 0 && nblm == 0) { C.light = -1; C.heavy = -1; }
+        }
         }
         if (s_unc) {
             if (tid == 0) { C.halted = H_NEED_EXACT; C.prepped = 0; C.total_exact_halts++; }
@@ -2305,6 +2330,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
         // each wave builds its records in LDS, then writes them as whole 16-B units
         constexpr int MAXU = sr_units(MAXR);
         __shared__ __align__(16) uint16_t s_rs[NW][G][8 * MAXU];
+        for (int rep = 0; rep < ((KB_REP & 2) ? 2 : 1); rep++) {
         if (tid == 0) s_cursor = 0;
         __syncthreads();
         while (s_cursor < nwords) {
@@ -2413,6 +2439,8 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
             }
             __syncthreads();
             KB_STAMP(ctl, 20);
+        }
+        __syncthreads();
         }
     }
     if (tid == 0) { C.prepped = 1; C.full_prep = 0; }

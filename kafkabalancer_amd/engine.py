@@ -282,10 +282,18 @@ class Engine:
 
     def plan(self, max_steps):
         """Device-resident plan; returns (changes, error_or_None)."""
+        return self.changes(*self.plan_raw(max_steps))
+
+    def plan_raw(self, max_steps):
+        """The plan call alone (the bench's timed region): (kb_change array, n, rc)."""
         buf = (kb_change * max(1, max_steps))()
         n = C.c_int64()
         rc = lib().kb_engine_plan(self.h, max_steps, buf, C.byref(n))
-        changes = [_change_dict(buf[i]) for i in range(n.value)]
+        return buf, n.value, rc
+
+    def changes(self, buf, n, rc):
+        """plan_raw's result as (changes, error_or_None)."""
+        changes = [_change_dict(buf[i]) for i in range(n)]
         err = None
         if rc < 0:
             err = EngineError(rc, self.last_error(), changes[-1] if changes else None)
