@@ -1022,11 +1022,6 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
 
     // ---- one memory round trip: the broker state, the allowed-set words, the control
     // block and (speculatively: the buffer always exists) the first record's header
-#ifndef KB_REP
-#define KB_REP 0                    // diagnostic timing builds: phases run twice (idempotent)
-#endif
-    for (int rep = 0; rep < ((KB_REP & 4) ? 2 : 1); rep++) {
-    if (rep) __syncthreads();
     for (int b = tid; b < B; b += STEP_THREADS) {
         s_ld[b] = a.load[b];
         s_e[b] = a.eb[b];
@@ -1040,7 +1035,6 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
             if (q + 1 < nq) *(uint4*)(s_sb + q) = *(const uint4*)(a.setbits + q);
             else s_sb[q] = a.setbits[q];
         }
-    }
     }
     KB_STAMP(ctl, 27);
     double hd0 = HUGE_VAL, hd1 = HUGE_VAL;
@@ -1797,18 +1791,23 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
         __shared__ int s_fwc[NW];
         // F1: touched marks; S, E and |bl_move| partials; clears; best keys issued
         if (srt && tid < nT) { s_fl[s_T[tid]] |= BF_TOUCHED; s_cntT[tid] = 0; }
-        for (int w = tid; w < MAXB / 64; w += STEP_THREADS) { s_blmb[w] = 0; s_presb[w] = 0; }
         for (int w = tid; w < (a.nsets + 31) / 32; w += STEP_THREADS) s_smark[w] = 0u;
         if (tid == 0) s_unc = 0;
+        // (the records' best keys came with their headers at the start: no round trip here)
         const bool bkeys = do_res && tid < a.R.n;
-        Contender bk0, bk1;
-        bk0.s = bk1.s = -1;
-        if (bkeys) { bk0 = ldobj(&a.R.h(tid)->best[0]); bk1 = ldobj(&a.R.h(tid)->best[1]); }
+        const Contender& bk0 = hb0;
+        const Contender& bk1 = hb1;
         {
             double sS = 0.0, sE = 0.0;
             int cn = 0;
-            for (int b = tid; b < B; b += STEP_THREADS)
-                if (s_fl[b] & (BF_PRESENT | BF_INCFG)) { sS += s_ld[b]; sE += s_e[b]; cn++; }
+            // (bl_move membership bits by broker id, one ballot per 64 brokers)
+            for (int b0 = 0; b0 < B; b0 += STEP_THREADS) {
+                const int b = b0 + tid;
+                const bool in = b < B && (s_fl[b] & (BF_PRESENT | BF_INCFG));
+                if (in) { sS += s_ld[b]; sE += s_e[b]; cn++; }
+                const unsigned long long m = __ballot(in);
+                if (lane == 0 && b0 + wid * 64 < B) s_blmb[(b0 >> 6) + wid] = m;
+            }
             sS = wave_sum(sS); sE = wave_sum(sE); cn = wave_sum(cn);
             if (lane == 0) { s_fq[0][wid] = sS; s_fq[1][wid] = sE; s_fcnt[wid] = cn; }
         }
@@ -1913,45 +1912,13 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
                 np[q] = i - before + below;
             }
         }
-        if (wid == 0) {
+        // the step totals: one wave per partial array (the combination waits for F4)
+        __shared__ double s_red[7];
+        if (wid < (a.incr ? 7 : 5)) {
             const bool in = lane < NW;
-            const double U0 = wave_sum(in ? s_fq2[0][lane] : 0.0), V = wave_sum(in ? s_fq2[1][lane] : 0.0);
-            const double Rm = wave_max(in ? s_fq2[2][lane] : 0.0);
-            const double ub0 = wave_min(in ? s_fq2[3][lane] : HUGE_VAL);
-            const double ub1 = wave_min(in ? s_fq2[4][lane] : HUGE_VAL);
-            // (every lane: the incremental certificate below needs eps on the whole wave)
-            const double u = DBL_EPSILON / 2;
-            const double n = (double)nblm;
-            const double R = Rm + a.wmax * iav;
-            const double Ea = E * iav;
-            double epsf = 64.0 * u * ((n + 8.0) * (U0 + 2.0 * V) + 4.0 * (1.0 + R) * (1.0 + R));
-            double epsl = 16.0 * Ea * (V / (n > 0 ? n : 1.0) + R + 1.0) + 4.0 * Ea * Ea;
-            double ep = epsf + epsl;
-            if (!(ep > 1e-300)) ep = 1e-300;
-            // incremental mode: after a move() with bl_move and the first-index predicates
-            // unchanged, the next scan may skip the blocks lighter than wskip
-            double ws = 0.0;
-            const bool inc = a.incr && do_res && D.status == 1 && D.kind == 1 && (D.step == 7 || D.step == 8) &&
-                             nblm == nblm0 && !s_fm && !a.rebalance && !a.sem_go && a.use_spill;
-            if (inc) {
-                const double rlo = wave_min(in ? s_fq2[5][lane] : HUGE_VAL);
-                const double rhi = wave_max(in ? s_fq2[6][lane] : -HUGE_VAL);
-                const double ubP = a.allow_leader ? (ub0 > ub1 ? ub0 : ub1) : ub1;
-                ws = incr_wskip(rlo, rhi, ubP + 16.0 * ep, avg, iav, lane);
-            }
-            if (lane == 0) {
-                C.incr_ok = ws > 0.0 ? 1 : 0;
-                C.wskip = ws;
-                C.S = S; C.avg = avg; C.inv_avg = iav; C.U0 = U0;
-                C.V = V; C.eps = ep; C.E = E; C.nblm = nblm;
-                // after a first-index stage (Remove/Add/Disallowed) the next step is most
-                // likely one too: no census (ub = -inf; k_step re-scans if move() is reached)
-                const bool sup = a.use_spill && do_res && D.status == 1 && D.step >= 3 && D.step <= 5;
-                C.ub[0] = sup ? -HUGE_VAL : ub0; C.ub[1] = sup ? -HUGE_VAL : ub1;
-                C.want_refresh = (epsl > epsf || C.ndirty >= 256) ? 1 : 0;
-                C.ncont = 0;
-                C.cont_overflow = 0;
-            }
+            const double x = in ? s_fq2[wid][lane] : (wid == 2 || wid == 6) ? -HUGE_VAL : (wid == 0 || wid == 1) ? 0.0 : HUGE_VAL;
+            const double y = (wid == 0 || wid == 1) ? wave_sum(x) : (wid == 2 || wid == 6) ? wave_max(x) : wave_min(x);
+            if (lane == 0) s_red[wid] = y;
         }
         __syncthreads();
         // F4: scatter into the new order
@@ -1971,6 +1938,40 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
                 s_ord[s_cntT[tid] + rank] = t;
             }
         }
+        if (wid == 0) {
+            const double U0 = s_red[0], V = s_red[1], Rm = s_red[2], ub0 = s_red[3], ub1 = s_red[4];
+            // (every lane: the incremental certificate below needs eps on the whole wave)
+            const double u = DBL_EPSILON / 2;
+            const double n = (double)nblm;
+            const double R = Rm + a.wmax * iav;
+            const double Ea = E * iav;
+            double epsf = 64.0 * u * ((n + 8.0) * (U0 + 2.0 * V) + 4.0 * (1.0 + R) * (1.0 + R));
+            double epsl = 16.0 * Ea * (V / (n > 0 ? n : 1.0) + R + 1.0) + 4.0 * Ea * Ea;
+            double ep = epsf + epsl;
+            if (!(ep > 1e-300)) ep = 1e-300;
+            // incremental mode: after a move() with bl_move and the first-index predicates
+            // unchanged, the next scan may skip the blocks lighter than wskip
+            double ws = 0.0;
+            const bool inc = a.incr && do_res && D.status == 1 && D.kind == 1 && (D.step == 7 || D.step == 8) &&
+                             nblm == nblm0 && !s_fm && !a.rebalance && !a.sem_go && a.use_spill;
+            if (inc) {
+                const double ubP = a.allow_leader ? (ub0 > ub1 ? ub0 : ub1) : ub1;
+                ws = incr_wskip(s_red[5], s_red[6], ubP + 16.0 * ep, avg, iav, lane);
+            }
+            if (lane == 0) {
+                C.incr_ok = ws > 0.0 ? 1 : 0;
+                C.wskip = ws;
+                C.S = S; C.avg = avg; C.inv_avg = iav; C.U0 = U0;
+                C.V = V; C.eps = ep; C.E = E; C.nblm = nblm;
+                // after a first-index stage (Remove/Add/Disallowed) the next step is most
+                // likely one too: no census (ub = -inf; k_step re-scans if move() is reached)
+                const bool sup = a.use_spill && do_res && D.status == 1 && D.step >= 3 && D.step <= 5;
+                C.ub[0] = sup ? -HUGE_VAL : ub0; C.ub[1] = sup ? -HUGE_VAL : ub1;
+                C.want_refresh = (epsl > epsf || C.ndirty >= 256) ? 1 : 0;
+                C.ncont = 0;
+                C.cont_overflow = 0;
+            }
+        }
         __syncthreads();
         KB_STAMP(ctl, 8);
 #if KB_ABL & 4
@@ -1980,8 +1981,6 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
 #endif
         // F5: bl_move = brokers present in the load map or listed in -broker-ids
         // (steps.go:150-157): membership bits, order / position writes, order certification
-        for (int rep = 0; rep < ((KB_REP & 1) ? 2 : 1); rep++) {
-        if (rep) __syncthreads();
         constexpr int PT = MAXB / STEP_THREADS;          // universe positions per thread
         int flag[PT], c = 0;
         const int base = tid * PT;
@@ -1992,10 +1991,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
             if (i < B) {
                 const int b = s_ord[i];
                 const uint8_t fl = s_fl[b];
-                const bool pres = (fl & BF_PRESENT) != 0;
                 flag[q] = (fl & (BF_PRESENT | BF_INCFG)) ? 1 : 0;
-                if (flag[q]) atomicOr((unsigned long long*)&s_blmb[b >> 6], 1ull << (b & 63));
-                if (pres) atomicOr((unsigned long long*)&s_presb[b >> 6], 1ull << (b & 63));
                 c += flag[q];
                 a.order[i] = b;
                 a.posu[b] = i;
@@ -2029,7 +2025,6 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
                 }
             }
             if (tid == 0 && nblm == 0) { C.light = -1; C.heavy = -1; }
-        }
         }
         if (s_unc) {
             if (tid == 0) { C.halted = H_NEED_EXACT; C.prepped = 0; C.total_exact_halts++; }
@@ -2330,7 +2325,6 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
         // each wave builds its records in LDS, then writes them as whole 16-B units
         constexpr int MAXU = sr_units(MAXR);
         __shared__ __align__(16) uint16_t s_rs[NW][G][8 * MAXU];
-        for (int rep = 0; rep < ((KB_REP & 2) ? 2 : 1); rep++) {
         if (tid == 0) s_cursor = 0;
         __syncthreads();
         while (s_cursor < nwords) {
@@ -2439,8 +2433,6 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
             }
             __syncthreads();
             KB_STAMP(ctl, 20);
-        }
-        __syncthreads();
         }
     }
     if (tid == 0) { C.prepped = 1; C.full_prep = 0; }
