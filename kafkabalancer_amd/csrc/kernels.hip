@@ -161,6 +161,41 @@ __device__ double exact_unbalance_lds(const double* Lm, int n, int ps, int pt, d
     return U;
 }
 
+// The same folds run by one whole wave (every lane gets the result).  The lanes load
+// and compute 64 elements at a time in parallel (the 4096-broker case divides per term:
+// one lane doing all of them was issue-bound on the division sequences); the in-order
+// additions then run on the wave, element j read from lane j with readlane (SGPR
+// operand), one dependent add per element as in the reference.  Padding past n adds
+// +0.0, which leaves every fold here unchanged (all its terms and sums are >= +0).
+__device__ __forceinline__ double lane_val(double v, int j) {
+    const int hi = __builtin_amdgcn_readlane(__double2hiint(v), j);
+    const int lo = __builtin_amdgcn_readlane(__double2loint(v), j);
+    return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double wave_fold64(double acc, double v) {
+#pragma unroll
+    for (int j = 0; j < 64; j++) acc += lane_val(v, j);
+    return acc;
+}
+// getUnbalanceBL of bl[] with bl[ps] = Ls, bl[pt] = Lt (ps / pt = -1: none)
+__device__ double exact_unbalance_wave(const double* Lm, int n, int ps, int pt, double Ls, double Lt) {
+    const int lane = threadIdx.x & 63;
+    double S = 0.0;
+    for (int k = 0; k < n; k += 64) {
+        const int i = k + lane;
+        const double v = i < n ? (i == ps ? Ls : (i == pt ? Lt : Lm[i])) : 0.0;
+        S = wave_fold64(S, v);
+    }
+    const double avg = S / (double)n;
+    double U = 0.0;
+    for (int k = 0; k < n; k += 64) {
+        const int i = k + lane;
+        const double t = i < n ? term_x(i == ps ? Ls : (i == pt ? Lt : Lm[i]), avg) : 0.0;
+        U = wave_fold64(U, t);
+    }
+    return U;
+}
+
 // ---------------------------------------------- near-tie de-duplication
 // LDS open-addressing table keyed by (kind, source, target); the weight bits are
 // claimed by the first insert; a different weight under the same key is a
@@ -1353,15 +1388,17 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
             // exact su (sequential folds in bl order); s_e doubles as the bl-ordered loads
             // (every load is exact here, so every error bound is zero)
             double* s_Lm = s_e;
-            auto exact_su = [&]() {
+            auto stage_exact = [&]() {
                 for (int k = tid; k < nblm0; k += STEP_THREADS) s_Lm[k] = s_ld[(int)ld32(a.blm + k)];
                 __syncthreads();
-                if (tid == 0) {
-                    const double S = fold_lds(s_Lm, nblm0);
-                    const double avg = S / (double)nblm0;
-                    s_sux = fold_terms_lds(s_Lm, nblm0, avg);
-                    atomicAdd(&C.total_folds, 1ull);
-                }
+            };
+            auto su_wave = [&]() {               // (wave 0, after stage_exact)
+                const double su = exact_unbalance_wave(s_Lm, nblm0, -1, -1, 0.0, 0.0);
+                if (lane == 0) { s_sux = su; atomicAdd(&C.total_folds, 1ull); }
+            };
+            auto exact_su = [&]() {
+                stage_exact();
+                if (wid == 0) su_wave();
                 __syncthreads();
             };
             auto unstage = [&]() {
@@ -1466,15 +1503,17 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
                     witer = cw.iter;
                 } else {
                     exact = 1;
-                    exact_su();                      // also stages the exact loads in bl order
-                    sux = s_sux;
+                    // exact su on wave 0 while the other waves fold the contenders
+                    stage_exact();
+                    if (wid == 0) su_wave();
                     if (!fail && ndist == 1) {
-                        if (tid == 0) {
-                            s_dv[0] = exact_unbalance_lds(s_Lm, nblm0, (int)ld32(a.posm + cw.s), (int)ld32(a.posm + cw.t),
-                                                          s_ld[cw.s] - cw.w, s_ld[cw.t] + cw.w);
-                            atomicAdd(&C.total_folds, 1ull);
+                        if (wid == 1) {
+                            const double u = exact_unbalance_wave(s_Lm, nblm0, (int)ld32(a.posm + cw.s), (int)ld32(a.posm + cw.t),
+                                                                  s_ld[cw.s] - cw.w, s_ld[cw.t] + cw.w);
+                            if (lane == 0) { s_dv[0] = u; atomicAdd(&C.total_folds, 1ull); }
                         }
                         __syncthreads();
+                        sux = s_sux;
                         Ustar = s_dv[0];
                         witer = cw.iter;
                     } else if (have) {
@@ -1484,17 +1523,29 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
                         int bs = -1, bt = -1;
                         double bw = 0.0;
                         unsigned long long nf = 0;
-                        auto consider = [&](const Contender& c) {
-                            const double u = exact_unbalance_lds(s_Lm, nblm0, (int)ld32(a.posm + c.s), (int)ld32(a.posm + c.t),
-                                                                 s_ld[c.s] - c.w, s_ld[c.t] + c.w);
-                            nf++;
+                        auto better = [&](double u, const Contender& c) {
                             if (u < bu || (u == bu && c.iter < bi)) { bu = u; bi = c.iter; bs = c.s; bt = c.t; bw = c.w; }
                         };
                         if (!fail) {
-                            for (int h = tid; h < DEDUP_STEP; h += STEP_THREADS)
-                                if (s_key[h] != NONE32 && (int)(s_key[h] >> 30) == kind) consider(dedup_entry(T, h));
+                            // one contender per wave (waves 1..NW-1; the table slot is wave-uniform)
+                            if (wid > 0)
+                                for (int h = wid - 1; h < DEDUP_STEP; h += NW - 1) {
+                                    if (!(s_key[h] != NONE32 && (int)(s_key[h] >> 30) == kind)) continue;
+                                    const Contender c = dedup_entry(T, h);
+                                    const double u = exact_unbalance_wave(s_Lm, nblm0, (int)ld32(a.posm + c.s), (int)ld32(a.posm + c.t),
+                                                                          s_ld[c.s] - c.w, s_ld[c.t] + c.w);
+                                    if (lane == 0) nf++;
+                                    better(u, c);
+                                }
                         } else {
-                            for_each_contender(a, s_ld, C.ncont, kind, g, eps, inv_avg, consider);
+                            // (the spill path: per-thread folds over the records and the buffer)
+                            __syncthreads();
+                            for_each_contender(a, s_ld, C.ncont, kind, g, eps, inv_avg, [&](const Contender& c) {
+                                const double u = exact_unbalance_lds(s_Lm, nblm0, (int)ld32(a.posm + c.s), (int)ld32(a.posm + c.t),
+                                                                     s_ld[c.s] - c.w, s_ld[c.t] + c.w);
+                                nf++;
+                                better(u, c);
+                            });
                         }
                         nf = wave_sum(nf);
                         if (lane == 0 && nf) atomicAdd(&C.total_folds, nf);
@@ -1515,8 +1566,12 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
                                 }
                         }
                         __syncthreads();
+                        sux = s_sux;
                         Ustar = s_dv[0]; witer = s_u[0];
                         cw.s = s_bs[0]; cw.t = s_bt[0]; cw.w = s_bw[0]; cw.iter = witer;
+                    } else {
+                        __syncthreads();
+                        sux = s_sux;
                     }
                     unstage();
                     // cu starts at su and only a strictly smaller u replaces it (steps.go:163,211)
@@ -2458,28 +2513,44 @@ __global__ __launch_bounds__(1024) void k_listop(DevCtl* ctl, Lists L) {
 // folded sequentially by one lane.
 
 constexpr int REFRESH_THREADS = 256;
-constexpr int REFRESH_CHUNK = 4096;
-
+constexpr int REFRESH_CHUNK = 1024;
+// One workgroup per dirty broker: the exact getBrokerLoad fold (utils.go:92-105) of its
+// contributions in partition order.  Double-buffered: while wave 0 folds chunk j (a
+// wave fold: 64 contributions per load, one dependent add each), waves 1.. gather
+// chunk j + 1 from the partition list.
 __global__ __launch_bounds__(REFRESH_THREADS) void k_refresh(RefreshArgs a) {
     const int b = blockIdx.x;
     if (b >= a.B || !(a.bfl[b] & BF_DIRTY)) return;
-    __shared__ double s_c[REFRESH_CHUNK];
+    __shared__ double s_c[2][REFRESH_CHUNK];
     const uint32_t st = a.L.lstart[b], n = a.L.llen[b];
-    double acc = 0.0;
-    for (uint32_t c0 = 0; c0 < n; c0 += REFRESH_CHUNK) {
+    const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
+    auto gather = [&](uint32_t c0, double* dst, int t0, int nt) {
         const uint32_t m = n - c0 < (uint32_t)REFRESH_CHUNK ? n - c0 : (uint32_t)REFRESH_CHUNK;
-        for (uint32_t i = threadIdx.x; i < m; i += REFRESH_THREADS) {
+        for (uint32_t i = (uint32_t)t0; i < m; i += (uint32_t)nt) {
             const uint32_t q = a.L.lent[st + c0 + i];
             const uint32_t mq = a.meta[q];
             const double w = a.w[q];
             // slot 0 carries the leader weight W * (len(R) + NumConsumers)
-            s_c[i] = (a.rep[q] == (uint16_t)b) ? w * (double)((int)meta_nrep(mq) + a.nc[q]) : w;
+            dst[i] = (a.rep[q] == (uint16_t)b) ? w * (double)((int)meta_nrep(mq) + a.nc[q]) : w;
+        }
+    };
+    double acc = 0.0;
+    if (n) gather(0, s_c[0], tid, REFRESH_THREADS);
+    __syncthreads();
+    for (uint32_t c0 = 0, j = 0; c0 < n; c0 += REFRESH_CHUNK, j++) {
+        const uint32_t m = n - c0 < (uint32_t)REFRESH_CHUNK ? n - c0 : (uint32_t)REFRESH_CHUNK;
+        if (wid > 0 && c0 + REFRESH_CHUNK < n)
+            gather(c0 + REFRESH_CHUNK, s_c[(j + 1) & 1], tid - 64, REFRESH_THREADS - 64);
+        if (wid == 0) {
+            const double* x = s_c[j & 1];
+            for (uint32_t k = 0; k < m; k += 64) {
+                const uint32_t i = k + (uint32_t)lane;
+                acc = wave_fold64(acc, i < m ? x[i] : 0.0);   // (+0.0 padding: contributions >= 0)
+            }
         }
         __syncthreads();
-        if (threadIdx.x == 0) acc = fold_lds(s_c, (int)m, acc);
-        __syncthreads();
     }
-    if (threadIdx.x == 0) {
+    if (tid == 0) {
         a.load[b] = acc;
         a.lerr[b] = gamma_n((int)n) * acc;
         a.eb[b] = 0.0;
