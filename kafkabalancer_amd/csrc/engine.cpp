@@ -110,6 +110,7 @@ struct kb_engine {
     int incr = 0;                  // incremental mode (kb_engine_set_incremental)
     BlockDesc* bdesc = nullptr;    // partition blocks of the shard by wmax descending
     int64_t nblk = 0;
+    int batch = 64;                // (scan, step) pairs per enqueued batch (adaptive, run_steps)
     bool ub_mode = false;          // a step re-scanned: enqueue the conditional bound pass per scan
     uint32_t list_slack = 1024;        // free entries per broker list (doubled on every re-layout)
     int64_t relists = 0;
@@ -862,8 +863,9 @@ static int run_steps(kb_engine* e, int64_t max_steps) {
     for (;;) {
         const int64_t done = e->h_ctl->steps - steps0;
         if (done >= max_steps) break;
-        const int64_t pairs = std::min<int64_t>(kStepBatch, max_steps - done + (prepped ? 0 : 1));
+        const int64_t pairs = std::min<int64_t>(e->batch, max_steps - done + (prepped ? 0 : 1));
         const int lp0 = e->h_ctl->logpos;
+        const int st0 = e->h_ctl->steps;
         for (int64_t s = 0; s < pairs; s++) {
             // pair 0 ran the full prep; once a step had to re-scan (no surviving best
             // keys bound the next minimum), every scan gets the conditional bound pass
@@ -885,6 +887,13 @@ static int run_steps(kb_engine* e, int64_t max_steps) {
         harvest(e);
         const DevCtl& c = *e->h_ctl;
         if (c.total_retries > 0) e->ub_mode = true;
+        // adaptive batch: the pairs enqueued behind a halted step run as no-ops (a launch
+        // each), so after a halt the next batch is about twice the steps that ran before
+        // it; full batches double it again, up to kStepBatch
+        if (c.halted == H_NEED_EXACT || c.halted == H_NEED_SPILL || c.want_refresh)
+            e->batch = (int)std::max<int64_t>(4, std::min<int64_t>(kStepBatch, 2 * (int64_t)(c.steps - st0) + 2));
+        else if (c.steps - st0 >= pairs - 1)
+            e->batch = std::min(kStepBatch, 2 * e->batch);
         if (c.halted == H_DONE) break;
         if (c.halted == H_NEED_SPILL) {
             // more near-tied candidates than the spill buffer holds: grow it, run the step again
