@@ -109,6 +109,8 @@ struct kb_engine {
     int dbg_scan = 0;
     int incr = 0;                  // incremental mode (kb_engine_set_incremental)
     BlockDesc* bdesc = nullptr;    // partition blocks of the shard by wmax descending
+    BlockDesc* ubdesc = nullptr;   // the bound pass's blocks (last best keys + heaviest)
+    int64_t nubdesc = 0;
     int64_t nblk = 0;
     int batch = 64;                // (scan, step) pairs per enqueued batch (adaptive, run_steps)
     bool ub_mode = false;          // a step re-scanned: enqueue the conditional bound pass per scan
@@ -496,6 +498,22 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
     HIPCHK(dalloc(&e->cont, e->cont_cap));
     HIPCHK(dalloc(&e->ctl, 1));
     HIPCHK(dalloc(&e->bdesc, std::max<size_t>(hbd.size(), 1)));
+    {
+        // bound-pass block list: [0, 2 * max(nscan, STEP_THREADS)) the blocks of the last
+        // records' best keys (k_step writes them; -1: none), then the heaviest blocks by
+        // weight up to one block per scan wave
+        const size_t kr = 2 * (size_t)std::max<int64_t>(e->nscan, STEP_THREADS);
+        const size_t tot = std::max<size_t>(kr, (size_t)e->nscan * (SCAN_THREADS / 64));
+        std::vector<BlockDesc> hub(tot);
+        for (size_t i = 0; i < tot; i++) {
+            const size_t j = i - kr;
+            if (i >= kr && j < hbd.size()) hub[i] = hbd[j];
+            else { hub[i].wmax = -1.0; hub[i].blk = 0; }
+        }
+        e->nubdesc = (int64_t)tot;
+        HIPCHK(dalloc(&e->ubdesc, tot));
+        HIPCHK(hipMemcpy(e->ubdesc, hub.data(), tot * sizeof(BlockDesc), hipMemcpyHostToDevice));
+    }
     if (!hbd.empty()) HIPCHK(hipMemcpy(e->bdesc, hbd.data(), hbd.size() * sizeof(BlockDesc), hipMemcpyHostToDevice));
     e->logcap = 1024;
     HIPCHK(dalloc(&e->log, e->logcap));
@@ -578,6 +596,8 @@ static void fill_step_args(kb_engine* e, StepArgs& a, const Recs& R, int use_spi
     a.minrep = e->minrep; a.min_unbalance = e->min_unb; a.wmax = e->wmax;
     a.log = e->log; a.L = e->L;
     a.incr = e->incr && use_spill;
+    a.ubdesc = e->ubdesc;
+    a.ub_heavy = e->nubdesc > 2 * std::max<int64_t>(e->nscan, STEP_THREADS) ? 1 : 0;
 }
 
 static const int kStepBatch = 64;
@@ -630,6 +650,11 @@ static void enqueue_ubinit(kb_engine* e) {
     s.listwg = 0;
     s.dbg |= 1;
     s.ubpass = 1;
+    // (set records in LDS: the block-list kernel, which scans only the blocks of the last
+    // records' best keys when k_step left them, DevCtl.ub_sub)
+    s.incr = e->lds_sets ? 1 : 0;
+    s.bdesc = e->ubdesc;
+    s.nblk = (int)e->nubdesc;
     launch_scan(s, e->rc_dev, e->lds_sets, e->scan_lds, e->st);
     launch_ubinit(e->ctl, scan_recs(e->recs, (int)e->nscan), e->allow_leader, e->st);
 }
@@ -1165,7 +1190,7 @@ extern "C" void kb_engine_destroy(kb_engine* e) {
     if (!e) return;
     void* ptrs[] = {e->w, e->rep, e->meta, e->nc, e->load, e->lerr, e->eb, e->bfl, e->cnt,
                     e->setbits, e->setrec, e->order, e->posu, e->blm, e->posm, e->r,
-                    e->bset_off, e->bset_ids, e->recs, e->cont, e->ctl, e->log, e->bdesc,
+                    e->bset_off, e->bset_ids, e->recs, e->cont, e->ctl, e->log, e->bdesc, e->ubdesc,
                     e->L.lstart, e->L.llen, e->L.lcap, e->L.lent};
     for (void* p : ptrs) if (p) hipFree(p);
     if (e->h_ctl) hipHostFree(e->h_ctl);

@@ -179,7 +179,10 @@ struct DevCtl {
     // may skip every partition block whose largest weight is below wskip (a lower-bound
     // certificate, see k_step); cand_cache = the candidate counts of the last full scan,
     // which move() steps leave unchanged
-    int32_t incr_ok, incr_pad;
+    int32_t incr_ok;
+    int32_t ub_sub;                 // > 0: the conditional bound pass may scan only the blocks of
+                                    // the last records' best keys (StepArgs.ubdesc), not all
+
     double wskip;
     unsigned long long cand_cache[2];
     unsigned long long total_blocks;    // partition blocks the incremental scans read

@@ -777,7 +777,7 @@ __device__ __forceinline__ void scan_round(const ScanArgs& a, const ScanParams& 
         nu++;
         c0 = c2;
     }
-    if (INCR && q.incr && lane == 0 && nu) atomicAdd(&ctl->total_blocks, (unsigned long long)nu);
+    if (INCR && q.incr && !a.ubpass && lane == 0 && nu) atomicAdd(&ctl->total_blocks, (unsigned long long)nu);
     // workgroup record: counts, first-index predicates, minima, near-tie keys
     cL = wave_sum(cL);
     cN = wave_sum(cN);
@@ -900,8 +900,10 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
     q.heavy = ctl->heavy; q.nblm = ctl->nblm;
     q.tk_on = ctl->tk_on;
     q.ubpass = 0;
-    q.incr = INCR && ctl->incr_ok;
-    q.wskip = INCR ? ctl->wskip : 0.0;
+    // (a conditional bound pass launched on the block list of the last records' best
+    // keys: those blocks only, when k_step left one, else every tile)
+    q.incr = INCR && (a.ubpass ? ctl->ub_sub > 0 : ctl->incr_ok);
+    q.wskip = INCR && !a.ubpass ? ctl->wskip : 0.0;
     long long c0 = -1;
     if (INCR && !q.incr && (int)blockIdx.x < a.ntiles) load_parts<RC>(a, a0, A);
     if (INCR && q.incr && d0.wmax >= q.wskip) {
@@ -1847,7 +1849,8 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
         // F1: touched marks; S, E and |bl_move| partials; clears; best keys issued
         if (srt && tid < nT) { s_fl[s_T[tid]] |= BF_TOUCHED; s_cntT[tid] = 0; }
         for (int w = tid; w < (a.nsets + 31) / 32; w += STEP_THREADS) s_smark[w] = 0u;
-        if (tid == 0) s_unc = 0;
+        __shared__ int s_nsub;
+        if (tid == 0) { s_unc = 0; s_nsub = 0; }
         // (the records' best keys came with their headers at the start: no round trip here)
         const bool bkeys = do_res && tid < a.R.n;
         const Contender& bk0 = hb0;
@@ -1908,11 +1911,24 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
 #pragma unroll
                 for (int k = 0; k < 2; k++) {
                     const Contender& c = k ? bk1 : bk0;
-                    if (c.s < 0 || (long long)(c.iter >> 21) == pm) continue;
+                    // the block of every best key other than the moved partition's: if no
+                    // key survives below, the conditional bound pass scans only these blocks
+                    // and the heaviest blocks by weight (engine.cpp fills that part once):
+                    // census-free, their minima bound the step's minimum from above, and
+                    // they hold last step's best candidates, so the bound stays tight
+                    const bool keep = c.s >= 0 && (long long)(c.iter >> 21) != pm;
+                    BlockDesc d;
+                    d.wmax = keep ? HUGE_VAL : -1.0;
+                    d.blk = keep ? (long long)(c.iter >> 21) / BLK : 0;
+                    if (a.ubdesc) {
+                        stobj(a.ubdesc + 2 * tid + k, d);
+                        if (keep) atomicAdd(&s_nsub, 1);
+                    }
+                    if (!keep) continue;
                     if ((s_fl[c.s] | s_fl[c.t]) & BF_TOUCHED) continue;
-                    const double d = cont_delta_ld(s_ld, c, iav);
-                    if (k == 0) ub0 = d < ub0 ? d : ub0;
-                    else ub1 = d < ub1 ? d : ub1;
+                    const double d2 = cont_delta_ld(s_ld, c, iav);
+                    if (k == 0) ub0 = d2 < ub0 ? d2 : ub0;
+                    else ub1 = d2 < ub1 ? d2 : ub1;
                 }
             }
             su = wave_sum(su); v = wave_sum(v); rm = wave_max(rm);
@@ -2016,6 +2032,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
             if (lane == 0) {
                 C.incr_ok = ws > 0.0 ? 1 : 0;
                 C.wskip = ws;
+                C.ub_sub = a.ubdesc && a.R.n <= STEP_THREADS && (s_nsub > 0 || a.ub_heavy) ? 1 : 0;
                 C.S = S; C.avg = avg; C.inv_avg = iav; C.U0 = U0;
                 C.V = V; C.eps = ep; C.E = E; C.nblm = nblm;
                 // after a first-index stage (Remove/Add/Disallowed) the next step is most
@@ -2310,6 +2327,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
         C.ub[0] = sup ? -HUGE_VAL : ub0; C.ub[1] = sup ? -HUGE_VAL : ub1;
         C.incr_ok = 0;                      // (the next scan reads every block)
         C.wskip = 0.0;
+        C.ub_sub = 0;                       // (a bound pass, if any, scans every tile)
         C.want_refresh = (epsl > epsf || C.ndirty >= 256) ? 1 : 0;
         C.ncont = 0;
         C.cont_overflow = 0;

@@ -78,6 +78,8 @@ struct StepArgs {
     ChangeDev* log;
     Lists L;
     int incr;                 // incremental mode (single GPU): decide DevCtl.incr_ok / wskip
+    BlockDesc* ubdesc;        // [2 * R.n] the blocks of the records' best keys (bound pass subset)
+    int ub_heavy;             // 1: ubdesc also lists the heaviest blocks (the subset is never empty)
 };
 
 struct RefreshArgs {
