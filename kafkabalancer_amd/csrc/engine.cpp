@@ -6,6 +6,7 @@
 //
 // Build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off (host folds must
 // round exactly like Go on amd64: no FMA contraction).
+#include <rocprofiler-sdk-roctx/roctx.h>   // host ranges per plan phase (rocprofv3 --marker-trace)
 #include <hip/hip_runtime.h>
 #include <algorithm>
 #include <cfloat>
@@ -716,6 +717,7 @@ static int relist(kb_engine* e) {
 // exact refolds of the approximate loads (k_refresh), then a full prep
 static int refresh(kb_engine* e) {
     if (e) e->ctl_mirror = false;            // (the device block changes behind the host copy)
+    roctxMark("kb:refresh (exact refolds of the approximate loads)");
     if (e->integral) return KB_OK;
     mark(e, -1);
     launch_listop(e->ctl, e->L, e->st);
@@ -844,6 +846,7 @@ static int ensure_log(kb_engine* e, int64_t max_steps) {
 static const uint32_t kContMax = 1u << 26;   // 64M candidates (2 GiB)
 static int grow_spill(kb_engine* e) {
     if (e) e->ctl_mirror = false;            // (the device block changes behind the host copy)
+    roctxMark("kb:grow_spill (near-tie buffer x8, step runs again)");
     if (e->cont_cap >= kContMax) {
         e->last_err = "engine capacity: more than " + std::to_string(kContMax) + " near-tied candidates in one step";
         return KB_ERR_CAPACITY;
@@ -891,6 +894,7 @@ static int run_steps(kb_engine* e, int64_t max_steps) {
         const int64_t pairs = std::min<int64_t>(e->batch, max_steps - done + (prepped ? 0 : 1));
         const int lp0 = e->h_ctl->logpos;
         const int st0 = e->h_ctl->steps;
+        roctxRangePush("kb:batch (scan + step pairs)");
         for (int64_t s = 0; s < pairs; s++) {
             // pair 0 ran the full prep; once a step had to re-scan (no surviving best
             // keys bound the next minimum), every scan gets the conditional bound pass
@@ -908,6 +912,7 @@ static int run_steps(kb_engine* e, int64_t max_steps) {
             HIPCHK(hipMemcpyAsync(e->h_log + lp0, e->log + lp0, (size_t)ln * sizeof(ChangeDev),
                                   hipMemcpyDeviceToHost, e->st));
         HIPCHK(hipStreamSynchronize(e->st));
+        roctxRangePop();
         fresh = true;
         harvest(e);
         const DevCtl& c = *e->h_ctl;

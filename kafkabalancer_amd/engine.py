@@ -119,9 +119,11 @@ def lib():
         L.kb_engine_sharded_resolve.restype = C.c_int
         L.kb_engine_sharded_collect.argtypes = [vp, C.POINTER(kb_change), C.c_int64, P64]
         L.kb_engine_sharded_collect.restype = C.c_int
-        L.kb_engine_set_incremental.argtypes = [vp, C.c_int32]
-        L.kb_engine_set_incremental.restype = C.c_int
-        if L.kb_abi_version() != 6:
+        any_abi = os.environ.get("KB_ABI_ANY") == "1"      # diagnostic: older builds (bisecting)
+        if hasattr(L, "kb_engine_set_incremental"):
+            L.kb_engine_set_incremental.argtypes = [vp, C.c_int32]
+            L.kb_engine_set_incremental.restype = C.c_int
+        if L.kb_abi_version() != 6 and not any_abi:
             raise ImportError("libkbengine.so ABI mismatch")
         _lib = L
     return _lib

@@ -230,3 +230,5 @@ def test_two_engines_one_gpu_batched_protocol():
     assert [key(c) for c in got[0]][:40] == [key(c) for c in want][:len(got[0][:40])]
     assert len(got[0]) == len(want)
     assert engs[0].state() == ref.state() == engs[1].state()
+
+
