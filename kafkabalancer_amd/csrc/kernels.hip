@@ -1103,7 +1103,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
     __shared__ unsigned long long s_lsb[64];
     if (tid == 0) { s_nT = 0; s_done = 0; s_exact_need = 0; s_retry = 0; s_moved = -1; s_lkind = 0; }
     if (tid < NF) s_first[tid] = NONE32;
-    if (tid < 2) s_kc[tid] = 0;
+    if (tid < 2) { s_kc[tid] = 0; s_sok[tid] = -1; }   // (s_sok: -1 = no record offered its best key)
     if (halted != H_RUN) return;
     KB_STAMP(ctl, 12);
     // ---- the scan records (or the gathered rank summaries): one per thread, reduced
@@ -1196,8 +1196,12 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
         }
         __syncthreads();
         // single-key kinds need the raw spill buffer to be empty (its keys are not counted)
-        const bool many = a.R.n > STEP_THREADS || (a.use_spill && C.ncont > 0);
-        const bool need0 = many || s_kc[0] > 1, need1 = many || s_kc[1] > 1;
+        // (rank summaries always take the key path: a summary's best key is its records'
+        // best, which need not be its one key when the census spilled past a workgroup
+        // table -- the summary's key list holds it; and a single key whose record
+        // offered no best key is collected rather than guessed)
+        const bool many = a.R.n > STEP_THREADS || (a.use_spill && C.ncont > 0) || !a.use_spill;
+        const bool need0 = many || s_kc[0] > 1 || s_sok[0] < 0, need1 = many || s_kc[1] > 1 || s_sok[1] < 0;
         if (tid < 2 && !(tid ? need1 : need0) && s_kc[tid] == 1) {
             s_nd[tid] = s_sok[tid] ? 1 : 0;          // resolve takes s_single (s_li == -2)
             s_li[tid] = -2;

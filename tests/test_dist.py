@@ -232,3 +232,112 @@ def test_two_engines_one_gpu_batched_protocol():
     assert engs[0].state() == ref.state() == engs[1].state()
 
 
+
+
+def _gpu_cluster():
+    from kafkabalancer_amd import synth
+    cl = synth.make_cluster(2500, 40, 3, "zipf", nsets=8, set_size=24, seed=5, with_names=True)
+    return cl, default_cfg(allow_leader=True, min_unbalance=0.0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [1, 2])
+def test_sharded_protocol_matches_oracle(world):
+    """One or two shards ([0, 2048) and the 452-partition tail) driven through the
+    batched protocol with host-staged summaries (the gloo rehearsal's exchange), against
+    the oracle's plan (oracle/kb_oracle.c), not the unsharded engine.  (Pins the fix of
+    round 2: rank summaries take the key path -- a summary's best key need not be its
+    one near-tie key when the first step's census spilled.)"""
+    from kafkabalancer_amd import engine as E
+    from kafkabalancer_amd import synth
+    from helpers import oracle_plan
+    cl, cfg = _gpu_cluster()
+    steps = 24
+    engs = [E.Engine(cl, cfg, shard=shard_bounds(cl.n, world, r)) for r in range(world)]
+    nb = engs[0].summary_bytes()
+    summ = [torch.zeros(nb, dtype=torch.uint8, device="cuda") for _ in range(world)]
+    gathered = torch.zeros(world * nb, dtype=torch.uint8, device="cuda")
+    h_gathered = torch.zeros(world * nb, dtype=torch.uint8)
+    torch.cuda.synchronize()
+    got = [[] for _ in range(world)]
+    done = False
+    while not done and len(got[0]) < steps:
+        batch = min(8, steps - len(got[0]))
+        for e in engs:
+            e.sharded_reset(batch)
+        for _ in range(batch):
+            for e, b in zip(engs, summ):
+                e.sharded_scan(b.data_ptr())
+            torch.cuda.synchronize()
+            for r in range(world):                     # staged: device -> host -> device
+                h_gathered[r * nb:(r + 1) * nb].copy_(summ[r])
+            gathered.copy_(h_gathered)
+            torch.cuda.synchronize()
+            for e in engs:
+                e.sharded_resolve(gathered.data_ptr(), world)
+            torch.cuda.synchronize()
+        res = [e.sharded_collect(batch + 1) for e in engs]
+        assert len({st for st, _ in res}) == 1, [st for st, _ in res]
+        for r in range(world):
+            got[r].extend(res[r][1])
+        done = res[0][0] == "done"
+    key = lambda c: (c["step"], c["pidx"], c["kind"], c["from_"], c["to"], c["slot"])
+    for r in range(1, world):
+        assert [key(c) for c in got[r]] == [key(c) for c in got[0]]
+    pl = synth.to_plist(cl)
+    och, oerr, opl = oracle_plan(pl, cfg, steps)
+    assert oerr is None
+    assert [key(c) for c in got[0]][:steps] == [key(c) for c in och]
+    for e in engs:
+        assert e.state() == opl.state()
+
+
+def _gpu_worker(rank, world, port, steps, q):
+    """One rank of the gloo-staged rehearsal on one GPU: the device engine on its shard,
+    the batched protocol (sharded_reset / scan / resolve / collect), summaries
+    exchanged through host copies over gloo (dist.ShardedPlanner(staged=True))."""
+    try:
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        torch.cuda.set_device(0)
+        from kafkabalancer_amd import engine as E
+        from kafkabalancer_amd.dist import _DeviceEngineAdapter
+        cl, cfg = _gpu_cluster()
+        eng = E.Engine(cl, cfg, shard=shard_bounds(cl.n, world, rank))
+        sp = ShardedPlanner(_DeviceEngineAdapter(eng), world, device_tensors=True, staged=True)
+        out = sp.plan(steps, batch=8)
+        q.put((rank, [(c["step"], c["pidx"], c["kind"], c["from_"], c["to"], c["slot"]) for c in out],
+               eng.state(), None))
+        eng.close()
+        dist.destroy_process_group()
+    except Exception as ex:                        # reported to the parent, not swallowed
+        q.put((rank, None, None, repr(ex)))
+
+
+@pytest.mark.gpu
+def test_gloo_two_ranks_gpu_engines_match_oracle():
+    """Two processes (gloo, host-staged summaries) running the engine's sharded scan and
+    resolve kernels on one GPU: both apply the oracle's plan (oracle/kb_oracle.c)."""
+    from kafkabalancer_amd import synth
+    from helpers import oracle_plan
+    steps = 24
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gpu_worker, args=(r, 2, port, steps, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in procs:
+        r, ch, st, err = q.get(timeout=240)
+        assert err is None, "rank %d: %s" % (r, err)
+        res[r] = (ch, st)
+    for p in procs:
+        p.join(timeout=60)
+    assert res[0] == res[1]                        # every rank applied the identical plan
+    cl, cfg = _gpu_cluster()
+    och, oerr, opl = oracle_plan(synth.to_plist(cl), cfg, steps)
+    assert oerr is None
+    assert res[0][0] == [(c["step"], c["pidx"], c["kind"], c["from_"], c["to"], c["slot"]) for c in och]
+    assert res[0][1] == opl.state()
