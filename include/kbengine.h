@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define KB_ABI_VERSION 6
+#define KB_ABI_VERSION 7
 
 /* step indices == position in the reference's steps table (balancer.go:34-44) */
 enum kb_step {
@@ -40,7 +40,9 @@ enum kb_step {
 
 /* kb_change.status / return value of kb_engine_balance */
 enum { KB_NOCHANGE = 0, KB_CHANGE = 1,
-       KB_RETRY = 2 /* kb_engine_step_finish only: loads were refolded exactly, redo the step */ };
+       KB_RETRY = 2 /* kb_engine_step_finish only: loads were refolded exactly, redo the step */,
+       KB_GROW = 3  /* sharded steps: a rank summary overflowed; kb_engine_summary_bytes grew,
+                       re-allocate the exchange buffers and redo the step */ };
 
 /* kinds of change (what replacepl/addpl did, utils.go:166-202) */
 enum { KB_KIND_NONE = 0, KB_KIND_REPLACE = 1, KB_KIND_REMOVE = 2, KB_KIND_ADD = 3, KB_KIND_SWAP = 4 };
@@ -208,6 +210,8 @@ void kb_engine_destroy(kb_engine *e);
  * A step is:  begin (local scan) -> exchange of fixed-size summaries between
  * ranks (all-gather, done by the caller over RCCL) -> finish (identical
  * resolution on every rank).  `summary` and `gathered` are DEVICE pointers. */
+/* bytes of one rank summary: 1936 (56 near-tie keys) to start with; after a KB_GROW it
+ * is 8x the keys (up to 2048), the same on every rank */
 int64_t kb_engine_summary_bytes(kb_engine *e);
 int kb_engine_step_begin(kb_engine *e, void *summary_dev);
 int kb_engine_step_finish(kb_engine *e, const void *gathered_dev, int32_t n_ranks, kb_change *out);

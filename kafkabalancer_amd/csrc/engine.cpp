@@ -114,6 +114,7 @@ struct kb_engine {
     int64_t nubdesc = 0;
     int64_t nblk = 0;
     int batch = 64;                // (scan, step) pairs per enqueued batch (adaptive, run_steps)
+    int sum_keys = SUMMARY_KEYS;   // near-tie keys per rank summary (grown on overflow)
     bool ub_mode = false;          // a step re-scanned: enqueue the conditional bound pass per scan
     uint32_t list_slack = 1024;        // free entries per broker list (doubled on every re-layout)
     int64_t relists = 0;
@@ -1209,7 +1210,45 @@ extern "C" void kb_engine_destroy(kb_engine* e) {
 
 // ----------------------------------------------------- multi-GPU phases
 
-extern "C" int64_t kb_engine_summary_bytes(kb_engine* e) { (void)e; return (int64_t)SUMMARY_BYTES; }
+extern "C" int64_t kb_engine_summary_bytes(kb_engine* e) {
+    return e ? (int64_t)summary_bytes(e->sum_keys) : (int64_t)summary_bytes(SUMMARY_KEYS);
+}
+
+// A rank summary overflowed (more near-tie keys than it carries) or the scan's spill
+// buffer did: every rank sees the same gathered flags and halts the same step; each
+// grows its summaries 8x (up to SUMMARY_KEYS_MAX) and, if its scan spilled past it, its
+// spill buffer; the caller re-allocates the exchange buffers (kb_engine_summary_bytes)
+// and runs the step again.  Past both limits it is a capacity error.
+static int grow_summary(kb_engine* e) {
+    HIPCHK(hipStreamSynchronize(e->st));
+    DevCtl c;
+    HIPCHK(hipMemcpy(&c, e->ctl, sizeof c, hipMemcpyDeviceToHost));
+    // (every rank grows its summaries alike -- the gathered layout needs one size; the
+    // spill buffer only where this rank's scan overflowed it)
+    bool grew = false;
+    if (c.cont_overflow && e->cont_cap < kContMax) {
+        const int rc = grow_spill(e);
+        if (rc != KB_OK) return rc;
+        HIPCHK(hipMemcpy(&c, e->ctl, sizeof c, hipMemcpyDeviceToHost));
+        grew = true;
+    }
+    if (e->sum_keys < SUMMARY_KEYS_MAX) {
+        e->sum_keys = std::min(SUMMARY_KEYS_MAX, 8 * e->sum_keys);
+        grew = true;
+    }
+    if (!grew) {
+        e->last_err = "engine capacity: more than " + std::to_string(SUMMARY_KEYS_MAX) +
+                      " near-tied candidates in one rank summary";
+        return KB_ERR_CAPACITY;
+    }
+    c.halted = H_RUN;
+    c.ncont = 0;
+    c.cont_overflow = 0;
+    HIPCHK(hipMemcpy(e->ctl, &c, sizeof c, hipMemcpyHostToDevice));
+    *e->h_ctl = c;
+    e->ctl_mirror = false;
+    return KB_GROW;
+}
 
 extern "C" int kb_engine_set_stream(kb_engine* e, void* s) {
     if (e) e->ctl_mirror = false;            // (the device block changes behind the host copy)
@@ -1229,7 +1268,7 @@ extern "C" int kb_engine_step_begin(kb_engine* e, void* summary_dev) {
     enqueue_scan(e);
     SumArgs s;
     s.ctl = e->ctl; s.R = scan_recs(e->recs, (int)e->nscan); s.cont = e->cont; s.cont_cap = e->cont_cap;
-    s.r = e->r; s.out = summary_recs((unsigned char*)summary_dev, 1);
+    s.r = e->r; s.out = summary_recs((unsigned char*)summary_dev, 1, e->sum_keys);
     launch_summary(s, e->st);
     HIPCHK(hipGetLastError());
     return KB_OK;
@@ -1253,7 +1292,7 @@ extern "C" int kb_engine_sharded_scan(kb_engine* e, void* summary_dev) {
     enqueue_scan(e);
     SumArgs s;
     s.ctl = e->ctl; s.R = scan_recs(e->recs, (int)e->nscan); s.cont = e->cont; s.cont_cap = e->cont_cap;
-    s.r = e->r; s.out = summary_recs((unsigned char*)summary_dev, 1);
+    s.r = e->r; s.out = summary_recs((unsigned char*)summary_dev, 1, e->sum_keys);
     launch_summary(s, e->st);
     HIPCHK(hipGetLastError());
     return KB_OK;
@@ -1263,7 +1302,7 @@ extern "C" int kb_engine_sharded_resolve(kb_engine* e, const void* gathered_dev,
     if (e) e->ctl_mirror = false;            // (the device block changes behind the host copy)
     if (!e || !gathered_dev || n_ranks < 1) return KB_ERR_INVALID;
     StepArgs a;
-    fill_step_args(e, a, summary_recs((unsigned char*)gathered_dev, n_ranks), 0);
+    fill_step_args(e, a, summary_recs((unsigned char*)gathered_dev, n_ranks, e->sum_keys), 0);
     launch_step(a, e->st);
     HIPCHK(hipGetLastError());
     return KB_OK;
@@ -1289,6 +1328,7 @@ extern "C" int kb_engine_sharded_collect(kb_engine* e, kb_change* out, int64_t c
     }
     *n_out = k;
     if (rc != KB_CHANGE) return rc;                   // no change / error: the plan ends
+    if (c.halted == H_NEED_SPILL) return grow_summary(e);   // bigger summaries, step again
     // exact loads needed (the resolve could not decide, or the load error grew):
     // every rank reaches the same verdict on the same state -- refold, then go on
     if (c.halted == H_NEED_EXACT || c.want_refresh) {
@@ -1303,7 +1343,7 @@ extern "C" int kb_engine_step_finish(kb_engine* e, const void* gathered_dev, int
     if (!e || !gathered_dev || n_ranks < 1 || !out) return KB_ERR_INVALID;
     if (e->pending) return pending_result(e, out);
     StepArgs a;
-    fill_step_args(e, a, summary_recs((unsigned char*)gathered_dev, n_ranks), 0);
+    fill_step_args(e, a, summary_recs((unsigned char*)gathered_dev, n_ranks, e->sum_keys), 0);
     launch_step(a, e->st);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(e->h_ctl, e->ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, e->st));
@@ -1317,6 +1357,12 @@ extern "C" int kb_engine_step_finish(kb_engine* e, const void* gathered_dev, int
         const int rc = convert(e, d, out);
         if (rc == KB_CHANGE && (c.halted == H_NEED_EXACT || c.want_refresh))
             if (refresh(e) != KB_OK) return KB_ERR_HIP;
+        return rc;
+    }
+    if (c.halted == H_NEED_SPILL) {                   // bigger summaries, then the step again
+        const int rc = grow_summary(e);
+        memset(out, 0, sizeof *out);
+        out->status = rc;
         return rc;
     }
     // the resolve could not certify its decision from the bounds: every rank reaches

@@ -23,7 +23,9 @@ constexpr uint32_t NONE32 = 0xFFFFFFFFu;
 constexpr unsigned long long NONE64 = ~0ull;
 constexpr uint16_t NONE16 = 0xFFFFu;
 constexpr int TILE_KEYS = 16;       // near-tie keys carried in a scan workgroup record
-constexpr int SUMMARY_KEYS = 1024;  // near-tie keys carried per rank in a summary
+constexpr int SUMMARY_KEYS = 56;    // near-tie keys per rank summary to start with (1936-B
+                                    // summaries); grown 8x (up to DEDUP_STEP) when one overflows
+constexpr int SUMMARY_KEYS_MAX = 2048;
 constexpr int DEDUP_STEP = 2048;    // LDS key table of k_step / k_summary
 constexpr int DEDUP_SCAN = 256;     // LDS key table of one k_scan workgroup
 constexpr int TMAX = 2 * MAXR + 4;  // brokers touched by one applied change (bound)
@@ -109,7 +111,9 @@ struct Recs {
 };
 constexpr int FIRST_BYTES = NF * 4;
 constexpr int WGREC_BYTES = (int)sizeof(RecHdr) + FIRST_BYTES + TILE_KEYS * (int)sizeof(Contender);
-constexpr int SUMMARY_BYTES = (int)sizeof(RecHdr) + FIRST_BYTES + SUMMARY_KEYS * (int)sizeof(Contender);
+__host__ __device__ constexpr int summary_bytes(int keys) {
+    return (int)sizeof(RecHdr) + FIRST_BYTES + keys * (int)sizeof(Contender);
+}
 inline Recs scan_recs(unsigned char* base, int nscan) {
     Recs r;
     r.hdr = base;
@@ -119,13 +123,13 @@ inline Recs scan_recs(unsigned char* base, int nscan) {
     r.n = nscan; r.cap = TILE_KEYS;
     return r;
 }
-inline Recs summary_recs(unsigned char* base, int n) {
+inline Recs summary_recs(unsigned char* base, int n, int keys) {
     Recs r;
     r.hdr = base;
     r.first = base + sizeof(RecHdr);
     r.keys = r.first + FIRST_BYTES;
-    r.hdr_stride = r.first_stride = r.key_stride = SUMMARY_BYTES;
-    r.n = n; r.cap = SUMMARY_KEYS;
+    r.hdr_stride = r.first_stride = r.key_stride = summary_bytes(keys);
+    r.n = n; r.cap = keys;
     return r;
 }
 

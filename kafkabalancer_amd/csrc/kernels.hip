@@ -1459,8 +1459,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
                         // and the step runs again (rank summaries: a capacity error)
                         const bool loose = a.use_spill && (C.ub[1] > s_g[1] || (a.allow_leader && C.ub[0] > s_g[0]));
                         if (loose) s_retry = 1;
-                        else if (a.use_spill) s_retry = 2;
-                        else { D.status = -1; D.step = step; D.err = E_CONT_OVERFLOW; s_done = 1; }
+                        else s_retry = 2;            // (rank summaries: the host grows them)
                     }
                 }
                 __syncthreads();
@@ -1608,9 +1607,8 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
 
         if (s_retry) {
             if (tid == 0 && s_retry == 2) {
-                C.halted = H_NEED_SPILL;                // the host grows the spill buffer
-                C.ncont = 0;
-                C.cont_overflow = 0;
+                C.halted = H_NEED_SPILL;                // the host grows the spill buffer (and
+                C.ncont = 0;                            // the rank summaries); it clears the flag
             } else if (tid == 0) {
                 if (C.ub[0] == -HUGE_VAL || C.ub[1] == -HUGE_VAL) {
                     // the scan pruned every wave: its minima are not the step's; open the
@@ -2681,12 +2679,12 @@ __global__ __launch_bounds__(1024) void k_summary(SumArgs a) {
         if (s_key[h] == NONE32) continue;
         const uint32_t k = atomicAdd(&s_n, 1u);
         atomicAdd(&s_nkk[s_key[h] >> 30], 1u);
-        if (k < (uint32_t)SUMMARY_KEYS) okeys[k] = dedup_entry(T, h);
+        if (k < (uint32_t)a.out.cap) okeys[k] = dedup_entry(T, h);
     }
     __syncthreads();
     if (tid == 0) {
-        out->nkeys = s_n < (uint32_t)SUMMARY_KEYS ? s_n : (uint32_t)SUMMARY_KEYS;
-        out->flags = ((ran && ctl->cont_overflow) || s_fail || s_n > (uint32_t)SUMMARY_KEYS) ? 1u : 0u;
+        out->nkeys = s_n < (uint32_t)a.out.cap ? s_n : (uint32_t)a.out.cap;
+        out->flags = ((ran && ctl->cont_overflow) || s_fail || s_n > (uint32_t)a.out.cap) ? 1u : 0u;
         if (ran) out->flags |= 2u;
         out->nkk[0] = (uint16_t)min(s_nkk[0], 0xFFFFu);
         out->nkk[1] = (uint16_t)min(s_nkk[1], 0xFFFFu);

@@ -37,15 +37,24 @@ class ShardedPlanner:
         self.world = world
         self.group = group
         self.staged = staged
-        nb = engine.summary_bytes()
-        dev = "cuda" if device_tensors else "cpu"
-        self.summary = torch.zeros(nb, dtype=torch.uint8, device=dev)
-        self.gathered = torch.zeros(world * nb, dtype=torch.uint8, device=dev)
+        self.dev = "cuda" if device_tensors else "cpu"
+        self._alloc()
+
+    def _alloc(self):
+        """Exchange buffers of the engine's current summary size (it grows when a rank
+        summary overflows: every rank sees the same flags and grows alike)."""
+        import torch
+        nb = self.engine.summary_bytes()
+        world = self.world
+        self.summary = torch.zeros(nb, dtype=torch.uint8, device=self.dev)
+        self.gathered = torch.zeros(world * nb, dtype=torch.uint8, device=self.dev)
         self.parts = list(self.gathered.chunk(world))
-        if staged:
+        if self.staged:
             self.h_summary = torch.zeros(nb, dtype=torch.uint8)
             self.h_gathered = torch.zeros(world * nb, dtype=torch.uint8)
             self.h_parts = list(self.h_gathered.chunk(world))
+        if self.dev == "cuda":
+            torch.cuda.synchronize()
 
     def step(self):
         import torch
@@ -64,7 +73,11 @@ class ShardedPlanner:
                 dist.all_gather(self.parts, self.summary, group=self.group)
             ch = self.engine.step_finish(self.gathered, self.world)
             # "retry": the bounds could not decide on approximate loads; every rank
-            # refolded its loads exactly and the step runs again
+            # refolded its loads exactly and the step runs again; "grow": a rank summary
+            # overflowed, the summaries grew and the step runs again
+            if isinstance(ch, str) and ch == "grow":
+                self._alloc()
+                continue
             if not (isinstance(ch, str) and ch == "retry"):
                 return ch
 
@@ -100,6 +113,8 @@ class ShardedPlanner:
             out.extend(changes)
             if status == "done":
                 break
+            if status == "grow":
+                self._alloc()
         return out[:steps]
 
 

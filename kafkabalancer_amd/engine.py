@@ -12,7 +12,7 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("KB_ENGINE_LIB") or os.path.join(_HERE, "lib", "libkbengine.so")
 
-KB_NOCHANGE, KB_CHANGE, KB_RETRY = 0, 1, 2
+KB_NOCHANGE, KB_CHANGE, KB_RETRY, KB_GROW = 0, 1, 2, 3
 KB_SEM_APPLIED, KB_SEM_GO = 0, 1
 ERRORS = {-1: "KB_ERR_INVALID", -2: "KB_ERR_HIP", -3: "KB_ERR_UNSUPPORTED", -4: "KB_ERR_STEP",
           -5: "KB_ERR_CAPACITY", -6: "KB_ERR_PANIC"}
@@ -123,7 +123,7 @@ def lib():
         if hasattr(L, "kb_engine_set_incremental"):
             L.kb_engine_set_incremental.argtypes = [vp, C.c_int32]
             L.kb_engine_set_incremental.restype = C.c_int
-        if L.kb_abi_version() != 6 and not any_abi:
+        if L.kb_abi_version() != 7 and not any_abi:
             raise ImportError("libkbengine.so ABI mismatch")
         _lib = L
     return _lib
@@ -396,6 +396,8 @@ class Engine:
             raise EngineError(rc, self.last_error(), changes[-1] if changes else None)
         if rc == KB_NOCHANGE:
             return "done", changes[:-1]
+        if rc == KB_GROW:
+            return "grow", changes                # summary_bytes() grew: new buffers, go on
         return ("retry" if rc == KB_RETRY else "ok"), changes
 
     def step_finish(self, gathered_ptr, n_ranks):
@@ -407,6 +409,8 @@ class Engine:
             return None
         if rc == KB_RETRY:
             return "retry"
+        if rc == KB_GROW:
+            return "grow"
         if rc == KB_CHANGE:
             return _change_dict(ch)
         raise EngineError(rc, self.last_error(), _change_dict(ch))

@@ -168,22 +168,29 @@ def test_two_engines_one_gpu_match_unsharded(workload):
     assert err is None
     world = 2
     engs = [E.Engine(cl, cfg, shard=shard_bounds(cl.n, world, r)) for r in range(world)]
-    nb = engs[0].summary_bytes()
-    bufs = [torch.zeros(nb, dtype=torch.uint8, device="cuda") for _ in range(world)]
-    got = []
-    for _ in range(30):
+    got, grows = [], 0
+    bufs = None
+    while len(got) < 30:
+        nb = engs[0].summary_bytes()                 # (grows when a summary overflows)
+        if bufs is None or bufs[0].numel() != nb:
+            bufs = [torch.zeros(nb, dtype=torch.uint8, device="cuda") for _ in range(world)]
+            torch.cuda.synchronize()
         for e, b in zip(engs, bufs):
             e.step_begin(b.data_ptr())
         torch.cuda.synchronize()
         gathered = torch.cat(bufs)
         chs = [e.step_finish(gathered.data_ptr(), world) for e in engs]
         assert chs[0] == chs[1]
+        if chs[0] in ("retry", "grow"):               # the same step again
+            grows += chs[0] == "grow"
+            continue
         if chs[0] is None:
             break
         got.append(chs[0])
     key = lambda c: (c["step"], c["pidx"], c["kind"], c["from_"], c["to"], c["slot"])
     assert [key(c) for c in got] == [key(c) for c in want]
     assert engs[0].state() == ref.state() == engs[1].state()
+
 
 
 @pytest.mark.gpu
@@ -199,10 +206,10 @@ def test_two_engines_one_gpu_batched_protocol():
     assert err is None
     world = 2
     engs = [E.Engine(cl, cfg, shard=shard_bounds(cl.n, world, r)) for r in range(world)]
-    nb = engs[0].summary_bytes()
     got = [[], []]
     done = False
     while not done and len(got[0]) < 40:
+        nb = engs[0].summary_bytes()
         batch = min(16, 40 - len(got[0]))
         for e in engs:
             e.sharded_reset(batch)
@@ -254,14 +261,14 @@ def test_sharded_protocol_matches_oracle(world):
     cl, cfg = _gpu_cluster()
     steps = 24
     engs = [E.Engine(cl, cfg, shard=shard_bounds(cl.n, world, r)) for r in range(world)]
-    nb = engs[0].summary_bytes()
-    summ = [torch.zeros(nb, dtype=torch.uint8, device="cuda") for _ in range(world)]
-    gathered = torch.zeros(world * nb, dtype=torch.uint8, device="cuda")
-    h_gathered = torch.zeros(world * nb, dtype=torch.uint8)
-    torch.cuda.synchronize()
     got = [[] for _ in range(world)]
     done = False
     while not done and len(got[0]) < steps:
+        nb = engs[0].summary_bytes()                 # (grows when a summary overflows)
+        summ = [torch.zeros(nb, dtype=torch.uint8, device="cuda") for _ in range(world)]
+        gathered = torch.zeros(world * nb, dtype=torch.uint8, device="cuda")
+        h_gathered = torch.zeros(world * nb, dtype=torch.uint8)
+        torch.cuda.synchronize()
         batch = min(8, steps - len(got[0]))
         for e in engs:
             e.sharded_reset(batch)
@@ -341,3 +348,52 @@ def test_gloo_two_ranks_gpu_engines_match_oracle():
     assert oerr is None
     assert res[0][0] == [(c["step"], c["pidx"], c["kind"], c["from_"], c["to"], c["slot"]) for c in och]
     assert res[0][1] == opl.state()
+
+
+@pytest.mark.gpu
+def test_sharded_summary_growth_matches_oracle():
+    """Exact ties over many broker pairs: more distinct near-tie keys than a 56-key
+    (1936-B) rank summary carries.  Every rank halts the step (KB_GROW), the summaries
+    grow 8x, the step runs again -- the oracle's plan, no capacity error."""
+    from kafkabalancer_amd import engine as E
+    from helpers import oracle_plan
+    # rings of RF2 partitions in three groups of 20 brokers (unit weights, leader 2,
+    # follower 1): every heavy broker carries 12k, every light one 6k, the rest 9k, so
+    # all 400 (heavy, light) moves tie; the ring set repeated 12 times (2160 partitions)
+    parts = []
+    for rep in range(12):
+        for g, rings in ((0, 4), (20, 2), (40, 3)):
+            for r in range(rings):
+                for i in range(20):
+                    parts.append({"topic": "t%d" % g, "partition": len(parts),
+                                  "replicas": [1 + g + i, 1 + g + (i + 1 + r) % 20]})
+    pl = {"version": 1, "partitions": parts}
+    cfg = default_cfg(min_unbalance=0.0)
+    world, steps = 2, 12
+    engs = [E.Engine(pl, cfg, shard=shard_bounds(len(parts), world, r)) for r in range(world)]
+    nb0 = engs[0].summary_bytes()
+    assert nb0 <= 2048
+    got, grows, bufs = [], 0, None
+    while len(got) < steps:
+        nb = engs[0].summary_bytes()
+        if bufs is None or bufs[0].numel() != nb:
+            bufs = [torch.zeros(nb, dtype=torch.uint8, device="cuda") for _ in range(world)]
+            torch.cuda.synchronize()
+        for e, b in zip(engs, bufs):
+            e.step_begin(b.data_ptr())
+        torch.cuda.synchronize()
+        gathered = torch.cat(bufs)
+        chs = [e.step_finish(gathered.data_ptr(), world) for e in engs]
+        assert chs[0] == chs[1]
+        if chs[0] in ("retry", "grow"):
+            grows += chs[0] == "grow"
+            continue
+        if chs[0] is None:
+            break
+        got.append(chs[0])
+    assert grows >= 1 and engs[0].summary_bytes() > nb0
+    och, oerr, opl = oracle_plan(pl, cfg, steps)
+    key = lambda c: (c["step"], c["pidx"], c["kind"], c["from_"], c["to"], c["slot"])
+    assert oerr is None
+    assert [key(c) for c in got] == [key(c) for c in och]
+    assert engs[0].state() == opl.state() == engs[1].state()
