@@ -560,6 +560,10 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
     HIPCHK(hipEventCreate(&e->ev0));
     HIPCHK(hipEventCreate(&e->ev1));
     e->scan_bytes = (e->shard_end - e->shard_begin) * (int64_t)(8 + 4 + 2 * e->rc_dev);
+    // thousands of brokers: a move rarely leaves a best key whose brokers it did not
+    // touch, so the next step's census bound is open; the conditional bound pass runs
+    // from the first step (else the second step's census spills once, ~1 s at c5)
+    e->ub_mode = e->B >= 2048;
     *out = e;
     return KB_OK;
 }
