@@ -163,35 +163,66 @@ __device__ double exact_unbalance_lds(const double* Lm, int n, int ps, int pt, d
 
 // The same folds run by one whole wave (every lane gets the result).  The lanes load
 // and compute 64 elements at a time in parallel (the 4096-broker case divides per term:
-// one lane doing all of them was issue-bound on the division sequences); the in-order
-// additions then run on the wave, element j read from lane j with readlane (SGPR
-// operand), one dependent add per element as in the reference.  Padding past n adds
-// +0.0, which leaves every fold here unchanged (all its terms and sums are >= +0).
-__device__ __forceinline__ double lane_val(double v, int j) {
-    const int hi = __builtin_amdgcn_readlane(__double2hiint(v), j);
-    const int lo = __builtin_amdgcn_readlane(__double2loint(v), j);
-    return __hiloint2double(hi, lo);
-}
-__device__ __forceinline__ double wave_fold64(double acc, double v) {
+// one lane doing all of them was issue-bound on the division sequences) into a
+// per-wave LDS row; then every lane runs the in-order additions itself over broadcast
+// 16-byte LDS reads, one dependent add per element as in the reference.  The chain is
+// bound by the f64 add latency: 11.3 cycles per element on gfx950 against 22 for
+// reading element j from lane j with readlane (tools/fold_bench.hip, 4096 elements:
+// 19.3 vs 37.4 us).  x must be 16-byte aligned.
+typedef __attribute__((address_space(3))) double lds_f64;
+typedef double f64x2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) f64x2 lds_f64x2;
+template <int D = 8>
+__device__ __forceinline__ double chain_lds(double acc, const lds_f64* x, int m) {
+    const lds_f64x2* x2 = (const lds_f64x2*)x;
+    int k = 0;
+    for (; k + 2 * D <= m; k += 2 * D) {
+        f64x2 v[D];
 #pragma unroll
-    for (int j = 0; j < 64; j++) acc += lane_val(v, j);
+        for (int j = 0; j < D; j++) v[j] = x2[(k >> 1) + j];
+#pragma unroll
+        for (int j = 0; j < D; j++) { acc += v[j].x; acc += v[j].y; }
+    }
+    for (; k < m; k++) acc += x[k];
     return acc;
 }
-// getUnbalanceBL of bl[] with bl[ps] = Ls, bl[pt] = Lt (ps / pt = -1: none)
-__device__ double exact_unbalance_wave(const double* Lm, int n, int ps, int pt, double Ls, double Lt) {
+// a wave's own LDS writes are seen by its later reads (LDS executes a wave's
+// operations in order); this keeps the compiler from moving them across
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+// getUnbalanceBL of bl[] with bl[ps] = Ls, bl[pt] = Lt (ps / pt = -1: none); Lm is
+// 16-byte aligned LDS, scr the calling wave's 64-double LDS row (wave-uniform call)
+// (not inlined: k_step's 128-VGPR budget spills with the unrolled chains inside it;
+// the pointers are cast to LDS so the call does not fall back to flat loads)
+__device__ __attribute__((noinline)) double exact_unbalance_wave(const double* Lm_, int n, int ps, int pt, double Ls, double Lt, double* scr_) {
+    const lds_f64* Lm = (const lds_f64*)Lm_;
+    lds_f64* scr = (lds_f64*)scr_;
     const int lane = threadIdx.x & 63;
     double S = 0.0;
     for (int k = 0; k < n; k += 64) {
-        const int i = k + lane;
-        const double v = i < n ? (i == ps ? Ls : (i == pt ? Lt : Lm[i])) : 0.0;
-        S = wave_fold64(S, v);
+        const int m = n - k < 64 ? n - k : 64;
+        if ((unsigned)(ps - k) < 64u || (unsigned)(pt - k) < 64u) {
+            const int i = k + lane;
+            if (lane < m) scr[lane] = i == ps ? Ls : (i == pt ? Lt : Lm[i]);
+            wave_lds_sync();
+            S = chain_lds(S, scr, m);
+            wave_lds_sync();
+        } else {
+            S = chain_lds(S, Lm + k, m);
+        }
     }
     const double avg = S / (double)n;
     double U = 0.0;
     for (int k = 0; k < n; k += 64) {
+        const int m = n - k < 64 ? n - k : 64;
         const int i = k + lane;
-        const double t = i < n ? term_x(i == ps ? Ls : (i == pt ? Lt : Lm[i]), avg) : 0.0;
-        U = wave_fold64(U, t);
+        if (lane < m) scr[lane] = term_x(i == ps ? Ls : (i == pt ? Lt : Lm[i]), avg);
+        wave_lds_sync();
+        U = chain_lds(U, scr, m);
+        wave_lds_sync();
     }
     return U;
 }
@@ -1039,6 +1070,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
     __shared__ int s_kc[2], s_sok[2];
     __shared__ Contender s_single[2];
     __shared__ double s_sux;
+    __shared__ __align__(16) double s_fold[NW * 64];   // per-wave rows of the exact folds
     __shared__ uint32_t s_key[DEDUP_STEP];
     __shared__ unsigned long long s_wb[DEDUP_STEP], s_it[DEDUP_STEP];
     extern __shared__ __align__(16) unsigned char dsm[];
@@ -1399,7 +1431,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
                 __syncthreads();
             };
             auto su_wave = [&]() {               // (wave 0, after stage_exact)
-                const double su = exact_unbalance_wave(s_Lm, nblm0, -1, -1, 0.0, 0.0);
+                const double su = exact_unbalance_wave(s_Lm, nblm0, -1, -1, 0.0, 0.0, s_fold);
                 if (lane == 0) { s_sux = su; atomicAdd(&C.total_folds, 1ull); }
             };
             auto exact_su = [&]() {
@@ -1514,7 +1546,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
                     if (!fail && ndist == 1) {
                         if (wid == 1) {
                             const double u = exact_unbalance_wave(s_Lm, nblm0, (int)ld32(a.posm + cw.s), (int)ld32(a.posm + cw.t),
-                                                                  s_ld[cw.s] - cw.w, s_ld[cw.t] + cw.w);
+                                                                  s_ld[cw.s] - cw.w, s_ld[cw.t] + cw.w, s_fold + 64);
                             if (lane == 0) { s_dv[0] = u; atomicAdd(&C.total_folds, 1ull); }
                         }
                         __syncthreads();
@@ -1538,7 +1570,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
                                     if (!(s_key[h] != NONE32 && (int)(s_key[h] >> 30) == kind)) continue;
                                     const Contender c = dedup_entry(T, h);
                                     const double u = exact_unbalance_wave(s_Lm, nblm0, (int)ld32(a.posm + c.s), (int)ld32(a.posm + c.t),
-                                                                          s_ld[c.s] - c.w, s_ld[c.t] + c.w);
+                                                                          s_ld[c.s] - c.w, s_ld[c.t] + c.w, s_fold + 64 * wid);
                                     if (lane == 0) nf++;
                                     better(u, c);
                                 }
@@ -2536,14 +2568,14 @@ constexpr int REFRESH_THREADS = 256;
 constexpr int REFRESH_CHUNK = 1024;
 // One workgroup per dirty broker: the exact getBrokerLoad fold (utils.go:92-105) of its
 // contributions in partition order.  Double-buffered: while wave 0 folds chunk j (a
-// wave fold: 64 contributions per load, one dependent add each), waves 1.. gather
+// broadcast-LDS chain, one dependent add each), waves 1.. gather
 // chunk j + 1 from the partition list.
 __global__ __launch_bounds__(REFRESH_THREADS) void k_refresh(RefreshArgs a) {
     const int b = blockIdx.x;
     if (b >= a.B || !(a.bfl[b] & BF_DIRTY)) return;
-    __shared__ double s_c[2][REFRESH_CHUNK];
+    __shared__ __align__(16) double s_c[2][REFRESH_CHUNK];
     const uint32_t st = a.L.lstart[b], n = a.L.llen[b];
-    const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
+    const int tid = threadIdx.x, wid = tid >> 6;
     auto gather = [&](uint32_t c0, double* dst, int t0, int nt) {
         const uint32_t m = n - c0 < (uint32_t)REFRESH_CHUNK ? n - c0 : (uint32_t)REFRESH_CHUNK;
         for (uint32_t i = (uint32_t)t0; i < m; i += (uint32_t)nt) {
@@ -2561,13 +2593,7 @@ __global__ __launch_bounds__(REFRESH_THREADS) void k_refresh(RefreshArgs a) {
         const uint32_t m = n - c0 < (uint32_t)REFRESH_CHUNK ? n - c0 : (uint32_t)REFRESH_CHUNK;
         if (wid > 0 && c0 + REFRESH_CHUNK < n)
             gather(c0 + REFRESH_CHUNK, s_c[(j + 1) & 1], tid - 64, REFRESH_THREADS - 64);
-        if (wid == 0) {
-            const double* x = s_c[j & 1];
-            for (uint32_t k = 0; k < m; k += 64) {
-                const uint32_t i = k + (uint32_t)lane;
-                acc = wave_fold64(acc, i < m ? x[i] : 0.0);   // (+0.0 padding: contributions >= 0)
-            }
-        }
+        if (wid == 0) acc = chain_lds(acc, (const lds_f64*)s_c[j & 1], (int)m);
         __syncthreads();
     }
     if (tid == 0) {
