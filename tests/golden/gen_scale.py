@@ -12,7 +12,14 @@ Each fixture stores the synth parameters, a SHA-256 of the generated input array
 (the GPU test regenerates the input and checks it first), the change list
 [step, pidx, kind, from, to, slot] and su / cu of every step as exact floats.
 
-Run:  python tests/golden/gen_scale.py [case ...]   (all cases: ~20 min on 8 cores)
+Full-size cases (`c3_full`, `c4_full`) regenerate BASELINE.json's headline configs
+themselves (kafkabalancer_amd/synth.config: c3 = 1M partitions x 1000 brokers, 256
+allowed sets of 64, Zipf weights, -allow-leader; c4 = 1M partitions, 1000 -> 1150
+allowed brokers with 50 decommissioned, 300 removes + 300 adds) and load them into the
+oracle as arrays (OraclePL.from_soa), not through the dict form.  `rl20k` pins
+distributeLeaders (steps.go:234-282, -rebalance-leader) at 20k partitions.
+
+Run:  python tests/golden/gen_scale.py [case ...]   (all cases: ~30 min on 8 cores)
 """
 import hashlib
 import json
@@ -57,10 +64,21 @@ CASES = {
                       dict(O.default_cfg(), min_unbalance=0.0), 12),
     "c4s": (dict(P=20000, B=200, rf=3, weights="zipf", seed=0x5EED1004, nr_seed=0x5EED1104),
             c4_cfg(), 1700),
+    # BASELINE.json configs[2] at full size: the first 20 steps of the bench workload
+    "c3_full": (dict(config="c3", scale=1.0), None, 20),
+    # BASELINE.json configs[3] at full size: the whole 1000-step plan (Remove, Add,
+    # Disallowed stages, steps.go:70-143)
+    "c4_full": (dict(config="c4", scale=1.0), None, 1000),
+    # -rebalance-leader (distributeLeaders, steps.go:234-282) with -allow-leader, 20k
+    # partitions, c3-shaped sets
+    "rl20k": (dict(P=20000, B=1000, rf=3, weights="zipf", nsets=256, set_size=64, seed=0x5EED3003),
+              dict(O.default_cfg(), allow_leader=True, rebalance_leaders=True, min_unbalance=0.0), 200),
 }
 
 
 def build(params):
+    if "config" in params:
+        return synth.config(params["config"], scale=params["scale"])[0]
     kw = dict(params)
     nr_seed = kw.pop("nr_seed", None)
     P = kw.pop("P")
@@ -79,11 +97,31 @@ def input_hash(cl):
     return h.hexdigest()
 
 
+def case_cfg(name):
+    params, cfg, _ = CASES[name]
+    if cfg is None:
+        cfg = synth.config(params["config"], scale=params["scale"])[1]
+    return cfg
+
+
+def oracle_pl(cl):
+    """Large clusters go into the oracle as arrays (the dict form of 1M partitions with
+    64-broker lists would need tens of GB of Python objects).  Weight / NumReplicas stay
+    raw: the oracle's FillDefaults (steps.go:39-66) fills them like the reference."""
+    if cl.n <= 100000:
+        return O.OraclePL(synth.to_plist(cl))
+    P = cl.n
+    return O.OraclePL.from_soa(b"t", np.zeros(P + 1, np.int64), np.arange(P, dtype=np.int64) % 100,
+                               cl.replica_ids, cl.replica_off, cl.weight, cl.num_replicas,
+                               cl.set_ids, cl.set_off, cl.set_idx, cl.num_consumers)
+
+
 def generate(name, threads):
-    params, cfg, steps = CASES[name]
+    params, _, steps = CASES[name]
+    cfg = case_cfg(name)
     cl = build(params)
     O.set_threads(threads)
-    o = O.OraclePL(synth.to_plist(cl))
+    o = oracle_pl(cl)
     changes, su, cu, err = [], [], [], None
     t0 = time.time()
     for k in range(steps):
