@@ -6,7 +6,14 @@
 //
 // Build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off (host folds must
 // round exactly like Go on amd64: no FMA contraction).
+#ifdef KB_ROCTX
 #include <rocprofiler-sdk-roctx/roctx.h>   // host ranges per plan phase (rocprofv3 --marker-trace)
+#else
+// production build: no profiler dependency (make roctx builds the instrumented library)
+#define roctxMark(msg) ((void)0)
+#define roctxRangePush(msg) ((void)0)
+#define roctxRangePop() ((void)0)
+#endif
 #include <hip/hip_runtime.h>
 #include <algorithm>
 #include <cfloat>
@@ -729,7 +736,7 @@ static int refresh(kb_engine* e) {
     HIPCHK(hipMemcpyAsync(e->h_ctl, e->ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, e->st));
     HIPCHK(hipStreamSynchronize(e->st));
     if (e->h_ctl->list_overflow) {
-        if (relist(e) != KB_OK) return KB_ERR_HIP;
+        if (const int rc = relist(e); rc != KB_OK) return rc;   // (a capacity limit stays one)
         DevCtl c = *e->h_ctl;
         c.list_overflow = 0;
         c.pending_list = 0;
@@ -763,7 +770,7 @@ static int reset_ctl(kb_engine* e, int64_t budget_steps) {
     e->ctl_mirror = false;
     DevCtl c = *e->h_ctl;
     if (c.halted == H_NEED_EXACT) {
-        if (refresh(e) != KB_OK) return KB_ERR_HIP;
+        if (const int rc = refresh(e); rc != KB_OK) return rc;
         c = *e->h_ctl;
         c.halted = H_RUN; c.prepped = 0; c.full_prep = 1; c.ndirty = 0; c.want_refresh = 0;
     }
@@ -888,7 +895,7 @@ static int run_steps(kb_engine* e, int64_t max_steps) {
         HIPCHK(hipHostMalloc((void**)&e->h_log, (size_t)e->logcap * sizeof(ChangeDev), hipHostMallocDefault));
         e->h_logcap = e->logcap;
     }
-    if (reset_ctl(e, max_steps) != KB_OK) return KB_ERR_HIP;
+    if (const int rc = reset_ctl(e, max_steps); rc != KB_OK) return rc;
     const int steps0 = e->h_ctl->steps;
     bool prepped = e->h_ctl->prepped != 0;
     bool fresh = false;                 // h_ctl holds the device block after the last batch
@@ -938,7 +945,7 @@ static int run_steps(kb_engine* e, int64_t max_steps) {
             continue;
         }
         if (c.halted == H_NEED_EXACT || (c.want_refresh && c.steps - steps0 < max_steps)) {
-            if (refresh(e) != KB_OK) return KB_ERR_HIP;
+            if (const int rc = refresh(e); rc != KB_OK) return rc;
             // refresh() cleared halted; the step log position is kept
             prepped = false;
             fresh = false;
@@ -1072,8 +1079,12 @@ extern "C" int kb_engine_stats(kb_engine* e, kb_stats* o) {
 extern "C" int kb_engine_set_incremental(kb_engine* e, int32_t on) {
     if (e) e->ctl_mirror = false;            // (the device block changes behind the host copy)
     if (!e) return KB_ERR_INVALID;
+    if (on && !e->lds_sets) {       // (the incremental scan kernel keeps the set records in LDS)
+        e->last_err = "incremental mode needs the allowed-set records in LDS (too many sets or brokers)";
+        return KB_ERR_UNSUPPORTED;
+    }
     HIPCHK(hipStreamSynchronize(e->st));
-    e->incr = on && e->lds_sets ? 1 : 0;           // (set records in LDS: the incremental scan kernel)
+    e->incr = on ? 1 : 0;
     DevCtl c;
     HIPCHK(hipMemcpy(&c, e->ctl, sizeof c, hipMemcpyDeviceToHost));
     c.incr_ok = 0;
@@ -1136,7 +1147,7 @@ extern "C" int kb_engine_bench_scan(kb_engine* e, int iters, double* avg_us) {
     if (e) e->ctl_mirror = false;            // (the device block changes behind the host copy)
     if (!e || iters < 1 || !avg_us) return KB_ERR_INVALID;
     if (e->pending) return e->pending;
-    if (reset_ctl(e, 1) != KB_OK) return KB_ERR_HIP;
+    if (const int rc = reset_ctl(e, 1); rc != KB_OK) return rc;
     if (!e->h_ctl->prepped) {
         enqueue_step(e);                              // prep only
         HIPCHK(hipStreamSynchronize(e->st));
@@ -1227,24 +1238,22 @@ static int grow_summary(kb_engine* e) {
     HIPCHK(hipStreamSynchronize(e->st));
     DevCtl c;
     HIPCHK(hipMemcpy(&c, e->ctl, sizeof c, hipMemcpyDeviceToHost));
-    // (every rank grows its summaries alike -- the gathered layout needs one size; the
-    // spill buffer only where this rank's scan overflowed it)
-    bool grew = false;
-    if (c.cont_overflow && e->cont_cap < kContMax) {
-        const int rc = grow_spill(e);
-        if (rc != KB_OK) return rc;
-        HIPCHK(hipMemcpy(&c, e->ctl, sizeof c, hipMemcpyDeviceToHost));
-        grew = true;
-    }
-    if (e->sum_keys < SUMMARY_KEYS_MAX) {
-        e->sum_keys = std::min(SUMMARY_KEYS_MAX, 8 * e->sum_keys);
-        grew = true;
-    }
-    if (!grew) {
+    // The decision depends only on state every rank shares (sum_keys, identical on all
+    // ranks): at the summary limit every rank returns the capacity error, whatever its
+    // own spill state, so no rank re-enters the collective alone.  Below it every rank
+    // grows its summaries alike (the gathered layout needs one size) and the spill
+    // buffer only where this rank's scan overflowed it.
+    if (e->sum_keys >= SUMMARY_KEYS_MAX) {
         e->last_err = "engine capacity: more than " + std::to_string(SUMMARY_KEYS_MAX) +
                       " near-tied candidates in one rank summary";
         return KB_ERR_CAPACITY;
     }
+    if (c.cont_overflow && e->cont_cap < kContMax) {
+        const int rc = grow_spill(e);
+        if (rc != KB_OK) return rc;
+        HIPCHK(hipMemcpy(&c, e->ctl, sizeof c, hipMemcpyDeviceToHost));
+    }
+    e->sum_keys = std::min(SUMMARY_KEYS_MAX, 8 * e->sum_keys);
     c.halted = H_RUN;
     c.ncont = 0;
     c.cont_overflow = 0;
@@ -1267,7 +1276,7 @@ extern "C" int kb_engine_step_begin(kb_engine* e, void* summary_dev) {
     if (e) e->ctl_mirror = false;            // (the device block changes behind the host copy)
     if (!e || !summary_dev) return KB_ERR_INVALID;
     if (e->pending) return e->pending;
-    if (reset_ctl(e, 1) != KB_OK) return KB_ERR_HIP;
+    if (const int rc = reset_ctl(e, 1); rc != KB_OK) return rc;
     if (!e->h_ctl->prepped) enqueue_step(e);       // prep only (nothing to resolve yet)
     enqueue_scan(e);
     SumArgs s;
@@ -1284,7 +1293,7 @@ extern "C" int kb_engine_sharded_reset(kb_engine* e, int64_t budget_steps) {
     if (e) e->ctl_mirror = false;            // (the device block changes behind the host copy)
     if (!e || budget_steps < 1) return KB_ERR_INVALID;
     if (e->pending) return e->pending;
-    if (reset_ctl(e, budget_steps) != KB_OK) return KB_ERR_HIP;
+    if (const int rc = reset_ctl(e, budget_steps); rc != KB_OK) return rc;
     if (!e->h_ctl->prepped) enqueue_step(e);       // prep only (nothing to resolve yet)
     HIPCHK(hipGetLastError());
     return KB_OK;
@@ -1336,7 +1345,7 @@ extern "C" int kb_engine_sharded_collect(kb_engine* e, kb_change* out, int64_t c
     // exact loads needed (the resolve could not decide, or the load error grew):
     // every rank reaches the same verdict on the same state -- refold, then go on
     if (c.halted == H_NEED_EXACT || c.want_refresh) {
-        if (refresh(e) != KB_OK) return KB_ERR_HIP;
+        if (const int rc = refresh(e); rc != KB_OK) return rc;
         return KB_RETRY;
     }
     return KB_CHANGE;
@@ -1360,7 +1369,7 @@ extern "C" int kb_engine_step_finish(kb_engine* e, const void* gathered_dev, int
         HIPCHK(hipMemcpy(&d, e->log, sizeof d, hipMemcpyDeviceToHost));
         const int rc = convert(e, d, out);
         if (rc == KB_CHANGE && (c.halted == H_NEED_EXACT || c.want_refresh))
-            if (refresh(e) != KB_OK) return KB_ERR_HIP;
+            if (const int rc = refresh(e); rc != KB_OK) return rc;
         return rc;
     }
     if (c.halted == H_NEED_SPILL) {                   // bigger summaries, then the step again
@@ -1371,7 +1380,7 @@ extern "C" int kb_engine_step_finish(kb_engine* e, const void* gathered_dev, int
     }
     // the resolve could not certify its decision from the bounds: every rank reaches
     // the same verdict on the same state -- refold, then redo the step
-    if (c.halted == H_NEED_EXACT && refresh(e) != KB_OK) return KB_ERR_HIP;
+    if (c.halted == H_NEED_EXACT) { if (const int rc = refresh(e); rc != KB_OK) return rc; }
     memset(out, 0, sizeof *out);
     out->status = KB_RETRY;
     return KB_RETRY;
