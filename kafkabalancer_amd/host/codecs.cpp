@@ -537,6 +537,94 @@ struct Fast {
             return false;
         }
     }
+    // the elements of the "partitions" array after its '[', through the closing ']'
+    bool partitions_seq(std::vector<Partition>& v) {
+        // (a reserve from the document size: partition objects are >= 16 bytes)
+        v.reserve(std::min<size_t>((size_t)(e - p) / 64 + 16, 1u << 26));
+        if (lit(']')) return true;
+        for (;;) {
+            v.emplace_back();
+            if (!partition(v.back())) return false;
+            if (lit(',')) continue;
+            if (lit(']')) return true;
+            return false;
+        }
+    }
+    // Large arrays are parsed by several threads, each from a split point: the first
+    // '{' after a "}<ws>,<ws>" found near an even share of the bytes.  A split point
+    // could lie inside a string, so every chunk but the last must end exactly at the
+    // next chunk's start: chunk 0 starts at a true element boundary, and a chunk that
+    // starts at one and parses its elements up to the next split point proves that
+    // point a boundary too (induction).  Anything else -- a chunk that overruns its
+    // end, meets the closing ']' early, or fails -- and the one-thread pass decides.
+    bool partitions_body(std::vector<Partition>& v) {
+        ws();
+        const size_t len = (size_t)(e - p);
+        unsigned nt = len < (8u << 20) ? 1u : std::thread::hardware_concurrency();
+        if (const char* x = getenv("KB_CODEC_THREADS")) nt = (unsigned)atoi(x);      // tests / benches
+        nt = (unsigned)std::max<size_t>(1, std::min<size_t>({(size_t)nt, 16, len / 4096 + 1}));
+        if (nt > 1 && partitions_par(v, nt)) return true;
+        v.clear();
+        return partitions_seq(v);
+    }
+    bool partitions_par(std::vector<Partition>& v, unsigned nt) {
+        const char* a0 = p;
+        std::vector<const char*> sp{a0};
+        for (unsigned k = 1; k < nt; k++) {
+            const char* q = std::max(sp.back() + 1, a0 + (size_t)(e - a0) * k / nt);
+            const char* hit = nullptr;
+            for (; q < e && !hit; q++) {
+                if (*q != '}') continue;
+                const char* r = q + 1;
+                while (r < e && (*r == ' ' || *r == '\t' || *r == '\n' || *r == '\r')) r++;
+                if (r >= e || *r != ',') continue;
+                r++;
+                while (r < e && (*r == ' ' || *r == '\t' || *r == '\n' || *r == '\r')) r++;
+                if (r < e && *r == '{') hit = r;
+            }
+            if (!hit) break;
+            sp.push_back(hit);
+        }
+        const unsigned nc = (unsigned)sp.size();
+        if (nc < 2) return false;
+        std::vector<std::vector<Partition>> part(nc);
+        std::vector<char> ok(nc, 0);
+        const char* tail = nullptr;                   // after the closing ']' (last chunk)
+        auto work = [&](unsigned k) {
+            Fast g{sp[k], e, {}};
+            std::vector<Partition>& out = part[k];
+            const bool last = k + 1 == nc;
+            out.reserve((size_t)((last ? e : sp[k + 1]) - sp[k]) / 64 + 16);
+            for (;;) {
+                out.emplace_back();
+                if (!g.partition(out.back())) return;
+                if (g.lit(',')) {
+                    if (last) continue;
+                    g.ws();
+                    if (g.p == sp[k + 1]) { ok[k] = 1; return; }
+                    if (g.p > sp[k + 1]) return;
+                    continue;
+                }
+                if (last && g.lit(']')) { tail = g.p; ok[k] = 1; }
+                return;
+            }
+        };
+        std::vector<std::thread> th;
+        for (unsigned k = 1; k < nc; k++) th.emplace_back(work, k);
+        work(0);
+        for (auto& t : th) t.join();
+        for (unsigned k = 0; k < nc; k++) if (!ok[k]) return false;
+        size_t tot = 0;
+        for (const auto& x : part) tot += x.size();
+        v.clear();
+        v.reserve(tot);
+        for (auto& x : part) {
+            for (auto& q : x) v.push_back(std::move(q));
+            std::vector<Partition>().swap(x);
+        }
+        p = tail;
+        return true;
+    }
     bool plist(PartitionList& pl) {
         if (!lit('{')) return false;
         if (lit('}')) return true;
@@ -552,17 +640,7 @@ struct Fast {
                     if (!lit('[')) return false;
                     pl.partitions.clear();
                     pl.nil_partitions = false;
-                    // (a reserve from the document size: partition objects are >= 16 bytes)
-                    pl.partitions.reserve(std::min<size_t>((size_t)(e - p) / 64 + 16, 1u << 26));
-                    if (!lit(']')) {
-                        for (;;) {
-                            pl.partitions.emplace_back();
-                            if (!partition(pl.partitions.back())) return false;
-                            if (lit(',')) continue;
-                            if (lit(']')) break;
-                            return false;
-                        }
-                    }
+                    if (!partitions_body(pl.partitions)) return false;
                 }
             } else return false;
             if (lit(',')) continue;

@@ -124,3 +124,28 @@ def test_float_formatting_matches_oracle():
     code, want, err = O.run_plan(O.OraclePL(pl), O.default_cfg(), max_reassign=0, full_output=True)
     assert rc == 0 and code == 0, err
     assert got == want
+
+
+@pytest.mark.parametrize("threads", ["2", "5", "16"])
+@pytest.mark.parametrize("trap", ["none", "some", "all"])
+def test_parallel_decode_matches_dom(threads, trap, monkeypatch):
+    """The partitions array split over threads (codecs.cpp partitions_par): split points
+    found inside topic strings that contain "},{" must not change the result -- the
+    chunk-boundary proof rejects them and the one-thread pass decides."""
+    monkeypatch.setenv("KB_CODEC_THREADS", threads)
+    pl = synthetic(3000, seed=11)
+    rng = random.Random(int(threads) * 7 + len(trap))
+    for p in pl["partitions"]:
+        if trap == "all" or (trap == "some" and rng.random() < 0.01):
+            p["topic"] = p["topic"] + "},{topic:x" + "}, {" * rng.randint(0, 2)
+    data = json.dumps(pl).encode()
+    assert same_as_dom(data) == 0
+    rc, got, *_ = cli.codec_roundtrip(data)
+    code, want, err = O.run_plan(O.OraclePL(pl), O.default_cfg(), max_reassign=0, full_output=True)
+    assert rc == 0 and code == 0 and got == want
+    # whitespace between elements and a truncated document
+    # (with traps the replacement also puts raw control bytes into topics: the DOM
+    # parser rejects those, and the fast path must give up and agree)
+    spaced = data.replace(b"}, {", b"} ,\n\t{")
+    assert same_as_dom(spaced) == (0 if trap == "none" else 2)
+    assert same_as_dom(data[: len(data) // 2]) != 0

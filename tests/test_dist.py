@@ -397,3 +397,115 @@ def test_sharded_summary_growth_matches_oracle():
     assert oerr is None
     assert [key(c) for c in got] == [key(c) for c in och]
     assert engs[0].state() == opl.state() == engs[1].state()
+
+
+def _tie_rings(group, reps, heavy_first=False):
+    """RF2 partitions in rings over three groups of `group` brokers (unit weights: the
+    leader carries 2, the follower 1): heavy brokers hold 12 per ring set, light ones 6,
+    the rest 9, so every (heavy, light) non-leader move ties exactly -- group**2
+    distinct near-tie keys.  heavy_first: every heavy-group partition comes first (in
+    the first shard), the light and middle groups after them."""
+    parts = []
+    blocks = {0: [], 1: [], 2: []}
+    for rep in range(reps):
+        for gi, (g, rings) in enumerate(((0, 4), (group, 2), (2 * group, 3))):
+            for r in range(rings):
+                for i in range(group):
+                    blocks[gi].append([1 + g + i, 1 + g + (i + 1 + r) % group])
+    order = blocks[0] + blocks[1] + blocks[2] if heavy_first else \
+        [x for rep in zip(blocks[0], blocks[1], blocks[2]) for x in rep]
+    for reps_ in order:
+        parts.append({"topic": "t", "partition": len(parts), "replicas": reps_})
+    return {"version": 1, "partitions": parts}
+
+
+@pytest.mark.gpu
+def test_sharded_summary_capacity_is_the_same_verdict_on_every_rank(monkeypatch):
+    """More than SUMMARY_KEYS_MAX (2048) exact-tied keys, all of them on the first shard,
+    whose scan spill buffer is also tiny (only that rank spills): the summaries grow
+    56 -> 448 -> 2048 keys on both ranks alike, then every rank returns the same
+    capacity error -- never one rank KB_GROW while the other errors (which would leave
+    the growing rank alone in the next collective)."""
+    from kafkabalancer_amd import engine as E
+    pl = _tie_rings(50, 3, heavy_first=True)          # 2500 (heavy, light) keys
+    cfg = default_cfg(min_unbalance=0.0)
+    world = 2
+    n = len(pl["partitions"])
+    monkeypatch.setenv("KB_CONT_CAP", "4")            # rank 0 only: its spill overflows
+    e0 = E.Engine(pl, cfg, shard=shard_bounds(n, world, 0))
+    monkeypatch.delenv("KB_CONT_CAP")
+    e1 = E.Engine(pl, cfg, shard=shard_bounds(n, world, 1))
+    engs = [e0, e1]
+    verdicts = []
+    for _ in range(12):
+        nb = engs[0].summary_bytes()
+        assert engs[1].summary_bytes() == nb
+        bufs = [torch.zeros(nb, dtype=torch.uint8, device="cuda") for _ in range(world)]
+        torch.cuda.synchronize()
+        for e, b in zip(engs, bufs):
+            e.step_begin(b.data_ptr())
+        torch.cuda.synchronize()
+        gathered = torch.cat(bufs)
+        out = []
+        for e in engs:
+            try:
+                out.append(e.step_finish(gathered.data_ptr(), world))
+            except E.EngineError as ex:
+                out.append(("error", ex.args[0] if ex.args else None))
+        verdicts.append(out)
+        assert out[0] == out[1] or (isinstance(out[0], tuple) and isinstance(out[1], tuple)), out
+        if isinstance(out[0], tuple) or out[0] not in ("grow", "retry"):
+            break
+    last = verdicts[-1]
+    assert isinstance(last[0], tuple) and isinstance(last[1], tuple), verdicts
+    assert sum(v[0] == "grow" for v in verdicts) == 2              # 56 -> 448 -> 2048 keys
+    for e in engs:
+        assert "near-tied candidates in one rank summary" in e.last_error()
+
+
+def _rccl_worker(steps, port, q):
+    """World size 1 over RCCL ("nccl"): the engine on torch's current stream (as
+    dist.bench_main sets it up), the batched protocol with all_gather_into_tensor on
+    device tensors (ShardedPlanner(staged=False)) -- the driver's multi-GPU path."""
+    try:
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        torch.cuda.set_device(0)
+        dist.init_process_group("nccl", rank=0, world_size=1)
+        from kafkabalancer_amd import engine as E
+        from kafkabalancer_amd.dist import _DeviceEngineAdapter
+        cl, cfg = _gpu_cluster()
+        eng = E.Engine(cl, cfg, shard=shard_bounds(cl.n, 1, 0))
+        eng.set_stream(torch.cuda.current_stream().cuda_stream)
+        sp = ShardedPlanner(_DeviceEngineAdapter(eng), 1, device_tensors=True, staged=False)
+        out = sp.plan(steps, batch=8)
+        out += [c for c in [sp.step()] if c is not None]       # the per-step protocol once
+        q.put(([(c["step"], c["pidx"], c["kind"], c["from_"], c["to"], c["slot"]) for c in out],
+               eng.state(), dist.get_backend(), None))
+        eng.close()
+        dist.destroy_process_group()
+    except Exception as ex:                        # reported to the parent, not swallowed
+        q.put((None, None, None, repr(ex)))
+
+
+@pytest.mark.gpu
+def test_rccl_world1_matches_oracle():
+    """The RCCL exchange path itself: one child process (started before it
+    touches the GPU) with init_process_group("nccl"), the engine on torch's stream and
+    all_gather_into_tensor between scan and resolve; the oracle's plan."""
+    from kafkabalancer_amd import synth
+    from helpers import oracle_plan
+    steps = 24
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_worker, args=(steps, _free_port(), q))
+    p.start()
+    ch, st, backend, err = q.get(timeout=240)
+    p.join(timeout=60)
+    assert err is None, err
+    assert backend == "nccl"
+    cl, cfg = _gpu_cluster()
+    och, oerr, opl = oracle_plan(synth.to_plist(cl), cfg, steps + 1)
+    assert oerr is None
+    assert ch == [(c["step"], c["pidx"], c["kind"], c["from_"], c["to"], c["slot"]) for c in och]
+    assert st == opl.state()

@@ -114,8 +114,9 @@ def test_engine_host_half_under_asan_ubsan(tmp_path):
         host_san += ["-Xarch_host", f]
     subprocess.run([hip] + common + host_san + ["-x", "hip", "-c", os.path.join(CSRC, "engine.cpp"), "-o", eobj],
                    check=True, capture_output=True)
-    subprocess.run([hip, "--offload-arch=gfx950", "-shared", "-fsanitize=address,undefined", "-o", lib, kobj, eobj],
-                   check=True, capture_output=True)
+    # (the host linker: the device code objects ride along in kernels.o's bundle)
+    subprocess.run(["g++", "-shared"] + SAN + ["-o", lib, kobj, eobj, "-L/opt/rocm/lib", "-lamdhip64",
+                    "-Wl,-rpath,/opt/rocm/lib"], check=True, capture_output=True)
     ubsan = subprocess.run(["gcc", "-print-file-name=libubsan.so"], capture_output=True, text=True).stdout.strip()
     pre = asan + (":" + ubsan if os.path.isabs(ubsan) else "")
     env = dict(os.environ, LD_PRELOAD=pre, PYTHONMALLOC="malloc", ASAN_OPTIONS="detect_leaks=0:abort_on_error=0",

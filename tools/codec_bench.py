@@ -1,8 +1,8 @@
 """Host codec throughput (codecs.go:15-27 / 84-93) on the c3 input:
 1M partitions x 1000 brokers, 64-broker allowed lists, Zipf weights, as JSON.
 
-Times the CLI's decode (one-pass decoder on one core; DOM fallback never taken on
-this input) and the Go-compatible encode of the whole list (contiguous slices on up
+Times the CLI's decode (one-pass decoder, the partitions array split over up to 16
+threads at chunk boundaries it proves; DOM fallback never taken on this input) and the Go-compatible encode of the whole list (contiguous slices on up
 to 16 threads), in MB/s of JSON;
 the DOM parser + decoder (the pre-fast-path implementation, a node per value) is
 timed on a 100k-partition slice for comparison.  Byte parity of the encoder with
@@ -73,7 +73,8 @@ def main():
         "dom_baseline": {"partitions": n_dom, "decode_mb_per_s": round(len(dom_data) / 1e6 / tp_dom, 1),
                          "one_pass_decode_mb_per_s_same_slice": round(len(dom_data) / 1e6 / tp_fast_slice, 1),
                          "note": "DOM parser + decoder (a node per JSON value), the pre-fast-path CLI"},
-        "decode_threads": 1,
+        "decode_threads": int(os.environ.get("KB_CODEC_THREADS", "0")) or
+                          (min(16, os.cpu_count() or 1) if len(data) >= (8 << 20) else 1),
         "encode_threads": int(os.environ.get("KB_CODEC_THREADS", "0")) or min(16, os.cpu_count() or 1),
         "cpu_model": cpu_model(), "nproc": os.cpu_count(), "reps": a.reps,
         "reference": "Go encoding/json is not buildable here (no Go toolchain); no reference timing",
