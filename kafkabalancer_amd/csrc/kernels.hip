@@ -1870,71 +1870,114 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
     if (!full) { if (tid == 0) C.prepped = 1; write_back(); return; }
 #endif
     const int nT = s_nT;
-    bool marked = false;                              // sets already marked (fused path)
+    bool marked = false;                              // (unused: the fused path returns itself)
     if (!full && a.sb_lds) {
-        // ---- fused incremental prep: the order-independent work (S, E, r, U0, eps, the
-        // upper bound, the set marks) rides along with the re-sort's phases, so the
-        // whole prep takes six barriers
-        const bool srt = nT > 0;
-        constexpr int NQ = (MAXB + STEP_THREADS - 1) / STEP_THREADS;
-        __shared__ double s_fq[2][NW], s_fq2[7][NW];     // F1 / F2 wave partials (distinct: no overwrite race)
-        __shared__ int s_fcnt[NW];
-        __shared__ int s_fwc[NW];
-        // F1: touched marks; S, E and |bl_move| partials; clears; best keys issued
-        if (srt && tid < nT) { s_fl[s_T[tid]] |= BF_TOUCHED; s_cntT[tid] = 0; }
-        for (int w = tid; w < (a.nsets + 31) / 32; w += STEP_THREADS) s_smark[w] = 0u;
-        __shared__ int s_nsub;
+        // ---- fused incremental prep, wave-specialised.  A wave reduction of a double
+        // costs ~340 clocks when all 16 waves run one (four per SIMD, issue-bound) and
+        // ~100 when one wave per SIMD does (tools/lat_probe.hip), while a workgroup
+        // barrier costs ~25: so the reductions run on the four "sum waves" (one per
+        // SIMD: S -> avg -> r -> U0 / V / Rm, the upper bound), the other twelve
+        // "order waves" re-sort the touched brokers and mark the sets meanwhile, and
+        // the phases are joined by barriers.  Four barriers, then the bl_move
+        // positions and the set records.
+        constexpr int NRW = 4;                          // sum waves (waves 0..3)
+        constexpr int OT = STEP_THREADS - NRW * 64;     // order-wave threads
+        constexpr int NQ = (MAXB + OT - 1) / OT;
+        const int ot = tid - NRW * 64;                  // order-wave thread index (< 0: sum wave)
+        __shared__ double s_fq[2][NRW], s_fq2[7][NW];
+        __shared__ int s_fcnt[NRW];
+        __shared__ int s_rt[MAXB / 64];                 // bl_move brokers per 64 universe positions
+        __shared__ int s_nsub, s_mn, s_mw;
+        // the marked sets in set order from word w0 on, at most MCAP of them (wave 1):
+        // the compact list of the record rebuild
+        constexpr int MCAP = 2 * DEDUP_STEP;
+        int* s_mlist = (int*)s_it;                      // (the key table is free after the resolve)
+        const int nwords = (a.nsets + 31) / 32;
+        auto compact = [&](int w0) {
+            int n = 0, w = w0;
+            while (w < nwords) {
+                const int ww = w + lane;
+                const uint32_t bits = ww < nwords ? s_smark[ww] : 0u;
+                const int c = __popc(bits);
+                const int incl = wave_incl_scan(c);
+                const bool fits = ww < nwords && n + incl <= MCAP;
+                const int nfit = (int)__popcll(__ballot(fits));   // a prefix of the lanes
+                if (fits) {
+                    int k = n + incl - c;
+                    for (uint32_t m = bits; m; m &= m - 1) s_mlist[k++] = ww * 32 + __ffs(m) - 1;
+                }
+                if (nfit > 0) n += __shfl(incl, nfit - 1);
+                w += nfit;
+                if (nfit < 64) break;
+            }
+            if (lane == 0) { s_mn = n; s_mw = w; }
+        };
+        // ---- P1.  sum waves: S, E, |bl_move| partials and the bl_move bits by broker id;
+        // order waves: old positions of the touched brokers, the sets holding one
+        if (tid < nT) { s_fl[s_T[tid]] |= BF_TOUCHED; s_cntT[tid] = 0; }
         if (tid == 0) { s_unc = 0; s_nsub = 0; }
-        // (the records' best keys came with their headers at the start: no round trip here)
-        const bool bkeys = do_res && tid < a.R.n;
-        const Contender& bk0 = hb0;
-        const Contender& bk1 = hb1;
-        {
+        if (wid < NRW) {
             double sS = 0.0, sE = 0.0;
             int cn = 0;
-            // (bl_move membership bits by broker id, one ballot per 64 brokers)
-            for (int b0 = 0; b0 < B; b0 += STEP_THREADS) {
-                const int b = b0 + tid;
+            for (int b0 = wid * 64; b0 < B; b0 += NRW * 64) {
+                const int b = b0 + lane;
                 const bool in = b < B && (s_fl[b] & (BF_PRESENT | BF_INCFG));
                 if (in) { sS += s_ld[b]; sE += s_e[b]; cn++; }
                 const unsigned long long m = __ballot(in);
-                if (lane == 0 && b0 + wid * 64 < B) s_blmb[(b0 >> 6) + wid] = m;
+                if (lane == 0) s_blmb[b0 >> 6] = m;
             }
             sS = wave_sum(sS); sE = wave_sum(sE); cn = wave_sum(cn);
             if (lane == 0) { s_fq[0][wid] = sS; s_fq[1][wid] = sE; s_fcnt[wid] = cn; }
-        }
-        __syncthreads();
-
-#if KB_ABL & 16
-        if (tid == 0) C.prepped = 1;                  // diagnostic timing build: stop here
-        write_back();
-        return;
-#endif
-        // F2: touched old positions; S, avg, r, U0/V/Rm partials; upper bound partials; set marks
-        if (srt)
-            for (int i = tid; i < B; i += STEP_THREADS) {
-                const int b = s_ord[i];
-                if (s_fl[b] & BF_TOUCHED)
+        } else {
+            if (nT > 0)
+                for (int i = ot; i < B; i += OT) {
+                    const int b = s_ord[i];
                     for (int x = 0; x < nT; x++) if (s_T[x] == b) s_posT[x] = i;
-            }
-        const double S = wave_sum(lane < NW ? s_fq[0][lane] : 0.0), E = wave_sum(lane < NW ? s_fq[1][lane] : 0.0);
-        const int nblm = wave_sum(lane < NW ? s_fcnt[lane] : 0);
-        const double avg = S / (double)nblm;
-        const double iav = 1.0 / avg;
-        {
-            double su = 0.0, v = 0.0, rm = 0.0, rlo = HUGE_VAL, rhi = -HUGE_VAL;
-            for (int b = tid; b < B; b += STEP_THREADS) {
-                double r = 0.0;
-                if (s_fl[b] & (BF_PRESENT | BF_INCFG)) {
-                    r = rel_ld(s_ld, b, iav);
-                    su += fsq(r);
-                    const double ar = fabs(r);
-                    v += ar * (1.0 + ar);
-                    rm = ar > rm ? ar : rm;
                 }
-                stdbl(a.r + b, r);
-                rlo = r < rlo ? r : rlo;                  // the scan's range of r[] (prune bound)
-                rhi = r > rhi ? r : rhi;
+            // a set is marked when it holds a touched broker: one lane per set, one
+            // ballot per 64 sets (no clear, no atomics)
+            for (int s0 = ot - lane; s0 < a.nsets; s0 += OT) {
+                const int set = s0 + lane;
+                bool hit = false;
+                if (set < a.nsets) {
+                    const uint64_t* sb = s_sb + (size_t)set * a.W64;
+                    for (int x = 0; x < nT; x++) {
+                        const int t = s_T[x];
+                        hit |= (sb[t >> 6] >> (t & 63)) & 1ull;
+                    }
+                }
+                const unsigned long long m = __ballot(hit);
+                if (lane == 0) { s_smark[s0 >> 5] = (uint32_t)m; s_smark[(s0 >> 5) + 1] = (uint32_t)(m >> 32); }
+            }
+        }
+        __syncthreads();                                // #1
+        KB_STAMP(ctl, 6);
+        // ---- P2.  sum waves (and any wave holding a record's best keys): avg, r, U0 /
+        // V / Rm partials, the upper bound; order waves: the new positions
+        const bool bkeys = do_res && tid < a.R.n;
+        int nb[NQ], np[NQ];
+        if (wid < NRW || wid * 64 < (do_res ? a.R.n : 0)) {
+            // (the same fixed-order combination on every such wave: identical bits)
+            const double S = ((s_fq[0][0] + s_fq[0][1]) + s_fq[0][2]) + s_fq[0][3];
+            const int nblm = (s_fcnt[0] + s_fcnt[1]) + (s_fcnt[2] + s_fcnt[3]);
+            const double avg = S / (double)nblm;
+            const double iav = 1.0 / avg;
+            double su = 0.0, v = 0.0, rm = 0.0, rlo = HUGE_VAL, rhi = -HUGE_VAL;
+            if (wid < NRW) {
+#pragma unroll 4
+                for (int b = wid * 64 + lane; b < B; b += NRW * 64) {
+                    double r = 0.0;
+                    if (s_fl[b] & (BF_PRESENT | BF_INCFG)) {
+                        r = rel_ld(s_ld, b, iav);
+                        su += fsq(r);
+                        const double ar = fabs(r);
+                        v += ar * (1.0 + ar);
+                        rm = ar > rm ? ar : rm;
+                    }
+                    stdbl(a.r + b, r);
+                    rlo = r < rlo ? r : rlo;            // the scan's range of r[] (prune bound)
+                    rhi = r > rhi ? r : rhi;
+                }
             }
             // upper bound of the next step's minimum per kind: the best keys of the scan
             // just resolved whose partition and brokers the applied move did not touch
@@ -1944,7 +1987,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
                 const long long pm = s_moved;
 #pragma unroll
                 for (int k = 0; k < 2; k++) {
-                    const Contender& c = k ? bk1 : bk0;
+                    const Contender& c = k ? hb1 : hb0;
                     // the block of every best key other than the moved partition's: if no
                     // key survives below, the conditional bound pass scans only these blocks
                     // and the heaviest blocks by weight (engine.cpp fills that part once):
@@ -1965,39 +2008,30 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
                     else ub1 = d2 < ub1 ? d2 : ub1;
                 }
             }
-            su = wave_sum(su); v = wave_sum(v); rm = wave_max(rm);
             ub0 = wave_min(ub0); ub1 = wave_min(ub1);
-            if (a.incr) { rlo = wave_min(rlo); rhi = wave_max(rhi); }
+            if (wid < NRW) {
+                su = wave_sum(su); v = wave_sum(v); rm = wave_max(rm);
+                if (a.incr) { rlo = wave_min(rlo); rhi = wave_max(rhi); }
+            }
             if (lane == 0) {
-                s_fq2[0][wid] = su; s_fq2[1][wid] = v; s_fq2[2][wid] = rm; s_fq2[3][wid] = ub0; s_fq2[4][wid] = ub1;
-                s_fq2[5][wid] = rlo; s_fq2[6][wid] = rhi;
+                s_fq2[3][wid] = ub0; s_fq2[4][wid] = ub1;
+                if (wid < NRW) {
+                    s_fq2[0][wid] = su; s_fq2[1][wid] = v; s_fq2[2][wid] = rm;
+                    s_fq2[5][wid] = rlo; s_fq2[6][wid] = rhi;
+                }
             }
+        } else if (lane == 0) {
+            s_fq2[3][wid] = HUGE_VAL; s_fq2[4][wid] = HUGE_VAL;
         }
-        for (int set = tid; set < a.nsets; set += STEP_THREADS) {
-            // a set is marked when it holds a touched broker
-            const uint64_t* sb = s_sb + (size_t)set * a.W64;
-            bool hit = false;
-            for (int x = 0; x < nT; x++) {
-                const int t = s_T[x];
-                hit |= (sb[t >> 6] >> (t & 63)) & 1ull;
-            }
-            if (hit) atomicOr(&s_smark[set >> 5], 1u << (set & 31));
-        }
-        __syncthreads();
-        KB_STAMP(ctl, 6);
-#if KB_ABL & 8
-        if (tid == 0) C.prepped = 1;                  // diagnostic timing build: stop here
-        write_back();
-        return;
-#endif
-        // F3: new positions of the untouched brokers; eps and the control block (wave 0)
-        int nb[NQ], np[NQ];
-        if (srt) {
+        if (ot >= 0 && nT > 0) {
+            // per untouched element: new position = old - (touched before it) + (touched
+            // keys below it); for every touched broker the untouched brokers below it
 #pragma unroll
             for (int q = 0; q < NQ; q++) {
                 nb[q] = -1;
-                if (q * STEP_THREADS >= B) continue;         // uniform
-                const int i = q * STEP_THREADS + tid;
+                np[q] = 0;
+                if (q * OT >= B) continue;                  // uniform
+                const int i = q * OT + ot;
                 const bool in = i < B;
                 const int b = in ? s_ord[i] : 0;
                 const bool untouched = in && !(s_fl[b] & BF_TOUCHED);
@@ -2008,7 +2042,6 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
                     const double Lt = s_ld[t];
                     below += ((Lt < Lb) || (Lt == Lb && t < b)) ? 1 : 0;
                     before += s_posT[x] < i ? 1 : 0;
-                    // count, for touched t, the untouched brokers below it
                     const bool b_lt_t = untouched && ((Lb < Lt) || (Lb == Lt && b < t));
                     const unsigned long long bal = __ballot(b_lt_t);
                     if (lane == 0 && bal) atomicAdd(&s_cntT[x], (int)__popcll(bal));
@@ -2017,22 +2050,16 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
                 np[q] = i - before + below;
             }
         }
-        // the step totals: one wave per partial array (the combination waits for F4)
-        __shared__ double s_red[7];
-        if (wid < (a.incr ? 7 : 5)) {
-            const bool in = lane < NW;
-            const double x = in ? s_fq2[wid][lane] : (wid == 2 || wid == 6) ? -HUGE_VAL : (wid == 0 || wid == 1) ? 0.0 : HUGE_VAL;
-            const double y = (wid == 0 || wid == 1) ? wave_sum(x) : (wid == 2 || wid == 6) ? wave_max(x) : wave_min(x);
-            if (lane == 0) s_red[wid] = y;
-        }
-        __syncthreads();
-        // F4: scatter into the new order
-        if (srt) {
+        __syncthreads();                                // #2
+        KB_STAMP(ctl, 8);
+        // ---- P3.  order waves: scatter into the new order; wave 0: the step totals,
+        // eps and the control block; wave 1: the list of marked sets
+        if (ot >= 0 && nT > 0) {
 #pragma unroll
             for (int q = 0; q < NQ; q++)
-                if (q * STEP_THREADS < B && nb[q] >= 0) s_ord[np[q]] = nb[q];
-            if (tid < nT) {
-                const int t = s_T[tid];
+                if (q * OT < B && nb[q] >= 0) s_ord[np[q]] = nb[q];
+            if (ot < nT) {
+                const int t = s_T[ot];
                 const double Lt = s_ld[t];
                 int rank = 0;
                 for (int x = 0; x < nT; x++) {
@@ -2040,11 +2067,20 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
                     const double L2 = s_ld[t2];
                     rank += ((L2 < Lt) || (L2 == Lt && t2 < t)) ? 1 : 0;
                 }
-                s_ord[s_cntT[tid] + rank] = t;
+                s_ord[s_cntT[ot] + rank] = t;
             }
         }
         if (wid == 0) {
-            const double U0 = s_red[0], V = s_red[1], Rm = s_red[2], ub0 = s_red[3], ub1 = s_red[4];
+            const double S = ((s_fq[0][0] + s_fq[0][1]) + s_fq[0][2]) + s_fq[0][3];
+            const double E = ((s_fq[1][0] + s_fq[1][1]) + s_fq[1][2]) + s_fq[1][3];
+            const int nblm = (s_fcnt[0] + s_fcnt[1]) + (s_fcnt[2] + s_fcnt[3]);
+            const double avg = S / (double)nblm;
+            const double iav = 1.0 / avg;
+            const double U0 = ((s_fq2[0][0] + s_fq2[0][1]) + s_fq2[0][2]) + s_fq2[0][3];
+            const double V = ((s_fq2[1][0] + s_fq2[1][1]) + s_fq2[1][2]) + s_fq2[1][3];
+            const double Rm = fmax(fmax(s_fq2[2][0], s_fq2[2][1]), fmax(s_fq2[2][2], s_fq2[2][3]));
+            const double ub0 = wave_min(lane < NW ? s_fq2[3][lane] : HUGE_VAL);
+            const double ub1 = wave_min(lane < NW ? s_fq2[4][lane] : HUGE_VAL);
             // (every lane: the incremental certificate below needs eps on the whole wave)
             const double u = DBL_EPSILON / 2;
             const double n = (double)nblm;
@@ -2060,8 +2096,10 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
             const bool inc = a.incr && do_res && D.status == 1 && D.kind == 1 && (D.step == 7 || D.step == 8) &&
                              nblm == nblm0 && !s_fm && !a.rebalance && !a.sem_go && a.use_spill;
             if (inc) {
+                const double rlo = fmin(fmin(s_fq2[5][0], s_fq2[5][1]), fmin(s_fq2[5][2], s_fq2[5][3]));
+                const double rhi = fmax(fmax(s_fq2[6][0], s_fq2[6][1]), fmax(s_fq2[6][2], s_fq2[6][3]));
                 const double ubP = a.allow_leader ? (ub0 > ub1 ? ub0 : ub1) : ub1;
-                ws = incr_wskip(s_red[5], s_red[6], ubP + 16.0 * ep, avg, iav, lane);
+                ws = incr_wskip(rlo, rhi, ubP + 16.0 * ep, avg, iav, lane);
             }
             if (lane == 0) {
                 C.incr_ok = ws > 0.0 ? 1 : 0;
@@ -2077,28 +2115,28 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
                 C.ncont = 0;
                 C.cont_overflow = 0;
             }
+        } else if (wid == 1) {
+            compact(0);
         }
-        __syncthreads();
-        KB_STAMP(ctl, 8);
-#if KB_ABL & 4
-        if (tid == 0) C.prepped = 1;                  // diagnostic timing build: stop here
-        write_back();
-        return;
-#endif
-        // F5: bl_move = brokers present in the load map or listed in -broker-ids
-        // (steps.go:150-157): membership bits, order / position writes, order certification
-        constexpr int PT = MAXB / STEP_THREADS;          // universe positions per thread
-        int flag[PT], c = 0;
-        const int base = tid * PT;
+        __syncthreads();                                // #3
+        KB_STAMP(ctl, 9);
+        // ---- P4.  bl_move = brokers present in the load map or listed in -broker-ids
+        // (steps.go:150-157), interleaved (position i = q * STEP_THREADS + tid): order
+        // and position writes, order certification, bl_move counts per 64 positions
+        constexpr int PQ = (MAXB + STEP_THREADS - 1) / STEP_THREADS;
+        int pb[PQ];
+        unsigned long long pm[PQ];
+        const unsigned long long lt = (1ull << lane) - 1ull;
 #pragma unroll
-        for (int q = 0; q < PT; q++) {
-            const int i = base + q;
-            flag[q] = 0;
+        for (int q = 0; q < PQ; q++) {
+            pb[q] = -1; pm[q] = 0;
+            if (q * STEP_THREADS >= B) continue;         // uniform
+            const int i = q * STEP_THREADS + tid;
+            bool f = false;
             if (i < B) {
                 const int b = s_ord[i];
-                const uint8_t fl = s_fl[b];
-                flag[q] = (fl & (BF_PRESENT | BF_INCFG)) ? 1 : 0;
-                c += flag[q];
+                pb[q] = b;
+                f = (s_fl[b] & (BF_PRESENT | BF_INCFG)) != 0;
                 a.order[i] = b;
                 a.posu[b] = i;
                 // with approximate loads, neighbours must be separated by more than
@@ -2109,35 +2147,114 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
                     if (e > 0.0 && !(s_ld[b2] - s_ld[b] > e)) s_unc = 1;
                 }
             }
+            pm[q] = __ballot(f);
+            if (lane == 0 && (i >> 6) < MAXB / 64) s_rt[i >> 6] = (int)__popcll(pm[q]);
         }
-        const int incl = wave_incl_scan(c);
-        if (lane == 63) s_fwc[wid] = incl;
-        __syncthreads();
-        // F6: bl_move positions; getBL's lightest / heaviest
-        {
-            const int wc = lane < NW ? s_fwc[lane] : 0;
-            const int woff = wave_sum(lane < wid ? wc : 0);
-            int pos = woff + incl - c;
-#pragma unroll
-            for (int q = 0; q < PT; q++) {
-                const int i = base + q;
-                if (i < B) {
-                    const int b = s_ord[i];
-                    if (flag[q]) {
-                        if (pos == 0) C.light = b;
-                        if (pos == nblm - 1) C.heavy = b;
-                        st32(a.blm + pos, (uint32_t)b); st32(a.posm + b, (uint32_t)pos); pos++;
-                    } else st32(a.posm + b, NONE32);
-                }
-            }
-            if (tid == 0 && nblm == 0) { C.light = -1; C.heavy = -1; }
-        }
+        __syncthreads();                                // #4
+        KB_STAMP(ctl, 16);
         if (s_unc) {
             if (tid == 0) { C.halted = H_NEED_EXACT; C.prepped = 0; C.total_exact_halts++; }
             write_back();
             return;
         }
-        marked = true;
+        // positions: the bl_move brokers before each 64-position row (lane-parallel prefix)
+        {
+            const int nrows = (B + 63) >> 6;
+            const int rc = lane < nrows ? s_rt[lane] : 0;
+            const int rincl = wave_incl_scan(rc);
+            const int nblm = __builtin_amdgcn_readlane(rincl, 63);
+            const int widu = __builtin_amdgcn_readfirstlane(wid);
+#pragma unroll
+            for (int q = 0; q < PQ; q++) {
+                if (q * STEP_THREADS >= B) continue;     // uniform
+                // exclusive prefix of this wave's row (rows are wave-uniform)
+                const int off = __builtin_amdgcn_readlane(rincl - rc, q * NW + widu);
+                if (pb[q] < 0) continue;
+                const int b = pb[q];
+                if ((pm[q] >> lane) & 1ull) {
+                    const int pos = off + (int)__popcll(pm[q] & lt);
+                    if (pos == 0) C.light = b;
+                    if (pos == nblm - 1) C.heavy = b;
+                    st32(a.blm + pos, (uint32_t)b); st32(a.posm + b, (uint32_t)pos);
+                } else st32(a.posm + b, NONE32);
+            }
+            if (tid == 0 && nblm == 0) { C.light = -1; C.heavy = -1; }
+        }
+        KB_STAMP(ctl, 19);
+        // ---- P5.  set records of the marked sets (steps.go:192-201 targets): each wave
+        // rebuilds G records at a time so their LDS chains overlap
+        for (;;) {
+            constexpr int G = 4;
+            const int W64 = a.W64, KR = a.KR;
+            const int mn = s_mn;
+            constexpr int MAXU = sr_units(MAXR);
+            __shared__ __align__(16) uint16_t s_rs2[NW][G][8 * MAXU];
+            for (int g = wid * G; g < mn; g += NW * G) {
+                const int ng = mn - g < G ? mn - g : G;
+                const uint64_t* sb[G];
+                uint16_t* rec16[G];
+                int found[G];
+#pragma unroll
+                for (int j = 0; j < G; j++) {
+                    const int jj = j < ng ? j : 0;
+                    sb[j] = s_sb + (size_t)s_mlist[g + jj] * W64;
+                    rec16[j] = &s_rs2[wid][j][0];
+                    found[j] = j < ng ? 0 : KR;
+                }
+                for (int base = 0; base < B; base += 64) {
+                    bool need = false;
+#pragma unroll
+                    for (int j = 0; j < G; j++) need |= found[j] < KR;
+                    if (!need) break;
+                    const int k = base + lane;
+                    const int b = s_ord[k < B ? k : 0];
+                    const bool inb = k < B && ((s_blmb[b >> 6] >> (b & 63)) & 1ull);
+                    uint64_t wj[G];
+#pragma unroll
+                    for (int j = 0; j < G; j++) wj[j] = sb[j][b >> 6];
+#pragma unroll
+                    for (int j = 0; j < G; j++) {
+                        const bool mem = inb && ((wj[j] >> (b & 63)) & 1ull);
+                        const unsigned long long m = __ballot(mem);
+                        if (mem && found[j] < KR) {
+                            const int rk = found[j] + (int)__popcll(m & lt);
+                            if (rk < KR) rec16[j][2 + rk] = (uint16_t)b;
+                        }
+                        found[j] += (int)__popcll(m);
+                    }
+                }
+                int nj[G];
+#pragma unroll
+                for (int j = 0; j < G; j++) nj[j] = lane < W64 ? (int)__popcll(sb[j][lane] & s_blmb[lane]) : 0;
+#pragma unroll
+                for (int j = 0; j < G; j++) nj[j] = wave_sum(nj[j]);
+#pragma unroll
+                for (int j = 0; j < G; j++) {
+                    if (j >= ng) break;
+                    for (int rk = found[j] + lane; rk < KR; rk += 64) rec16[j][2 + rk] = NONE16;
+                    if (lane == 0) {
+                        rec16[j][1] = (uint16_t)(found[j] < KR ? found[j] : KR);
+                        rec16[j][0] = (uint16_t)nj[j];
+                    }
+                }
+                __builtin_amdgcn_wave_barrier();
+                if (lane < ng * a.units) {
+                    const int j = lane / a.units, u = lane - j * a.units;
+                    stobj(a.setrec + (size_t)s_mlist[g + j] * a.units + u, *(const uint4*)&s_rs2[wid][j][8 * u]);
+                }
+                __builtin_amdgcn_wave_barrier();
+            }
+            // (more marked sets than one list holds: the next chunk)
+            const int mw = s_mw;
+            if (mw >= nwords) break;
+            __syncthreads();
+            if (wid == 1) compact(mw);
+            __syncthreads();
+        }
+        KB_STAMP(ctl, 20);
+        if (tid == 0) { C.prepped = 1; C.full_prep = 0; }
+        write_back();
+        return;
     } else {
     if (full) {
         // every load is exact here (fresh state or after k_refresh): s_e holds the sort keys
