@@ -80,7 +80,10 @@ def cpu_baseline(cl, cfg, seconds=12.0):
     try:
         sys.path.insert(0, os.path.join(ROOT, "tools", "cpu_engine"))
         import cpu_engine
-        threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+        # every core this process may run on (OpenMP on all host cores);
+        # OMP_NUM_THREADS, when set (16 on the GPU pool's boxes), is the box's share
+        avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+        threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or avail
         ce = cpu_engine.CpuEngine(cl, cfg, threads=threads)
         c0 = ce.candidates()
         t0 = time.perf_counter()
@@ -92,6 +95,8 @@ def cpu_baseline(cl, cfg, seconds=12.0):
         dt = time.perf_counter() - t0
         out["optimised_cpu"] = {"value": (ce.candidates() - c0) / dt, "unit": "candidates/s",
                                 "ms_per_step": 1e3 * dt / max(steps, 1), "cores": threads, "steps": steps,
+                                "cores_available": avail,
+                                "cores_source": "OMP_NUM_THREADS" if os.environ.get("OMP_NUM_THREADS") else "affinity",
                                 "kind": "engine algorithm on the host (tools/cpu_engine, OpenMP)"}
         ce.close()
     except (ImportError, OSError, ValueError) as ex:
@@ -132,6 +137,71 @@ def bytes_8d(cl, changes, nsets, B, rmax, full_steps):
     return total
 
 
+def drop_in(args):
+    """What a drop-in user pays at the workload: one line, not the headline.
+    (a) kb_engine_balance per call -- the cgo shim's path, one Balance() =
+    one enqueue + one synchronisation -- against the device-resident plan's per-step time;
+    (b) the C++ CLI end to end on the workload's reassignment JSON (kafkabalancer.go:181-235):
+    read, decode (codecs.go:15-27), kb_engine_create, the -max-reassign plan, encode
+    (codecs.go:84-93), from its KB_CLI_TIMINGS phase stamps and the process wall time."""
+    import subprocess
+    import tempfile
+    import torch
+    from kafkabalancer_amd import engine as E
+    from kafkabalancer_amd import synth
+    torch.cuda.set_device(0)
+    cl, cfg, desc = synth.config(args.workload, scale=args.scale)
+    eng = E.Engine(cl, cfg, device=0)
+    for _ in range(5):
+        assert eng.balance() is not None
+    n = args.steps
+    t0 = time.perf_counter()
+    for _ in range(n):
+        if eng.balance() is None:
+            break
+    per_call = (time.perf_counter() - t0) / n
+    t0 = time.perf_counter()
+    buf, k, rc = eng.plan_raw(n)
+    plan_step = (time.perf_counter() - t0) / max(k, 1)
+    eng.close()
+    out = {"metric": "drop-in cost (%s)" % args.workload, "unit": "us",
+           "balance_per_call_us": 1e6 * per_call, "plan_per_step_us": 1e6 * plan_step, "calls": n,
+           "balance_def": "kb_engine_balance via ctypes, one Balance() per call (enqueue + sync), after 5 warm calls"}
+    # the CLI on the same cluster as reassignment JSON
+    cli_bin = os.path.join(ROOT, "kafkabalancer_amd", "lib", "kafkabalancer")
+    tmp = tempfile.mkdtemp(prefix="kbdrop")
+    jpath, tpath = os.path.join(tmp, "in.json"), os.path.join(tmp, "t.json")
+    try:
+        t0 = time.perf_counter()
+        cl.topics = None
+        with open(jpath, "wb") as f:
+            f.write(json.dumps(synth.to_plist(cl), separators=(",", ":")).encode())
+        gen_s = time.perf_counter() - t0
+        cmd = [cli_bin, "-input-json", "-input", jpath, "-max-reassign", str(args.cli_reassign)]
+        if cfg.get("allow_leader"):
+            cmd.append("-allow-leader")
+        cmd += ["-min-unbalance", repr(float(cfg.get("min_unbalance", 0.01)))]
+        env = dict(os.environ, KB_CLI_TIMINGS=tpath)
+        t0 = time.perf_counter()
+        r = subprocess.run(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=600)
+        wall = time.perf_counter() - t0
+        assert r.returncode == 0, r.stderr[-2000:]
+        with open(tpath) as f:
+            ph = json.loads(f.readline())
+        out["cli"] = dict(ph, wall_s=wall, cmd=" ".join(os.path.basename(c) if c == cli_bin else c for c in cmd[:1]) +
+                          " " + " ".join(cmd[1:2] + ["-input", "<%.0f MB JSON>" % (ph["input_bytes"] / 1e6)] + cmd[4:]),
+                          json_generation_s=gen_s,
+                          plan_ms_per_change=1e3 * ph["plan_s"] / max(ph["changes"], 1))
+    finally:
+        for q in (jpath, tpath):
+            if os.path.exists(q):
+                os.unlink(q)
+        os.rmdir(tmp)
+    out["cpu_model"] = cpu_model()
+    out["nproc"] = os.cpu_count()
+    print(json.dumps(out))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -149,7 +219,13 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--stamps", action="store_true",
                     help="diagnostic: load the -DKB_STAMPS build and print per-phase times (not a bench line)")
+    ap.add_argument("--drop-in", action="store_true",
+                    help="what a drop-in user pays: kb_engine_balance per call and the CLI end to end "
+                         "(decode / create / plan / encode) on the workload's JSON; a separate line")
+    ap.add_argument("--cli-reassign", type=int, default=1000)
     args = ap.parse_args()
+    if args.drop_in:
+        return drop_in(args)
     if args.stamps:
         os.environ["KB_ENGINE_LIB"] = os.path.join(ROOT, "kafkabalancer_amd", "lib", "libkbengine_stamps.so")
 
@@ -257,8 +333,10 @@ def main():
     if args.stamps:
         st = eng.stamps()
         n = max(1, eng.stats()["steps"])       # every step since the engine was created
-        names = ["prep.S+r+ubloop", "step.loads", "res.reduce", "res.pred", "res.move", "res.apply(tail)", "prep.sort", None,
-                 "prep.blm+cert", "prep.reduce+eps", "prep.sets", "res.move->apply", "loads.bro+ctl", "loads.rec_reduce", "loads.keys", None, "sets.mark", "eps.sync1", "eps.wave0red", "sets.list", "sets.build", "keys.pre", "keys.insert"]
+        # (stamp ids as placed in kernels.hip; 6..20 name the fused incremental prep's phases)
+        names = ["prep.S+r+ubloop", "step.loads", "res.reduce", "res.pred", "res.move", "res.apply(tail)", "prep.P1", None,
+                 "prep.P2", "prep.P3", "prep.end", "res.move->apply", "loads.bro+ctl", "loads.rec_reduce", "loads.keys", None, "prep.P4",
+                 "eps.sync1", "eps.wave0red", "prep.positions", "prep.sets", "apply.loads", "apply.update"]
         counts = {"waves_scored": 7, "waves_gated_in": 15, "emits": 31, "spills": 30, "walks": 29, "walk_steps": 28, "walk_global": 27}
         mhz = 100.0 * st[25] / max(st[24], 1)           # shader clock (the phase stamps' unit)
         names = names + ["loads.broker", None, None, "stamp.overhead", "loads.setbits", "loads.hdr"]

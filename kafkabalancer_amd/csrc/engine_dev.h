@@ -190,6 +190,8 @@ struct DevCtl {
     double wskip;
     unsigned long long cand_cache[2];
     unsigned long long total_blocks;    // partition blocks the incremental scans read
+    double rlo, rhi;                    // range of r[] (every broker; k_step's prep): the scan's
+                                        // lower-bound prune reads it instead of reducing r[]
     // diagnostic phase stamps (builds with -DKB_STAMPS): accumulated
     // shader-clock ticks (clock64) per phase of k_step; [24]/[25] the wall-clock
     // (100 MHz) and shader-clock length of k_step; [26] one stamp's own cost

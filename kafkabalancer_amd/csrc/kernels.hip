@@ -508,6 +508,7 @@ struct ScanParams {
     int ubpass;                     // census-free round whose minima close an open bound
     int incr;                       // incremental round: only the blocks with wmax >= wskip
     double wskip;
+    double rlo, rhi;                // range of r[] (prune bound)
 };
 
 // One scan round of a workgroup over its tiles (its first tile already loaded into
@@ -541,19 +542,12 @@ __device__ __forceinline__ void scan_round(const ScanArgs& a, const ScanParams& 
 
     int tile = wg;
     // the lookup tables (one memory round trip, overlapping the first tile's loads)
-    double rlo = HUGE_VAL, rhi = -HUGE_VAL;          // range of the relative loads (prune bound)
     for (int i = tid; i < a.B; i += SCAN_THREADS) {
         const double r = ldd(a.r + i);
         s_rf[i] = make_double2(r, fsq(r));
         s_pos[i] = (int16_t)(int32_t)ld32(a.posm + i);
         s_blm[i] = (uint16_t)ld32(a.blm + i);
-        rlo = r < rlo ? r : rlo;
-        rhi = r > rhi ? r : rhi;
     }
-    __shared__ double s_rr[2][NW];
-    rlo = wave_min(rlo);
-    rhi = wave_max(rhi);
-    if (lane == 0) { s_rr[0][wid] = rlo; s_rr[1][wid] = rhi; }
     if (LSETS) for (int i = tid; i < a.nsets * U; i += SCAN_THREADS) s_set[i] = ldobj(a.setrec + i);
     for (int i = tid; i < DEDUP_SCAN; i += SCAN_THREADS) { s_key[i] = NONE32; s_wb[i] = NONE64; s_it[i] = NONE64; }
     if (tid == 0) s_nk = 0;
@@ -577,8 +571,9 @@ __device__ __forceinline__ void scan_round(const ScanArgs& a, const ScanParams& 
     // partitions all have LB > ub + 16 eps (rounding of d and LB: < 2 eps, see the
     // (1+R)^2 term of eps) holds neither the minimum nor a near tie: it only counts
     // its candidates.  With skewed weights that is almost every wave.
-    const double rmin = wave_min(lane < NW ? s_rr[0][lane] : HUGE_VAL);
-    const double rmax = wave_max(lane < NW ? s_rr[1][lane] : -HUGE_VAL);
+    // (the range [rmin, rmax] of r[] over every broker comes with the control block:
+    // k_step's prep reduced it; a 16-wave reduction here costs ~0.3 us per scan)
+    const double rmin = q.rlo, rmax = q.rhi;
     const double fmn = fsq(rmin), fmx = fsq(rmax);
     const double ubP = a.allow_leader ? (ubL > ubN ? ubL : ubN) : ubN;
     const double prune_t = (a.dbg & 16) ? HUGE_VAL : ubP + 16.0 * eps;    // dbg 16: no pruning
@@ -711,9 +706,14 @@ __device__ __forceinline__ void scan_round(const ScanArgs& a, const ScanParams& 
         // wave minima; the census runs only where a wave minimum can be within 8*eps
         // of the step's global minimum, which is at most ub (k_step's upper bound)
         // (g <= ub + 2*eps: the first-target score is monotone in the target up to 2*eps)
-        const double tL = wave_min(lL), tN = wave_min(lN);
-        const bool hasL = tL < HUGE_VAL && tL <= ubL + 12.0 * eps;
-        const bool hasN = tN < HUGE_VAL && tN <= ubN + 12.0 * eps;
+        // (the wave minimum is within 12 eps of ub iff some lane's is: a ballot, and the
+        // wave reduction only where it passes -- rare: the wave holding the step's minimum
+        // always does, since ub bounds it from above.  The record carries the minimum over
+        // the waves that passed, which is the step's minimum; a wave that did not pass
+        // holds no candidate within 12 eps of ub)
+        const bool hasL = __ballot(lL < HUGE_VAL && lL <= ubL + 12.0 * eps) != 0;
+        const bool hasN = __ballot(lN < HUGE_VAL && lN <= ubN + 12.0 * eps) != 0;
+        const double tL = hasL ? wave_min(lL) : HUGE_VAL, tN = hasN ? wave_min(lN) : HUGE_VAL;
 #ifdef KB_WALK_COUNTS
         if (lane == 0) {
             KB_COUNT(a.ctl, 7, 1);                                  // waves scored
@@ -810,8 +810,16 @@ __device__ __forceinline__ void scan_round(const ScanArgs& a, const ScanParams& 
     }
     if (INCR && q.incr && !a.ubpass && lane == 0 && nu) atomicAdd(&ctl->total_blocks, (unsigned long long)nu);
     // workgroup record: counts, first-index predicates, minima, near-tie keys
-    cL = wave_sum(cL);
-    cN = wave_sum(cN);
+    // (a wave's counts fit 32 bits unless the workgroup has tens of thousands of units:
+    // a 32-bit reduction is one DPP add per step against two moves and a carry chain)
+    const long long upw = (long long)(a.ntiles + a.nscan - 1) / a.nscan + (INCR ? (long long)a.nblk / ((long long)a.nscan * NW) + 1 : 0);
+    if (upw * (PER_LANE * 64) * a.B * RC < (1ll << 32)) {
+        cL = wave_sum((uint32_t)cL);
+        cN = wave_sum((uint32_t)cN);
+    } else {
+        cL = wave_sum(cL);
+        cN = wave_sum(cN);
+    }
     bool anyf = false;
 #pragma unroll
     for (int f = 0; f < NF; f++) anyf |= fst[f] != NONE32;
@@ -827,9 +835,12 @@ __device__ __forceinline__ void scan_round(const ScanArgs& a, const ScanParams& 
         for (int f = 0; f < NF; f++) s_f[f][wid] = fst[f];
     }
     __syncthreads();   // also orders every census insert before the flush
-    // the wave partials, combined lane-parallel (no serial LDS chains)
-    wgL = wave_min(lane < NW ? s_wm[0][lane] : HUGE_VAL);
-    wgN = wave_min(lane < NW ? s_wm[1][lane] : HUGE_VAL);
+    // the wave partials, combined lane-parallel by the waves that use them (the key
+    // flush below: waves 0..3, one per SIMD)
+    if (wid < DEDUP_SCAN / 64) {
+        wgL = wave_min(lane < NW ? s_wm[0][lane] : HUGE_VAL);
+        wgN = wave_min(lane < NW ? s_wm[1][lane] : HUGE_VAL);
+    }
     RecHdr* hdr = a.R.h(wg);
     Contender* keys = a.R.k(wg);
     // the near-tie keys within 4*eps of the workgroup minima; the minimum-score key
@@ -930,6 +941,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
     q.ubL = ctl->ub[0]; q.ubN = ctl->ub[1];
     q.heavy = ctl->heavy; q.nblm = ctl->nblm;
     q.tk_on = ctl->tk_on;
+    q.rlo = ctl->rlo; q.rhi = ctl->rhi;
     q.ubpass = 0;
     // (a conditional bound pass launched on the block list of the last records' best
     // keys: those blocks only, when k_step left one, else every tile)
@@ -1109,15 +1121,13 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
     double hd0 = HUGE_VAL, hd1 = HUGE_VAL;
     unsigned long long hc0 = 0, hc1 = 0;
     uint32_t hflg = 0, hfm = 0, hnk0 = 0, hnk1 = 0;
-    Contender hb0, hb1;                              // the record's best keys
-    hb0.s = hb1.s = -1;
     if (tid < a.R.n) {
-        const RecHdr h = ldobj(a.R.h(tid));
-        hd0 = h.dmin[0]; hd1 = h.dmin[1];
-        hc0 = h.cand[0]; hc1 = h.cand[1];
-        hflg = h.flags & 1u; hfm = h.fmask;
-        hnk0 = h.nkk[0]; hnk1 = h.nkk[1];
-        hb0 = h.best[0]; hb1 = h.best[1];
+        const RecHdr* h = a.R.h(tid);
+        hd0 = ldd(&h->dmin[0]); hd1 = ldd(&h->dmin[1]);
+        hc0 = ldobj(&h->cand[0]); hc1 = ldobj(&h->cand[1]);
+        hflg = ld32(&h->flags) & 1u; hfm = ld32(&h->fmask);
+        const uint32_t nkk = ld32(&h->nkk[0]);
+        hnk0 = nkk & 0xFFFFu; hnk1 = nkk >> 16;
     }
     KB_STAMP(ctl, 28);
     dedup_clear(T);
@@ -1137,42 +1147,50 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
     if (tid < NF) s_first[tid] = NONE32;
     if (tid < 2) { s_kc[tid] = 0; s_sok[tid] = -1; }   // (s_sok: -1 = no record offered its best key)
     if (halted != H_RUN) return;
+    // the records' best keys (the single-key shortcut below): issued after the staging
+    // round trip so they are not held in registers through it
+    Contender hb0, hb1;
+    hb0.s = hb1.s = -1;
+    if (do_res && tid < a.R.n) { hb0 = ldobj(&a.R.h(tid)->best[0]); hb1 = ldobj(&a.R.h(tid)->best[1]); }
     KB_STAMP(ctl, 12);
     // ---- the scan records (or the gathered rank summaries): one per thread, reduced
     // per wave with DPP and across the waves by wave 0; then every thread collects
     // its record's near-tie keys of both kinds within 4*eps of the minima (distinct
     // keys, earliest iteration index per key)
     if (do_res) {
-        double d0 = hd0, d1 = hd1;
-        unsigned long long c0 = hc0, c1 = hc1;
-        uint32_t flg = hflg, fm = hfm;
-        for (int i = tid + STEP_THREADS; i < a.R.n; i += STEP_THREADS) {
-            const RecHdr h = ldobj(a.R.h(i));
-            d0 = h.dmin[0] < d0 ? h.dmin[0] : d0;
-            d1 = h.dmin[1] < d1 ? h.dmin[1] : d1;
-            c0 += h.cand[0]; c1 += h.cand[1];
-            flg |= h.flags & 1u;
-            fm |= h.fmask;
-        }
-        d0 = wave_min(d0); d1 = wave_min(d1); c0 = wave_sum(c0); c1 = wave_sum(c1);
-        flg = wave_red_or(flg);
-        fm = wave_red_or(fm);
+        // the first-level reductions run only on the waves holding records (one per SIMD
+        // at 256 records: a wave reduction costs ~3.4x more with four waves per SIMD),
+        // the second level on wave 0, published through LDS
+        const int nrw = a.R.n >= STEP_THREADS ? NW : (a.R.n + 63) >> 6;
         __shared__ double s_pd[2][NW];
         __shared__ unsigned long long s_pc[2][NW];
-        __shared__ uint32_t s_pf[NF + 2][NW];
-        if (lane == 0) {
-            s_pd[0][wid] = d0; s_pd[1][wid] = d1; s_pc[0][wid] = c0; s_pc[1][wid] = c1;
-            s_pf[NF][wid] = flg; s_pf[NF + 1][wid] = fm;
+        __shared__ uint32_t s_pf[2][NW];
+        if (wid < nrw) {
+            double d0 = hd0, d1 = hd1;
+            unsigned long long c0 = hc0, c1 = hc1;
+            uint32_t flg = hflg, fm = hfm;
+            for (int i = tid + STEP_THREADS; i < a.R.n; i += STEP_THREADS) {
+                const RecHdr h = ldobj(a.R.h(i));
+                d0 = h.dmin[0] < d0 ? h.dmin[0] : d0;
+                d1 = h.dmin[1] < d1 ? h.dmin[1] : d1;
+                c0 += h.cand[0]; c1 += h.cand[1];
+                flg |= h.flags & 1u;
+                fm |= h.fmask;
+            }
+            d0 = wave_min(d0); d1 = wave_min(d1); c0 = wave_sum(c0); c1 = wave_sum(c1);
+            flg = wave_red_or(flg);
+            fm = wave_red_or(fm);
+            if (lane == 0) {
+                s_pd[0][wid] = d0; s_pd[1][wid] = d1; s_pc[0][wid] = c0; s_pc[1][wid] = c1;
+                s_pf[0][wid] = flg; s_pf[1][wid] = fm;
+            }
         }
         __syncthreads();
-        // every wave combines the wave partials of the minima itself (lane-parallel):
-        // no second barrier; wave 0 publishes the rest for the resolve
-        const bool pin = lane < NW;
-        const double g0 = wave_min(pin ? s_pd[0][lane] : HUGE_VAL), g1 = wave_min(pin ? s_pd[1][lane] : HUGE_VAL);
-        fm = wave_red_or(pin ? s_pf[NF + 1][lane] : 0u);
         if (wid == 0) {
-            c0 = wave_sum(pin ? s_pc[0][lane] : 0ull); c1 = wave_sum(pin ? s_pc[1][lane] : 0ull);
-            flg = wave_red_or(pin ? s_pf[NF][lane] : 0u);
+            const bool pin = lane < nrw;
+            const double g0 = wave_min(pin ? s_pd[0][lane] : HUGE_VAL), g1 = wave_min(pin ? s_pd[1][lane] : HUGE_VAL);
+            unsigned long long c0 = wave_sum(pin ? s_pc[0][lane] : 0ull), c1 = wave_sum(pin ? s_pc[1][lane] : 0ull);
+            const uint32_t flg = wave_red_or(pin ? s_pf[0][lane] : 0u), fm = wave_red_or(pin ? s_pf[1][lane] : 0u);
             if (lane == 0) {
                 if (a.incr) {
                     // an incremental scan read only some blocks: the counts are the last
@@ -1185,7 +1203,9 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
                 s_fm = fm;
             }
         }
-        if (fm) {
+        __syncthreads();
+        const double g0 = s_g[0], g1 = s_g[1];
+        if (s_fm) {
             // some record holds a first-index predicate (the plan is not in shape yet)
             uint32_t f[NF];
 #pragma unroll
@@ -1207,9 +1227,8 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
         // keys within the window, per kind, over the records within 8*eps of the
         // minimum; a kind with exactly one such key needs no key round trip: it is
         // that record's best key (inserted here speculatively in any case)
-        {
+        if (wid < nrw) {
             int kc0 = 0, kc1 = 0;
-            KB_STAMP(ctl, 21);
             if (tid < a.R.n) {
                 const bool q0 = hd0 <= g0 + 8.0 * eps, q1 = hd1 <= g1 + 8.0 * eps;
                 kc0 = q0 ? (int)hnk0 : 0;
@@ -1219,7 +1238,6 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
                 if (kc0 && hb0.s >= 0) { s_single[0] = hb0; s_sok[0] = cont_delta_ld(s_ld, hb0, inv_avg) <= g0 + 4.0 * eps; }
                 if (kc1 && hb1.s >= 0) { s_single[1] = hb1; s_sok[1] = cont_delta_ld(s_ld, hb1, inv_avg) <= g1 + 4.0 * eps; }
             }
-            KB_STAMP(ctl, 22);
             kc0 = wave_sum(kc0); kc1 = wave_sum(kc1);
             if (lane == 0) {
                 if (kc0) atomicAdd(&s_kc[0], kc0);
@@ -1269,6 +1287,28 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
         __syncthreads();
     }
     KB_STAMP(ctl, 1);
+
+    // the apply's operands for the single-key kinds (the usual move() decision), issued
+    // now so their round trip overlaps the resolve: replica counts and load error
+    // bounds of the key's source / target (lanes 2k, 2k + 1), the leader key's meta word
+    // and NumConsumers (a leader move carries W * (len(R) + NumConsumers))
+    int pf_cnt = 0, pf_nc = 0;
+    uint32_t pf_meta = 0;
+    double pf_lerr = 0.0;
+    if (do_res && wid == 0 && lane < 4) {
+        const int k = lane >> 1;
+        if (s_li[k] == -2) {
+            const Contender c = s_single[k];
+            const int b = (lane & 1) ? c.t : c.s;
+            pf_cnt = a.cnt[b];
+            if (!a.integral) pf_lerr = a.lerr[b];
+            if (lane == 0) {
+                const long long p = (long long)(c.iter >> 21);
+                pf_meta = a.meta[p];
+                pf_nc = a.nc[p];
+            }
+        }
+    }
 
     // ================================================================ resolve
     if (do_res) {
@@ -1688,14 +1728,36 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
             double oldc = 0.0, newc = 0.0, av = 0.0;
             if (fast) {
                 b = lane == 0 ? D.from : to;
+                // (the operands prefetched before the resolve when the decision is the
+                // kind's single key; else one round trip)
+                const int k = D.step == 7 ? 0 : 1;
+                bool pf = s_li[k] == -2;
+                if (pf) {
+                    const Contender& c = s_single[k];
+                    pf = c.s == D.from && c.t == to && (long long)(c.iter >> 21) == p;
+                }
                 if (lane < 2) {                              // every load in one round trip
-                    cv = a.cnt[b];
-                    if (!a.integral) av = a.lerr[b];
+                    if (pf) {
+                        cv = lane == 0 ? __builtin_amdgcn_readlane(pf_cnt, 2 * k) : __builtin_amdgcn_readlane(pf_cnt, 2 * k + 1);
+                        if (!a.integral) {
+                            const long long lo = __double_as_longlong(pf_lerr);
+                            const int l0 = __builtin_amdgcn_readlane((int)lo, 2 * k), h0 = __builtin_amdgcn_readlane((int)(lo >> 32), 2 * k);
+                            const int l1 = __builtin_amdgcn_readlane((int)lo, 2 * k + 1), h1 = __builtin_amdgcn_readlane((int)(lo >> 32), 2 * k + 1);
+                            av = lane == 0 ? __longlong_as_double(((long long)h0 << 32) | (uint32_t)l0)
+                                           : __longlong_as_double(((long long)h1 << 32) | (uint32_t)l1);
+                        }
+                    } else {
+                        cv = a.cnt[b];
+                        if (!a.integral) av = a.lerr[b];
+                    }
                 }
                 double c = D.w;
                 if (slot == 0) {
-                    const uint32_t m = a.meta[p];
-                    c = D.w * (double)((int)meta_nrep(m) + a.nc[p]);
+                    uint32_t m;
+                    int ncp;
+                    if (pf && k == 0) { m = (uint32_t)__builtin_amdgcn_readlane((int)pf_meta, 0); ncp = __builtin_amdgcn_readlane(pf_nc, 0); }
+                    else { m = a.meta[p]; ncp = a.nc[p]; }
+                    c = D.w * (double)((int)meta_nrep(m) + ncp);
                 }
                 if (lane == 0) a.rep[(long long)slot * a.Ppad + p] = (uint16_t)to;
                 act = lane < 2;
@@ -1785,6 +1847,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
                     upd = true;
                 }
             }
+            KB_STAMP(ctl, 21);
             if (upd) {
                 const bool touched = act && oldc != newc;
                 const bool cnt_changes = act && dcnt != 0;
@@ -1818,6 +1881,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
                         a.bfl[b] = fl; s_fl[b] = fl;
                     }
                 }
+                KB_STAMP(ctl, 22);
                 dd = wave_sum(dd);
                 const unsigned long long bt = __ballot(touched);
                 if (touched) {
@@ -1914,6 +1978,13 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
         };
         // ---- P1.  sum waves: S, E, |bl_move| partials and the bl_move bits by broker id;
         // order waves: old positions of the touched brokers, the sets holding one
+        // the records' best keys for the upper bound (P2): issued now, in flight during P1
+        // (held in registers from the header load, they would stay live through the
+        // resolve, the apply and the exact folds)
+        const bool bkeys = do_res && tid < a.R.n;
+        Contender bk0, bk1;
+        bk0.s = bk1.s = -1;
+        if (bkeys) { bk0 = ldobj(&a.R.h(tid)->best[0]); bk1 = ldobj(&a.R.h(tid)->best[1]); }
         if (tid < nT) { s_fl[s_T[tid]] |= BF_TOUCHED; s_cntT[tid] = 0; }
         if (tid == 0) { s_unc = 0; s_nsub = 0; }
         if (wid < NRW) {
@@ -1954,7 +2025,6 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
         KB_STAMP(ctl, 6);
         // ---- P2.  sum waves (and any wave holding a record's best keys): avg, r, U0 /
         // V / Rm partials, the upper bound; order waves: the new positions
-        const bool bkeys = do_res && tid < a.R.n;
         int nb[NQ], np[NQ];
         if (wid < NRW || wid * 64 < (do_res ? a.R.n : 0)) {
             // (the same fixed-order combination on every such wave: identical bits)
@@ -1987,7 +2057,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
                 const long long pm = s_moved;
 #pragma unroll
                 for (int k = 0; k < 2; k++) {
-                    const Contender& c = k ? hb1 : hb0;
+                    const Contender& c = k ? bk1 : bk0;
                     // the block of every best key other than the moved partition's: if no
                     // key survives below, the conditional bound pass scans only these blocks
                     // and the heaviest blocks by weight (engine.cpp fills that part once):
@@ -2011,7 +2081,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
             ub0 = wave_min(ub0); ub1 = wave_min(ub1);
             if (wid < NRW) {
                 su = wave_sum(su); v = wave_sum(v); rm = wave_max(rm);
-                if (a.incr) { rlo = wave_min(rlo); rhi = wave_max(rhi); }
+                rlo = wave_min(rlo); rhi = wave_max(rhi);
             }
             if (lane == 0) {
                 s_fq2[3][wid] = ub0; s_fq2[4][wid] = ub1;
@@ -2095,13 +2165,14 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
             double ws = 0.0;
             const bool inc = a.incr && do_res && D.status == 1 && D.kind == 1 && (D.step == 7 || D.step == 8) &&
                              nblm == nblm0 && !s_fm && !a.rebalance && !a.sem_go && a.use_spill;
+            const double rlo = fmin(fmin(s_fq2[5][0], s_fq2[5][1]), fmin(s_fq2[5][2], s_fq2[5][3]));
+            const double rhi = fmax(fmax(s_fq2[6][0], s_fq2[6][1]), fmax(s_fq2[6][2], s_fq2[6][3]));
             if (inc) {
-                const double rlo = fmin(fmin(s_fq2[5][0], s_fq2[5][1]), fmin(s_fq2[5][2], s_fq2[5][3]));
-                const double rhi = fmax(fmax(s_fq2[6][0], s_fq2[6][1]), fmax(s_fq2[6][2], s_fq2[6][3]));
                 const double ubP = a.allow_leader ? (ub0 > ub1 ? ub0 : ub1) : ub1;
                 ws = incr_wskip(rlo, rhi, ubP + 16.0 * ep, avg, iav, lane);
             }
             if (lane == 0) {
+                C.rlo = rlo; C.rhi = rhi;
                 C.incr_ok = ws > 0.0 ? 1 : 0;
                 C.wskip = ws;
                 C.ub_sub = a.ubdesc && a.R.n <= STEP_THREADS && (s_nsub > 0 || a.ub_heavy) ? 1 : 0;
@@ -2418,7 +2489,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
     const double S = wave_sum(lane < NW ? s_q[0][lane] : 0.0), E = wave_sum(lane < NW ? s_q[1][lane] : 0.0);
     const double avg = S / (double)nblm;
     const double iav = 1.0 / avg;
-    double su = 0.0, v = 0.0, rm = 0.0;
+    double su = 0.0, v = 0.0, rm = 0.0, rlo = HUGE_VAL, rhi = -HUGE_VAL;
     for (int b = tid; b < B; b += STEP_THREADS) {
         double r = 0.0;
         if (s_fl[b] & (BF_PRESENT | BF_INCFG)) {
@@ -2429,8 +2500,13 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
             rm = ar > rm ? ar : rm;
         }
         stdbl(a.r + b, r);
+        rlo = r < rlo ? r : rlo;                    // the scan's range of r[] (prune bound)
+        rhi = r > rhi ? r : rhi;
     }
     su = wave_sum(su); v = wave_sum(v); rm = wave_max(rm);
+    rlo = wave_min(rlo); rhi = wave_max(rhi);
+    __shared__ double s_rr2[2][NW];
+    if (lane == 0) { s_rr2[0][wid] = rlo; s_rr2[1][wid] = rhi; }
     // upper bound of the next step's minimum per kind: the near-tie keys of the scan
     // just resolved whose partition and brokers the applied move did not touch are
     // still candidates; re-scored on the new loads they bound the new minimum
@@ -2460,6 +2536,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
         const double Rm = wave_max(in ? s_q[2][lane] : 0.0);
         ub0 = wave_min(in ? s_ubw[0][lane] : HUGE_VAL);
         ub1 = wave_min(in ? s_ubw[1][lane] : HUGE_VAL);
+        const double rlo2 = wave_min(in ? s_rr2[0][lane] : HUGE_VAL), rhi2 = wave_max(in ? s_rr2[1][lane] : -HUGE_VAL);
 #ifdef KB_STAMPS
         if (lane == 0) KB_STAMP(ctl, 18);
 #endif
@@ -2474,6 +2551,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
         if (!(ep > 1e-300)) ep = 1e-300;
         C.S = S; C.avg = avg; C.inv_avg = iav; C.U0 = U0;
         C.V = V; C.eps = ep; C.E = E; C.nblm = nblm;
+        C.rlo = rlo2; C.rhi = rhi2;
         const bool sup = a.use_spill && do_res && !full && D.status == 1 && D.step >= 3 && D.step <= 5;
         C.ub[0] = sup ? -HUGE_VAL : ub0; C.ub[1] = sup ? -HUGE_VAL : ub1;
         C.incr_ok = 0;                      // (the next scan reads every block)

@@ -6,6 +6,7 @@
 // slice aliasing) and -device N.  -from-zk (ZooKeeper ingest) is
 // out of scope: it fails like an unreachable ZooKeeper (exit 2).
 #include <cerrno>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -240,6 +241,12 @@ int Run(const std::vector<std::string>& args, const std::function<std::string(bo
         usage();
         return 3;
     }
+    // diagnostic phase wall times (KB_CLI_TIMINGS=<file>: one JSON line appended; what a
+    // drop-in user pays end to end, bench.py --drop-in)
+    using clk = std::chrono::steady_clock;
+    const clk::time_point t_start = clk::now();
+    double t_read = 0, t_decode = 0, t_create = 0, t_plan = 0, t_encode = 0;
+    auto secs = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double>(b - a).count(); };
     std::string data;
     if (!input.empty()) {
         FILE* fp = fopen(input.c_str(), "rb");
@@ -268,6 +275,8 @@ int Run(const std::vector<std::string>& args, const std::function<std::string(bo
     }
     PartitionList pl;
     std::string perr;
+    clk::time_point t_mark = clk::now();
+    t_read = secs(t_start, t_mark);
     if (!zk.empty()) {
         perr = "failed parsing zk connection string: ZooKeeper ingest is not supported by this build (" + zk + ")";
     } else {
@@ -282,6 +291,7 @@ int Run(const std::vector<std::string>& args, const std::function<std::string(bo
         log.print("failed getting partition list: " + perr);
         return 2;
     }
+    { const clk::time_point t = clk::now(); t_decode = secs(t_mark, t); t_mark = t; }
 
     cfg.allow_leader = B("allow-leader");
     cfg.rebalance_leaders = B("rebalance-leader");
@@ -309,6 +319,7 @@ int Run(const std::vector<std::string>& args, const std::function<std::string(bo
         log.print("failed optimizing distribution: " + planner.error());
         return 3;
     }
+    { const clk::time_point t = clk::now(); t_create = secs(t_mark, t); t_mark = t; }
     bool completing = false;
     Partition cpart;
     int64_t r = max_reassign;
@@ -357,12 +368,24 @@ int Run(const std::vector<std::string>& args, const std::function<std::string(bo
             }
         }
     }
+    { const clk::time_point t = clk::now(); t_plan = secs(t_mark, t); t_mark = t; }
     PartitionList* res = &opl;
     PartitionList filtered;
     if (B("full-output")) res = &pl;
     if (B("unique")) { filtered = FilterPartitionList(*res); res = &filtered; }
     log.print("Writing " + std::to_string(res->partitions.size()) + " changes.");
     std::string bytes = EncodePartitionList(*res);
+    t_encode = secs(t_mark, clk::now());
+    if (const char* tf = getenv("KB_CLI_TIMINGS")) {
+        if (FILE* fp = fopen(tf, "a")) {
+            fprintf(fp, "{\"read_s\": %.6f, \"decode_s\": %.6f, \"create_s\": %.6f, \"plan_s\": %.6f, "
+                        "\"encode_s\": %.6f, \"input_bytes\": %zu, \"partitions\": %zu, \"changes\": %zu, "
+                        "\"output_bytes\": %zu}\n",
+                    t_read, t_decode, t_create, t_plan, t_encode, data.size(), pl.partitions.size(),
+                    opl.partitions.size(), bytes.size());
+            fclose(fp);
+        }
+    }
     if (fail_output) {
         log.print("failed writing partition list: failed serializing json: write failed");
         return 4;
