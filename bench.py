@@ -223,9 +223,37 @@ def main():
                     help="what a drop-in user pays: kb_engine_balance per call and the CLI end to end "
                          "(decode / create / plan / encode) on the workload's JSON; a separate line")
     ap.add_argument("--cli-reassign", type=int, default=1000)
+    ap.add_argument("--step-alone", action="store_true",
+                    help="diagnostic: k_step alone on a fixed input after the warm-up plan "
+                         "(kb_engine_bench_step; with a -DKB_STOP_AT=k library: the cost up to phase k)")
     args = ap.parse_args()
     if args.drop_in:
         return drop_in(args)
+    if args.step_alone:
+        import torch
+        from kafkabalancer_amd import engine as E
+        from kafkabalancer_amd import synth
+        torch.cuda.set_device(0)
+        cl, cfg, desc = synth.config(args.workload, scale=args.scale)
+        eng = E.Engine(cl, cfg, device=0)
+        _, err = eng.plan(max(args.warmup, 1))
+        assert err is None, err
+        steplib = os.environ.get("KB_STEP_LIB")
+        if steplib:
+            # a -DKB_STOP_AT=k build's k_step on this engine (same sources: same host layout);
+            # the warm-up plan above ran the production library
+            import ctypes
+            L2 = ctypes.CDLL(steplib)
+            L2.kb_engine_bench_step.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
+            v = ctypes.c_double()
+            rc = L2.kb_engine_bench_step(eng.h, args.steps, ctypes.byref(v))
+            assert rc == 0, rc
+            res = v.value
+        else:
+            res = eng.bench_step(args.steps)
+        print(json.dumps({"workload": args.workload, "lib": os.path.basename(steplib or E.LIB_PATH),
+                          "k_step_alone_us": res, "iters": args.steps}))
+        return
     if args.stamps:
         os.environ["KB_ENGINE_LIB"] = os.path.join(ROOT, "kafkabalancer_amd", "lib", "libkbengine_stamps.so")
 

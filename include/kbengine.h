@@ -200,6 +200,10 @@ int kb_engine_stamps(kb_engine *e, uint64_t *out, int n);
 /* Diagnostic: average device time (us) of the scan kernel over `iters`
  * back-to-back launches on the current state (nothing is applied). */
 int kb_engine_bench_scan(kb_engine *e, int iters, double *avg_us);
+/* Diagnostic: k_step alone on a fixed input (state snapshotted after a scan, restored
+ * before each launch); HIP-event time per launch in *avg_us.  The engine is left as it
+ * was after the scan.  (Phase costs: run it on -DKB_STOP_AT=k builds.) */
+int kb_engine_bench_step(kb_engine *e, int iters, double *avg_us);
 
 /* Reference-format message of the last error ("<Step>: partition Partition(t,p,[..]) ..."). */
 int kb_engine_last_error(kb_engine *e, char *buf, size_t n);

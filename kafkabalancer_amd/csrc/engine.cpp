@@ -74,6 +74,7 @@ struct kb_engine {
     double* w = nullptr;
     uint16_t* rep = nullptr;
     uint32_t* meta = nullptr;
+    uint32_t* pset = nullptr;         // [Ppad] allowed-set index per partition (set records not in LDS)
     int32_t* nc = nullptr;
     double* load = nullptr;
     double* lerr = nullptr;
@@ -278,8 +279,8 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
     }
     e->nsets = (int64_t)sets.size();
     if (e->nsets == 0) { sets.emplace_back(); e->nsets = 1; }
-    if ((uint64_t)e->nsets >= MAX_SETS) {
-        e->last_err = "engine supports at most 32767 distinct broker lists";
+    if (e->nsets > (1ll << 30)) {
+        e->last_err = "engine supports at most 2^30 distinct broker lists";
         *out = e;
         return KB_ERR_UNSUPPORTED;
     }
@@ -410,7 +411,9 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
         }
         const uint32_t elig = want[i] >= e->minrep ? 1u : 0u;
         const uint32_t wnt = want[i] < 0 ? 0u : (uint32_t)std::min<int64_t>(want[i], 31);
-        hm[i] = make_meta((uint32_t)len[i], wnt, elig, dis, nin, (uint32_t)pset[i]);
+        // (the meta word's 15-bit set field serves the LDS-resident set records, at most
+        // 4096 sets; with more, the scan and the step read the index array pset)
+        hm[i] = make_meta((uint32_t)len[i], wnt, elig, dis, nin, (uint32_t)pset[i] & (MAX_SETS - 1));
     }
     std::vector<uint8_t> hin(e->B, 0);
     if (!cfg->brokers_nil)
@@ -488,14 +491,15 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
     HIPCHK(dalloc(&e->meta, e->Ppad));
     HIPCHK(dalloc(&e->rep, (size_t)e->rc_dev * e->Ppad));
     HIPCHK(dalloc(&e->nc, e->Ppad));
-    HIPCHK(dalloc(&e->load, e->B));
+    // (+16 B on the arrays k_step stages by LDS-DMA: it copies whole 16-B granules)
+    HIPCHK(dalloc(&e->load, e->B + 2));
     HIPCHK(dalloc(&e->lerr, e->B));
-    HIPCHK(dalloc(&e->eb, e->B));
-    HIPCHK(dalloc(&e->bfl, e->B));
+    HIPCHK(dalloc(&e->eb, e->B + 2));
+    HIPCHK(dalloc(&e->bfl, e->B + 16));
     HIPCHK(dalloc(&e->cnt, e->B));
-    HIPCHK(dalloc(&e->setbits, (size_t)e->nsets * e->W64));
+    HIPCHK(dalloc(&e->setbits, (size_t)e->nsets * e->W64 + 2));   // (+2: k_step reads whole 16-B words)
     HIPCHK(dalloc(&e->setrec, (size_t)e->nsets * e->units));
-    HIPCHK(dalloc(&e->order, e->B));
+    HIPCHK(dalloc(&e->order, e->B + 4));
     HIPCHK(dalloc(&e->posu, e->B));
     HIPCHK(dalloc(&e->blm, e->B));
     HIPCHK(dalloc(&e->posm, e->B));
@@ -529,6 +533,12 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
     HIPCHK(hipHostMalloc((void**)&e->h_ctl, sizeof(DevCtl), hipHostMallocDefault));
     HIPCHK(hipMemcpy(e->w, hw.data(), hw.size() * 8, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(e->meta, hm.data(), hm.size() * 4, hipMemcpyHostToDevice));
+    if (!e->lds_sets) {
+        std::vector<uint32_t> hp(e->Ppad, 0u);
+        for (int64_t i = 0; i < n; i++) hp[i] = (uint32_t)pset[i];
+        HIPCHK(dalloc(&e->pset, e->Ppad));
+        HIPCHK(hipMemcpy(e->pset, hp.data(), hp.size() * 4, hipMemcpyHostToDevice));
+    }
     HIPCHK(hipMemcpy(e->rep, hr.data(), hr.size() * 2, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(e->nc, hnc.data(), hnc.size() * 4, hipMemcpyHostToDevice));
     if (e->B) {
@@ -591,6 +601,7 @@ static void fill_scan_args(kb_engine* e, ScanArgs& s) {
     s.ubpass = 0;
     s.L = e->L;
     s.incr = e->incr; s.nblk = (int)e->nblk; s.bdesc = e->bdesc;
+    s.pset = e->pset;
 }
 
 static void fill_step_args(kb_engine* e, StepArgs& a, const Recs& R, int use_spill) {
@@ -611,6 +622,7 @@ static void fill_step_args(kb_engine* e, StepArgs& a, const Recs& R, int use_spi
     a.incr = e->incr && use_spill;
     a.ubdesc = e->ubdesc;
     a.ub_heavy = e->nubdesc > 2 * std::max<int64_t>(e->nscan, STEP_THREADS) ? 1 : 0;
+    a.pset = e->pset;
 }
 
 static const int kStepBatch = 64;
@@ -1201,6 +1213,62 @@ extern "C" int kb_engine_bench_scan(kb_engine* e, int iters, double* avg_us) {
     return KB_OK;
 }
 
+// Diagnostic: k_step alone on one fixed input: the state k_step mutates is snapshotted
+// after a scan and restored before every launch, and HIP events time the launch alone.
+// Run on -DKB_STOP_AT=k builds (kernels.hip, KB_STOP: return after phase k), the
+// cumulative times give the phase costs without instrumenting the production kernel.
+extern "C" int kb_engine_bench_step(kb_engine* e, int iters, double* avg_us) {
+    if (e) e->ctl_mirror = false;
+    if (!e || iters < 1 || !avg_us) return KB_ERR_INVALID;
+    if (e->pending) return e->pending;
+    if (const int rc = reset_ctl(e, 1); rc != KB_OK) return rc;
+    if (!e->h_ctl->prepped) {
+        enqueue_step(e);                              // prep only
+        HIPCHK(hipStreamSynchronize(e->st));
+    }
+    if (e->ub_mode) enqueue_ubinit(e);
+    enqueue_scan(e);                                  // the records k_step resolves
+    struct Arr { void* p; size_t bytes; void* snap; };
+    std::vector<Arr> arrs = {
+        {e->ctl, sizeof(DevCtl), nullptr}, {e->load, (size_t)e->B * 8, nullptr}, {e->lerr, (size_t)e->B * 8, nullptr},
+        {e->eb, (size_t)e->B * 8, nullptr}, {e->bfl, (size_t)e->B, nullptr}, {e->cnt, (size_t)e->B * 4, nullptr},
+        {e->order, (size_t)e->B * 4, nullptr}, {e->posu, (size_t)e->B * 4, nullptr}, {e->blm, (size_t)e->B * 4, nullptr},
+        {e->posm, (size_t)e->B * 4, nullptr}, {e->r, (size_t)e->B * 8, nullptr},
+        {e->rep, (size_t)e->rc_dev * e->Ppad * 2, nullptr}, {e->meta, (size_t)e->Ppad * 4, nullptr},
+        {e->setrec, (size_t)e->nsets * e->units * 16, nullptr}};
+    if (e->ubdesc) arrs.push_back({e->ubdesc, (size_t)e->nubdesc * sizeof(BlockDesc), nullptr});
+    for (auto& x : arrs) {
+        if (!x.bytes) continue;
+        HIPCHK(hipMalloc(&x.snap, x.bytes));
+        HIPCHK(hipMemcpyAsync(x.snap, x.p, x.bytes, hipMemcpyDeviceToDevice, e->st));
+    }
+    hipEvent_t a, b;
+    HIPCHK(hipEventCreate(&a));
+    HIPCHK(hipEventCreate(&b));
+    StepArgs sa;
+    fill_step_args(e, sa, scan_recs(e->recs, (int)e->nscan), 1);
+    double tot = 0;
+    for (int i = 0; i <= iters; i++) {               // (the first launch warms up)
+        for (auto& x : arrs)
+            if (x.bytes) HIPCHK(hipMemcpyAsync(x.p, x.snap, x.bytes, hipMemcpyDeviceToDevice, e->st));
+        HIPCHK(hipEventRecord(a, e->st));
+        launch_step(sa, e->st);
+        HIPCHK(hipEventRecord(b, e->st));
+        HIPCHK(hipEventSynchronize(b));
+        float ms = 0;
+        hipEventElapsedTime(&ms, a, b);
+        if (i) tot += ms;
+    }
+    *avg_us = 1e3 * tot / iters;
+    for (auto& x : arrs)                              // (leave the engine as it was after the scan)
+        if (x.bytes) { HIPCHK(hipMemcpyAsync(x.p, x.snap, x.bytes, hipMemcpyDeviceToDevice, e->st)); }
+    HIPCHK(hipStreamSynchronize(e->st));
+    for (auto& x : arrs) if (x.snap) hipFree(x.snap);
+    hipEventDestroy(a);
+    hipEventDestroy(b);
+    return KB_OK;
+}
+
 extern "C" int kb_engine_last_error(kb_engine* e, char* buf, size_t n) {
     if (!e || !buf || n == 0) return KB_ERR_INVALID;
     snprintf(buf, n, "%s", e->last_err.c_str());
@@ -1209,7 +1277,7 @@ extern "C" int kb_engine_last_error(kb_engine* e, char* buf, size_t n) {
 
 extern "C" void kb_engine_destroy(kb_engine* e) {
     if (!e) return;
-    void* ptrs[] = {e->w, e->rep, e->meta, e->nc, e->load, e->lerr, e->eb, e->bfl, e->cnt,
+    void* ptrs[] = {e->w, e->rep, e->meta, e->pset, e->nc, e->load, e->lerr, e->eb, e->bfl, e->cnt,
                     e->setbits, e->setrec, e->order, e->posu, e->blm, e->posm, e->r,
                     e->bset_off, e->bset_ids, e->recs, e->cont, e->ctl, e->log, e->bdesc, e->ubdesc,
                     e->L.lstart, e->L.llen, e->L.lcap, e->L.lent};

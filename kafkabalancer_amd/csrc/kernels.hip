@@ -290,7 +290,7 @@ __device__ __forceinline__ double cont_delta(const double* r, const Contender& c
 // (partition lists sorted by index, for the exact refold of k_refresh)
 
 // remove partition q from broker b's list (block-wide, all threads call)
-__device__ void list_remove(const Lists& L, int b, uint32_t q, int* s_i) {
+__device__ void list_remove(Lists L, int b, uint32_t q, int* s_i) {
     const uint32_t st = L.lstart[b], n = L.llen[b];
     const uint32_t nt = blockDim.x;
     if (threadIdx.x == 0) *s_i = -1;
@@ -314,7 +314,7 @@ __device__ void list_remove(const Lists& L, int b, uint32_t q, int* s_i) {
 }
 
 // insert partition q into broker b's sorted list
-__device__ bool list_insert(const Lists& L, int b, uint32_t q, int* s_i) {
+__device__ bool list_insert(Lists L, int b, uint32_t q, int* s_i) {
     const uint32_t st = L.lstart[b], n = L.llen[b];
     const uint32_t nt = blockDim.x;
     if (n >= L.lcap[b]) return false;
@@ -345,7 +345,9 @@ __device__ bool list_insert(const Lists& L, int b, uint32_t q, int* s_i) {
 }
 
 // the list change of the last applied move (kind 1 replace, 2 remove, 3 add)
-__device__ void do_list_op(DevCtl* ctl, const Lists& L, int* s_i) {
+// (the lists by value: a reference into k_step's kernel-argument struct would make the
+// struct's address escape -- copied to scratch, every field then a scratch load)
+__device__ void do_list_op(DevCtl* ctl, Lists L, int* s_i) {
     if (!ctl->pending_list) return;
     const int kind = ctl->pl_kind, from = ctl->pl_from, to = ctl->pl_to;
     const uint32_t p = (uint32_t)ctl->pl_part;
@@ -379,6 +381,8 @@ struct PartRaw {
     double2 w;                      // weights of the lane's two partitions
     uint2 m;                        // their meta words
     uint32_t r[RC];                 // slot k: two u16 dense broker ids
+    uint2 ps;                       // their allowed-set indices (set records in memory only:
+                                    // ScanArgs.pset; else the meta word's set field)
     __device__ __forceinline__ double wt(int j) const { return j ? w.y : w.x; }
     __device__ __forceinline__ uint32_t mt(int j) const { return j ? m.y : m.x; }
     __device__ __forceinline__ uint32_t rp(int k, int j) const { return j ? (r[k] >> 16) : (r[k] & 0xFFFFu); }
@@ -386,12 +390,19 @@ struct PartRaw {
 
 // two consecutive partitions per lane: one 16-B weight load, one 8-B meta load
 // and one 4-B load per replica slot (coalesced across the wave)
-template <int RC>
+template <int RC, bool LSETS>
 __device__ __forceinline__ void load_parts(const ScanArgs& a, long long base, PartRaw<RC>& P) {
     P.w = *(const double2*)(a.w + base);
     P.m = *(const uint2*)(a.meta + base);
 #pragma unroll
     for (int k = 0; k < RC; k++) P.r[k] = *(const uint32_t*)(a.rep + (long long)k * a.Ppad + base);
+    if (!LSETS) P.ps = *(const uint2*)(a.pset + base);
+}
+// a partition's allowed-set index: the meta word's 15-bit field when the set records
+// live in LDS (at most 4096 sets), else the per-partition index array (any count)
+template <int RC, bool LSETS>
+__device__ __forceinline__ uint32_t set_of(const PartRaw<RC>& P, int j) {
+    return LSETS ? meta_set(P.mt(j)) : (j ? P.ps.y : P.ps.x);
 }
 
 __device__ __forceinline__ void emit_global(const ScanArgs& a, const Contender& c) {
@@ -465,12 +476,12 @@ __device__ void walk_targets(const ScanArgs& a, const Dedup& T, const double2* s
 // first allowed target in bl order that is not a replica (steps.go:192-201):
 // among the first RC+1 entries of the partition's set record
 template <int RC, bool LSETS>
-__device__ __forceinline__ int first_target(const ScanArgs& a, const uint4* s_set, uint32_t m,
+__device__ __forceinline__ int first_target(const ScanArgs& a, const uint4* s_set, uint32_t set,
                                             const uint32_t (&reps)[RC], int nrep, int* nelig) {
     constexpr int U = sr_units(RC);
     constexpr int KT = RC + 1;
     uint4 R[U];
-    set_record<RC, LSETS>(a, s_set, meta_set(m), R);
+    set_record<RC, LSETS>(a, s_set, set, R);
     *nelig = (int)rec_u16(R, 0);
     // slots past nrep compare against an id no record holds (ids < MAXB, NONE16 = padding);
     // padding is never a replica, so it is picked only when no valid target precedes it
@@ -511,11 +522,22 @@ struct ScanParams {
     double rlo, rhi;                // range of r[] (prune bound)
 };
 
-// One scan round of a workgroup over its tiles (its first tile already loaded into
-// A): stage the tables, score, write the workgroup record.
+// the lookup tables as loaded by one thread (issued with the control block, before the
+// first tile: one round trip; written to LDS by scan_round)
+// (pre: up to SCAN_THREADS brokers and set-record units, one of each per thread; larger
+// tables are loaded by scan_round itself)
+struct TabRaw {
+    bool pre;
+    double r;
+    int32_t pos, blm;
+    uint4 set;
+};
+
+// One scan round of a workgroup over its tiles (its first tile and the tables already
+// loaded into A / T): stage the tables, score, write the workgroup record.
 template <int RC, bool LSETS, bool INCR>
 __device__ __forceinline__ void scan_round(const ScanArgs& a, const ScanParams& q, unsigned char* smem,
-                                           PartRaw<RC>& A,
+                                           PartRaw<RC>& A, const TabRaw& TR,
                                            unsigned long long t_in,
                                            int wg, long long c0_in) {
     DevCtl* ctl = a.ctl;
@@ -541,14 +563,40 @@ __device__ __forceinline__ void scan_round(const ScanArgs& a, const ScanParams& 
     __shared__ uint32_t s_bslot[2], s_nkk[2];
 
     int tile = wg;
-    // the lookup tables (one memory round trip, overlapping the first tile's loads)
-    for (int i = tid; i < a.B; i += SCAN_THREADS) {
-        const double r = ldd(a.r + i);
-        s_rf[i] = make_double2(r, fsq(r));
-        s_pos[i] = (int16_t)(int32_t)ld32(a.posm + i);
-        s_blm[i] = (uint16_t)ld32(a.blm + i);
+    // the lookup tables (loaded by the caller with the control block when they are small)
+    if (TR.pre) {
+        if (tid < a.B) {
+            s_rf[tid] = make_double2(TR.r, fsq(TR.r));
+            s_pos[tid] = (int16_t)TR.pos;
+            s_blm[tid] = (uint16_t)TR.blm;
+        }
+    } else {
+        // (more brokers: every load first -- at most MAXB / SCAN_THREADS per thread --
+        // then the LDS writes: one round trip, not one per loop iteration)
+        constexpr int TQ = (MAXB + SCAN_THREADS - 1) / SCAN_THREADS;
+        double rr[TQ];
+        int32_t pp[TQ], bb[TQ];
+#pragma unroll
+        for (int k = 0; k < TQ; k++) {
+            const int i = min(k * SCAN_THREADS + tid, a.B - 1);
+            rr[k] = ldd(a.r + i);
+            pp[k] = (int32_t)ld32(a.posm + i);
+            bb[k] = (int32_t)ld32(a.blm + i);
+        }
+#pragma unroll
+        for (int k = 0; k < TQ; k++) {
+            const int i = k * SCAN_THREADS + tid;
+            if (i < a.B) {
+                s_rf[i] = make_double2(rr[k], fsq(rr[k]));
+                s_pos[i] = (int16_t)pp[k];
+                s_blm[i] = (uint16_t)bb[k];
+            }
+        }
     }
-    if (LSETS) for (int i = tid; i < a.nsets * U; i += SCAN_THREADS) s_set[i] = ldobj(a.setrec + i);
+    if (LSETS) {
+        if (TR.pre) { if (tid < a.nsets * U) s_set[tid] = TR.set; }
+        else for (int i = tid; i < a.nsets * U; i += SCAN_THREADS) s_set[i] = ldobj(a.setrec + i);
+    }
     for (int i = tid; i < DEDUP_SCAN; i += SCAN_THREADS) { s_key[i] = NONE32; s_wb[i] = NONE64; s_it[i] = NONE64; }
     if (tid == 0) s_nk = 0;
     if (tid < 2) { s_benc[tid] = NONE64; s_bslot[tid] = NONE32; s_nkk[tid] = 0; }
@@ -634,7 +682,7 @@ __device__ __forceinline__ void scan_round(const ScanArgs& a, const ScanParams& 
 #pragma unroll
             for (int j = 0; j < PER_LANE; j++) {
                 const uint32_t m = P.mt(j);
-                const uint32_t nrep = meta_nrep(m), nin = meta_nin(m), set = meta_set(m);
+                const uint32_t nrep = meta_nrep(m), nin = meta_nin(m), set = set_of<RC, LSETS>(P, j);
                 const uint32_t nelig = LSETS ? (uint32_t)((const uint16_t*)(s_set + (size_t)set * U))[0]
                                              : (ld32(a.setrec + (size_t)set * U) & 0xFFFFu);
                 const bool ok = base + j < a.shard_end && meta_elig(m) && nrep > 0 && nelig > nin;
@@ -683,7 +731,7 @@ __device__ __forceinline__ void scan_round(const ScanArgs& a, const ScanParams& 
 #pragma unroll
             for (int k = 0; k < RC; k++) reps[k] = P.rp(k, j);
             int nelig;
-            const int tb0 = first_target<RC, LSETS>(a, s_set, m, reps, nrep, &nelig);
+            const int tb0 = first_target<RC, LSETS>(a, s_set, set_of<RC, LSETS>(P, j), reps, nrep, &nelig);
             const bool ok = base + j < a.shard_end && meta_elig(m) && nrep > 0 && tb0 >= 0;
             const double delta = P.wt(j) * inv_avg;
             const double dt = dtgt_f(s_rf[tb0 >= 0 ? tb0 : 0], delta);
@@ -732,7 +780,7 @@ __device__ __forceinline__ void scan_round(const ScanArgs& a, const ScanParams& 
 #pragma unroll
                 for (int k = 0; k < RC; k++) reps[k] = P.rp(k, j);
                 int nelig;
-                const int tb = first_target<RC, LSETS>(a, s_set, m, reps, nrep, &nelig);
+                const int tb = first_target<RC, LSETS>(a, s_set, set_of<RC, LSETS>(P, j), reps, nrep, &nelig);
                 if (tb < 0) continue;
                 const double delta = P.wt(j) * inv_avg;
                 const double dt = dtgt_f(s_rf[tb], delta);
@@ -756,7 +804,7 @@ __device__ __forceinline__ void scan_round(const ScanArgs& a, const ScanParams& 
                 uint32_t src = reps[0];
 #pragma unroll
                 for (int q2 = 1; q2 < RC; q2++) src = k == q2 ? reps[q2] : src;
-                const int nrep = (int)meta_nrep(m), set = (int)meta_set(m);
+                const int nrep = (int)meta_nrep(m), set = (int)set_of<RC, LSETS>(P, j);
                 uint4 R[U];
                 set_record<RC, LSETS>(a, s_set, (uint32_t)set, R);
                 const double ds = dsrc_f(s_rf[src], w * inv_avg);
@@ -798,12 +846,12 @@ __device__ __forceinline__ void scan_round(const ScanArgs& a, const ScanParams& 
     // compiler waits for exactly the older unit's loads: vmcnt(N), not vmcnt(0))
     for (long long k = 0; c0 >= 0; k += 2) {
         const long long c1 = unit(k + 1);
-        load_parts<RC>(a, (c1 >= 0 ? c1 : c0) + lofs, Bq);
+        load_parts<RC, LSETS>(a, (c1 >= 0 ? c1 : c0) + lofs, Bq);
         score(A, c0 + lofs);
         nu++;
         if (c1 < 0) break;
         const long long c2 = unit(k + 2);
-        load_parts<RC>(a, (c2 >= 0 ? c2 : c1) + lofs, A);
+        load_parts<RC, LSETS>(a, (c2 >= 0 ? c2 : c1) + lofs, A);
         score(Bq, c1 + lofs);
         nu++;
         c0 = c2;
@@ -916,18 +964,50 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
     DevCtl* ctl = a.ctl;
     if (a.listwg && (int)blockIdx.x == a.nscan) { if (!(a.dbg & 8)) do_list_op(ctl, a.L, &s_li); return; }
     const unsigned long long t_in = wall_clock64();
+    // the control words the round reads do not change while a scan runs (it writes only
+    // the spill counters, the timing interval and the list flags): read through the
+    // constant address space, they are scalar loads on lgkmcnt, outside the in-order
+    // vmcnt queue of the table and tile loads (the launch's acquire makes the last
+    // k_step's writes visible to the scalar cache)
+    typedef const __attribute__((address_space(4))) DevCtl* CtlK;
+    const CtlK cc = (CtlK)ctl;
     // a conditional bound pass returns at once unless a bound is open: decided before
     // any partition word is loaded (it runs before every scan once a plan retried)
     if (a.ubpass) {
-        const double ubL = ctl->ub[0], ubN = ctl->ub[1];
+        const double ubL = cc->ub[0], ubN = cc->ub[1];
         if (!(ubN == HUGE_VAL || (a.allow_leader && ubL == HUGE_VAL))) return;
     }
-    // every load that does not depend on the control block goes out first: the
-    // first tile's stream, then the lookup tables (one memory round trip)
-    // (incremental mode: the control block decides first whether the tiles are read)
+    // One round trip: the control words, the lookup tables and the first tile, issued in
+    // that order in one straight-line block (no short-circuit between the control words,
+    // clamped indices): vmcnt drains in issue order, so a load behind a branch on an
+    // earlier load's value would wait for everything issued before it -- the first tile
+    // included -- and each such split costs a round trip per workgroup.
+    // (incremental kernel: the control block decides first whether the tiles are read)
+    ScanParams q;
+    const int c_halted = cc->halted, c_prepped = cc->prepped, c_steps = cc->steps, c_budget = cc->budget;
+    q.inv_avg = cc->inv_avg; q.eps = cc->eps;
+    q.ubL = cc->ub[0]; q.ubN = cc->ub[1];
+    q.heavy = cc->heavy; q.nblm = cc->nblm;
+    q.tk_on = cc->tk_on;
+    q.rlo = cc->rlo; q.rhi = cc->rhi;
+    const int c_incr_ok = cc->incr_ok, c_ub_sub = cc->ub_sub;
+    const double c_wskip = cc->wskip;
+    TabRaw TR;
+    const int nu = LSETS ? a.nsets * sr_units(RC) : 0;
+    TR.pre = a.B <= SCAN_THREADS && nu <= SCAN_THREADS;
+    if (TR.pre) {
+        const int i = min((int)threadIdx.x, a.B - 1);
+        TR.r = ldd(a.r + i);
+        TR.pos = (int32_t)ld32(a.posm + i);
+        TR.blm = (int32_t)ld32(a.blm + i);
+        if (LSETS) TR.set = ldobj(a.setrec + ((int)threadIdx.x < nu ? (int)threadIdx.x : 0));
+    }
     PartRaw<RC> A;
     const long long a0 = a.shard_begin + (long long)blockIdx.x * TILE + (long long)threadIdx.x * PER_LANE;
-    if (!INCR && (int)blockIdx.x < a.ntiles) load_parts<RC>(a, a0, A);
+    // (unconditional: a branch here would make the table loads wait for the tile's;
+    // every scanning workgroup has a tile, and the arrays are padded by two tiles)
+    if (!INCR) load_parts<RC, LSETS>(a, (int)blockIdx.x < a.ntiles ? a0 : a.shard_begin + (long long)threadIdx.x * PER_LANE, A);
+    __builtin_amdgcn_sched_barrier(0);                 // (no use of a control word moves above the loads)
     // incremental kernel: this wave's first block descriptor goes out with the control
     // block; the block's partition words follow as soon as both are in (two round trips
     // before the first score, none of them behind the table staging)
@@ -935,25 +1015,19 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
     d0.wmax = -1.0; d0.blk = 0;
     const long long i0 = (long long)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) * a.nscan + blockIdx.x;
     if (INCR && i0 < a.nblk) d0 = ldobj(a.bdesc + i0);
-    ScanParams q;
-    q.run = ctl->halted == H_RUN && ctl->prepped && ctl->steps < ctl->budget;
-    q.inv_avg = ctl->inv_avg; q.eps = ctl->eps;
-    q.ubL = ctl->ub[0]; q.ubN = ctl->ub[1];
-    q.heavy = ctl->heavy; q.nblm = ctl->nblm;
-    q.tk_on = ctl->tk_on;
-    q.rlo = ctl->rlo; q.rhi = ctl->rhi;
+    q.run = c_halted == H_RUN && c_prepped && c_steps < c_budget;
     q.ubpass = 0;
     // (a conditional bound pass launched on the block list of the last records' best
     // keys: those blocks only, when k_step left one, else every tile)
-    q.incr = INCR && (a.ubpass ? ctl->ub_sub > 0 : ctl->incr_ok);
-    q.wskip = INCR && !a.ubpass ? ctl->wskip : 0.0;
+    q.incr = INCR && (a.ubpass ? c_ub_sub > 0 : c_incr_ok);
+    q.wskip = INCR && !a.ubpass ? c_wskip : 0.0;
     long long c0 = -1;
-    if (INCR && !q.incr && (int)blockIdx.x < a.ntiles) load_parts<RC>(a, a0, A);
+    if (INCR && !q.incr && (int)blockIdx.x < a.ntiles) load_parts<RC, LSETS>(a, a0, A);
     if (INCR && q.incr && d0.wmax >= q.wskip) {
         c0 = d0.blk * BLK;
-        load_parts<RC>(a, c0 + (long long)(threadIdx.x & 63) * PER_LANE, A);
+        load_parts<RC, LSETS>(a, c0 + (long long)(threadIdx.x & 63) * PER_LANE, A);
     }
-    scan_round<RC, LSETS, INCR>(a, q, smem, A, t_in, (int)blockIdx.x, c0);
+    scan_round<RC, LSETS, INCR>(a, q, smem, A, TR, t_in, (int)blockIdx.x, c0);
 }
 
 // --------------------------------------------------------------- k_step
@@ -983,7 +1057,7 @@ __device__ __forceinline__ double cont_delta_ld(const double* s_ld, const Conten
 // every near-tie contender of `kind` within 4*eps of g: the keys of the
 // records whose minimum is within 8*eps, then the raw spill buffer
 template <typename F>
-__device__ void for_each_contender(const StepArgs& a, const double* s_ld, uint32_t ncont, int kind, double g,
+__device__ __forceinline__ void for_each_contender(const StepArgs& a, const double* s_ld, uint32_t ncont, int kind, double g,
                                    double eps, double inv_avg, F f) {
     const int nt = blockDim.x;
     for (int i = threadIdx.x; i < a.R.n; i += nt) {
@@ -1040,6 +1114,22 @@ __device__ double incr_wskip(double rlo, double rhi, double thr, double avg, dou
     return ws * iav <= best ? ws : 0.0;
 }
 
+// Copy nbytes (16-B granules; the source is readable to the next granule) from global
+// memory to LDS by LDS-DMA: global_load_lds_dwordx4 moves 1 KB per wave instruction
+// without registers and without a wait per load.  Chunk c of all the copies of one
+// staging pass goes to wave (k + c) % nw; returns the next chunk number.  The caller
+// waits with s_waitcnt vmcnt(0) and a barrier before reading.
+__device__ __forceinline__ int dma_lds(void* dst, const void* src, int nbytes, int k, int wid, int lane, int nw) {
+    typedef __attribute__((address_space(3))) void lds_void;
+    for (int c = 0; c * 1024 < nbytes; c++, k++) {
+        if (k % nw != wid) continue;
+        const int off = c * 1024 + lane * 16;
+        if (off < nbytes)
+            __builtin_amdgcn_global_load_lds((const char*)src + off, (lds_void*)((char*)dst + c * 1024), 16, 0, 0);
+    }
+    return k;
+}
+
 // the control block lives in LDS for the whole k_step (one load round trip at the
 // start, stores only at the end): the serial code never waits on a global RMW
 constexpr int CTL_WORDS = (int)(offsetof(DevCtl, stamps) / 4);
@@ -1047,28 +1137,32 @@ constexpr int CTL_WORDS = (int)(offsetof(DevCtl, stamps) / 4);
 // The serial half of one Balance() step (k_step): stage the control block, the
 // broker tables and the allowed-set words in LDS, resolve the scan records (when
 // prepped), apply the change and prep the next step.
+template <bool BIG>
 __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
     DevCtl* ctl = a.ctl;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     constexpr int NW = STEP_THREADS / 64;
     const unsigned long long t_in = wall_clock64();
     KB_STAMP_BEGIN();
-    if (tid < CTL_WORDS) ((uint32_t*)&C)[tid] = ((const uint32_t*)ctl)[tid];
     auto write_back = [&]() {
         KB_STAMP_FLUSH(ctl);
         __syncthreads();
         if (tid == 0 && C.tk_on) {
-            // kernel timing: this launch, and the scan that ran before it (if any)
+            // kernel timing: this launch (the scan's interval was folded in at the start:
+            // a load here would wait for every store this thread issued)
             C.tk_sum[1] += wall_clock64() - t_in;
             C.tk_n[1]++;
-            const unsigned long long b = ctl->ts_beg, e = ctl->ts_end;
-            if (b != NONE64 && e > b) { C.tk_sum[0] += e - b; C.tk_n[0]++; }
-            ctl->ts_beg = NONE64;
-            ctl->ts_end = 0;
         }
         __syncthreads();
         if (tid < CTL_WORDS) ((uint32_t*)ctl)[tid] = ((const uint32_t*)&C)[tid];
     };
+    // diagnostic phase stops: a -DKB_STOP_AT=k build returns after phase k (the code
+    // after it is dead there); kb_engine_bench_step times such builds on a fixed input
+#ifdef KB_STOP_AT
+#define KB_STOP(k) do { if ((k) == KB_STOP_AT) { write_back(); return; } } while (0)
+#else
+#define KB_STOP(k) (void)0
+#endif
     __shared__ Decision D;
     __shared__ int s_done, s_i, s_exact_need, s_retry, s_nT, s_unc, s_nblm;
     __shared__ unsigned long long s_u[NW];
@@ -1101,22 +1195,23 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
     Dedup T{s_key, s_wb, s_it, DEDUP_STEP, s_nd, s_li};
     const int B = a.B;
 
-    // ---- one memory round trip: the broker state, the allowed-set words, the control
-    // block and (speculatively: the buffer always exists) the first record's header
-    for (int b = tid; b < B; b += STEP_THREADS) {
-        s_ld[b] = a.load[b];
-        s_e[b] = a.eb[b];
-        s_fl[b] = a.bfl[b];
-        s_ord[b] = a.order[b];
+    // ---- one memory round trip: the control block, the broker state and the allowed-set
+    // words go straight to LDS by LDS-DMA (global_load_lds_dwordx4: 1 KB per wave
+    // instruction, no registers, no wait per load -- a plain load-then-LDS-write loop
+    // waits for each load before issuing the next, one round trip per iteration, and
+    // holding the values in registers instead costs the later phases their VGPRs); one
+    // vmcnt wait before the first barrier.  The record headers come to registers.
+    const unsigned long long ts_b = ctl->ts_beg, ts_e = ctl->ts_end;   // (kernel timing, tk_on)
+    {
+        int k = 0;                                    // chunk counter: chunks dealt round-robin to the waves
+        k = dma_lds(&C, ctl, CTL_WORDS * 4, k, wid, lane, NW);
+        k = dma_lds(s_ld, a.load, B * 8, k, wid, lane, NW);
+        k = dma_lds(s_e, a.eb, B * 8, k, wid, lane, NW);
+        k = dma_lds(s_ord, a.order, B * 4, k, wid, lane, NW);
+        k = dma_lds(s_fl, a.bfl, B, k, wid, lane, NW);
+        if (a.sb_lds) dma_lds(s_sb, a.setbits, a.nsets * a.W64 * 8, k, wid, lane, NW);
     }
     KB_STAMP(ctl, 23);
-    if (a.sb_lds) {
-        const int nq = a.nsets * a.W64;                   // 16-B loads (the rows are contiguous)
-        for (int q = 2 * tid; q < nq; q += 2 * STEP_THREADS) {
-            if (q + 1 < nq) *(uint4*)(s_sb + q) = *(const uint4*)(a.setbits + q);
-            else s_sb[q] = a.setbits[q];
-        }
-    }
     KB_STAMP(ctl, 27);
     double hd0 = HUGE_VAL, hd1 = HUGE_VAL;
     unsigned long long hc0 = 0, hc1 = 0;
@@ -1132,7 +1227,15 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
     KB_STAMP(ctl, 28);
     dedup_clear(T);
     if (tid < 2) { s_nd[tid] = 0; s_li[tid] = -1; s_kfail[tid] = 0; }
+    __builtin_amdgcn_s_waitcnt(0);                 // (the LDS-DMA copies: vmcnt covers them)
     __syncthreads();                               // the control block copy
+    if (tid == 0 && C.tk_on) {
+        // kernel timing: the interval of the scan that ran before this launch (if any)
+        const unsigned long long b = ts_b, e = ts_e;
+        if (b != NONE64 && e > b) { C.tk_sum[0] += e - b; C.tk_n[0]++; }
+        ctl->ts_beg = NONE64;
+        ctl->ts_end = 0;
+    }
     const int halted = C.halted;
     const bool do_res = C.prepped && C.steps < C.budget;
     const double eps = C.eps, inv_avg = C.inv_avg, U0h = C.U0;
@@ -1153,6 +1256,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
     hb0.s = hb1.s = -1;
     if (do_res && tid < a.R.n) { hb0 = ldobj(&a.R.h(tid)->best[0]); hb1 = ldobj(&a.R.h(tid)->best[1]); }
     KB_STAMP(ctl, 12);
+    KB_STOP(1);
     // ---- the scan records (or the gathered rank summaries): one per thread, reduced
     // per wave with DPP and across the waves by wave 0; then every thread collects
     // its record's near-tie keys of both kinds within 4*eps of the minima (distinct
@@ -1205,6 +1309,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
         }
         __syncthreads();
         const double g0 = s_g[0], g1 = s_g[1];
+    KB_STOP(2);
         if (s_fm) {
             // some record holds a first-index predicate (the plan is not in shape yet)
             uint32_t f[NF];
@@ -1275,6 +1380,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
     }
     __syncthreads();
     KB_STAMP(ctl, 14);
+    KB_STOP(3);
     if (do_res && a.use_spill && C.ncont > 0) {
         // raw spills of the scan (rare): every thread
         const uint32_t n = min(C.ncont, a.cont_cap);
@@ -1382,7 +1488,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
                 } else if (F[F_REMOVE] != NONE32) {                      // steps.go:70-89
                     const uint32_t p = F[F_REMOVE];
                     const uint32_t m = a.meta[p];
-                    const int nrep = (int)meta_nrep(m), set = (int)meta_set(m);
+                    const int nrep = (int)meta_nrep(m), set = (int)(BIG && a.pset ? a.pset[p] : meta_set(m));
                     const uint64_t* sb = a.setbits + (size_t)set * a.W64;
                     // lightest allowed replica in (load, id) order = smallest universe position
                     int best = -1, bslot = -1, bpos = 0x7FFFFFFF;
@@ -1421,7 +1527,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
                 // over the brokers holding replicas (Disallowed, utils.go:81-90)
                 const uint32_t p = s_lpart;
                 const uint32_t m = a.meta[p];
-                const int nrep = (int)meta_nrep(m), set = (int)meta_set(m);
+                const int nrep = (int)meta_nrep(m), set = (int)(BIG && a.pset ? a.pset[p] : meta_set(m));
                 if (wid == 0) {
                     if (lane < nrep) s_lrep[lane] = (int)a.rep[(long long)lane * a.Ppad + p];
                     const unsigned long long sbw = lane < a.W64 ? (unsigned long long)a.setbits[(size_t)set * a.W64 + lane] : 0ull;
@@ -1717,6 +1823,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
         // inside the set, so the meta word is unchanged and only the source and the
         // target change (contribution W, or W * (len(R) + NumConsumers) at slot 0)
         KB_STAMP(ctl, 11);
+    KB_STOP(4);
         if (wid == 0) {
             int nT = 0;
             const bool chg = D.status == 1;
@@ -1767,7 +1874,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
                 upd = true;
             } else {
                 int ro = -1;                                 // old replica at slot `lane`
-                uint32_t m = 0;
+                uint32_t m = 0, setx = 0;
                 double wv = 0.0;
                 int ncp = 0;
                 if (chg) {
@@ -1775,6 +1882,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
                     m = a.meta[p];
                     wv = a.w[p];
                     ncp = a.nc[p];
+                    setx = BIG && a.pset ? a.pset[p] : meta_set(m);
                 }
                 const int nrep = (int)meta_nrep(m);
                 if (lane >= nrep) ro = -1;
@@ -1805,7 +1913,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
                     bool in = false;
                     if (lane < nw) {
                         // (typed LDS pointer: the two loads must not merge into one flat load)
-                        const size_t wi = (size_t)meta_set(m) * a.W64 + (rn >> 6);
+                        const size_t wi = (size_t)setx * a.W64 + (rn >> 6);
                         const uint64_t wd = a.sb_lds ? ((const __attribute__((address_space(3))) uint64_t*)s_sb)[wi]
                                                      : a.setbits[wi];
                         in = (wd >> (rn & 63)) & 1ull;
@@ -1924,6 +2032,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
         __syncthreads();
         if (D.status != 1) { write_back(); return; }
         KB_STAMP(ctl, 5);
+    KB_STOP(5);
     }
 
     // ================================================================== prep
@@ -2023,6 +2132,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
         }
         __syncthreads();                                // #1
         KB_STAMP(ctl, 6);
+    KB_STOP(6);
         // ---- P2.  sum waves (and any wave holding a record's best keys): avg, r, U0 /
         // V / Rm partials, the upper bound; order waves: the new positions
         int nb[NQ], np[NQ];
@@ -2122,6 +2232,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
         }
         __syncthreads();                                // #2
         KB_STAMP(ctl, 8);
+    KB_STOP(7);
         // ---- P3.  order waves: scatter into the new order; wave 0: the step totals,
         // eps and the control block; wave 1: the list of marked sets
         if (ot >= 0 && nT > 0) {
@@ -2191,6 +2302,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
         }
         __syncthreads();                                // #3
         KB_STAMP(ctl, 9);
+    KB_STOP(8);
         // ---- P4.  bl_move = brokers present in the load map or listed in -broker-ids
         // (steps.go:150-157), interleaved (position i = q * STEP_THREADS + tid): order
         // and position writes, order certification, bl_move counts per 64 positions
@@ -2223,6 +2335,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
         }
         __syncthreads();                                // #4
         KB_STAMP(ctl, 16);
+    KB_STOP(9);
         if (s_unc) {
             if (tid == 0) { C.halted = H_NEED_EXACT; C.prepped = 0; C.total_exact_halts++; }
             write_back();
@@ -2252,6 +2365,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
             if (tid == 0 && nblm == 0) { C.light = -1; C.heavy = -1; }
         }
         KB_STAMP(ctl, 19);
+    KB_STOP(10);
         // ---- P5.  set records of the marked sets (steps.go:192-201 targets): each wave
         // rebuilds G records at a time so their LDS chains overlap
         for (;;) {
@@ -2323,6 +2437,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
             __syncthreads();
         }
         KB_STAMP(ctl, 20);
+    KB_STOP(11);
         if (tid == 0) { C.prepped = 1; C.full_prep = 0; }
         write_back();
         return;
@@ -2564,8 +2679,12 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
     }
     }
     KB_STAMP(ctl, 9);
-    // ---- set records: full, or the sets containing a touched broker
-    for (int w = tid; !marked && w < (a.nsets + 31) / 32; w += STEP_THREADS) {
+    // ---- set records: full, or the sets containing a touched broker.  Past MAX_SETS sets
+    // (the LDS bitmap's capacity) the sets come as a list instead: every set, or the
+    // touched brokers' set lists (a set in two of them is rebuilt twice, identically)
+    const bool bigm = BIG && a.nsets > (int)MAX_SETS;
+    __shared__ int s_bo[TMAX + 1], s_bb[TMAX];
+    for (int w = tid; !bigm && !marked && w < (a.nsets + 31) / 32; w += STEP_THREADS) {
         const int rem = a.nsets - w * 32;                 // only bits of existing sets
         s_smark[w] = full ? (rem >= 32 ? 0xFFFFFFFFu : (1u << rem) - 1u) : 0u;
     }
@@ -2585,7 +2704,6 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
         }
     } else if (!full) {
         // two memory round trips: the touched brokers' set-list extents, then the lists
-        __shared__ int s_bo[TMAX + 1], s_bb[TMAX];
         if (tid < nT) {
             const int t = s_T[tid];
             const int o0 = a.bset_off[t], o1 = a.bset_off[t + 1];
@@ -2603,7 +2721,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
         }
         __syncthreads();
         const int tot = s_bo[nT];
-        for (int q = tid; q < tot; q += STEP_THREADS) {
+        for (int q = tid; !bigm && q < tot; q += STEP_THREADS) {
             int x = 0;
             while (x + 1 < nT && s_bo[x + 1] <= q) x++;
             const int set = a.bset_ids[s_bb[x] + q - s_bo[x]];
@@ -2629,8 +2747,24 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
         __shared__ __align__(16) uint16_t s_rs[NW][G][8 * MAXU];
         if (tid == 0) s_cursor = 0;
         __syncthreads();
-        while (s_cursor < nwords) {
-            if (wid == 0) {
+        const int lim = bigm ? (full ? a.nsets : s_bo[nT]) : nwords;
+        while (s_cursor < lim) {
+            const int c0 = s_cursor;
+            int bn = 0;
+            if (bigm) {
+                // the next CH sets of the list
+                bn = min(CH, lim - c0);
+                for (int q = tid; q < bn; q += STEP_THREADS) {
+                    int set = c0 + q;
+                    if (!full) {
+                        int x = 0;
+                        while (x + 1 < nT && s_bo[x + 1] <= set) x++;
+                        set = a.bset_ids[s_bb[x] + set - s_bo[x]];
+                    }
+                    s_mlist[q] = set;
+                }
+                if (tid == 0) s_mn = bn;
+            } else if (wid == 0) {
                 // the next marked sets, up to CH, in set order
                 int n = 0, w = s_cursor;
                 while (w < nwords) {
@@ -2653,6 +2787,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
             }
             __syncthreads();
             KB_STAMP(ctl, 19);
+            if (bigm && tid == 0) s_cursor = c0 + bn;      // (every thread has read the old cursor)
             const int mn = s_mn;
             if (!a.sb_lds) {
                 for (int q = tid; q < mn * W64; q += STEP_THREADS) {
@@ -2742,9 +2877,12 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
     write_back();
 }
 
+// (BIG: more broker lists than the meta word's set field / the LDS mark bitmap hold --
+// a separate instantiation, so the common kernel's register allocation is untouched)
+template <bool BIG>
 __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
     __shared__ DevCtl C;
-    step_body(a, C);
+    step_body<BIG>(a, C);
 }
 
 // ------------------------------------------------------------- k_listop
@@ -3025,13 +3163,17 @@ void launch_touch(double* r, int B, int32_t* blm, int32_t* posm, uint4* setrec, 
 }
 
 int step_static_lds() {
-    hipFuncAttributes fa;
-    if (hipFuncGetAttributes(&fa, (const void*)k_step) != hipSuccess) return -1;
-    return (int)fa.sharedSizeBytes;
+    hipFuncAttributes fa, fb;
+    if (hipFuncGetAttributes(&fa, (const void*)k_step<false>) != hipSuccess) return -1;
+    if (hipFuncGetAttributes(&fb, (const void*)k_step<true>) != hipSuccess) return -1;
+    return (int)(fa.sharedSizeBytes > fb.sharedSizeBytes ? fa.sharedSizeBytes : fb.sharedSizeBytes);
 }
 
 void launch_step(const StepArgs& a, hipStream_t st) {
-    hipLaunchKernelGGL(k_step, dim3(1), dim3(STEP_THREADS), a.lds_bytes, st, a);
+    if (a.pset && a.nsets > (int)MAX_SETS)
+        hipLaunchKernelGGL(k_step<true>, dim3(1), dim3(STEP_THREADS), a.lds_bytes, st, a);
+    else
+        hipLaunchKernelGGL(k_step<false>, dim3(1), dim3(STEP_THREADS), a.lds_bytes, st, a);
 }
 void launch_listop(DevCtl* ctl, const Lists& L, hipStream_t st) {
     hipLaunchKernelGGL(k_listop, dim3(1), dim3(1024), 0, st, ctl, L);

@@ -42,6 +42,7 @@ struct ScanArgs {
     int incr;                 // incremental mode: block descriptors (DevCtl.incr_ok decides per step)
     int nblk;
     const BlockDesc* bdesc;
+    const uint32_t* pset;     // [Ppad] allowed-set index per partition (set records in memory only)
 };
 
 struct StepArgs {
@@ -80,6 +81,7 @@ struct StepArgs {
     int incr;                 // incremental mode (single GPU): decide DevCtl.incr_ok / wskip
     BlockDesc* ubdesc;        // [2 * R.n] the blocks of the records' best keys (bound pass subset)
     int ub_heavy;             // 1: ubdesc also lists the heaviest blocks (the subset is never empty)
+    const uint32_t* pset;     // [Ppad] allowed-set index per partition, or null (the meta word's field)
 };
 
 struct RefreshArgs {

@@ -23,7 +23,7 @@ KIND_NAMES = {0: "none", 1: "replace", 2: "remove", 3: "add", 4: "swap"}
 
 EXPORTS = ["kb_abi_version", "kb_engine_create", "kb_engine_balance", "kb_engine_plan",
            "kb_engine_replicas", "kb_engine_loads", "kb_engine_unbalance", "kb_engine_stats",
-           "kb_engine_timings", "kb_engine_set_timing", "kb_engine_stamps", "kb_engine_bench_scan",
+           "kb_engine_timings", "kb_engine_set_timing", "kb_engine_stamps", "kb_engine_bench_scan", "kb_engine_bench_step",
            "kb_engine_last_error", "kb_engine_destroy", "kb_engine_summary_bytes",
            "kb_engine_step_begin", "kb_engine_step_finish", "kb_engine_set_stream",
            "kb_engine_sharded_reset", "kb_engine_sharded_scan", "kb_engine_sharded_resolve",
@@ -99,6 +99,9 @@ def lib():
         L.kb_engine_stamps.restype = C.c_int
         L.kb_engine_bench_scan.argtypes = [vp, C.c_int, PD]
         L.kb_engine_bench_scan.restype = C.c_int
+        if hasattr(L, "kb_engine_bench_step"):          # (diagnostic; older builds in A/B runs lack it)
+            L.kb_engine_bench_step.argtypes = [vp, C.c_int, PD]
+            L.kb_engine_bench_step.restype = C.c_int
         L.kb_engine_last_error.argtypes = [vp, C.c_char_p, C.c_size_t]
         L.kb_engine_last_error.restype = C.c_int
         L.kb_engine_destroy.argtypes = [vp]
@@ -349,6 +352,14 @@ class Engine:
         out = np.zeros(32, np.int64)
         lib().kb_engine_stamps(self.h, out.ctypes.data_as(P64), 32)
         return out.tolist()
+
+    def bench_step(self, iters=100):
+        """Diagnostic: k_step alone on a fixed input (us per launch; phase costs from -DKB_STOP_AT builds)."""
+        v = C.c_double()
+        rc = lib().kb_engine_bench_step(self.h, iters, C.byref(v))
+        if rc != 0:
+            raise EngineError(rc, self.last_error())
+        return v.value
 
     def bench_scan(self, iters=100):
         """Diagnostic: average k_scan device time (us) on the current state."""

@@ -329,3 +329,42 @@ def test_candidate_count_first_step():
         nin = inset[rows].sum(axis=1)
         want += int(((n_elig - nin) * 2).sum())
     assert cand == want
+
+
+# ------------------------------------------------- many distinct broker lists
+# More distinct `Brokers` lists than the meta word's 15-bit set field holds (and than
+# fit in LDS): the scan reads the per-partition set index array and the set records
+# from memory, k_step rebuilds the records from list-driven chunks (utils.go:66-90,
+# steps.go:117-143; the reference has no such limit).
+
+def _many_sets_plist(seed, P, B, disallowed=0.0, nrvar=0.0):
+    rng = random.Random(seed)
+    parts = []
+    for i in range(P):
+        reps = rng.sample(range(1, B + 1), 3)
+        extra = rng.sample([b for b in range(1, B + 1) if b not in reps], rng.randint(2, 5))
+        allowed = list(reps) + extra
+        if disallowed and rng.random() < disallowed:
+            allowed.remove(reps[rng.randint(0, 2)])      # a replica outside the list
+        p = {"topic": "t%d" % (i % 5), "partition": i, "replicas": reps,
+             "weight": rng.uniform(1, 1e6) ** -1.1, "brokers": sorted(allowed)}
+        if nrvar and rng.random() < nrvar:
+            p["num_replicas"] = rng.choice([2, 4])
+        parts.append(p)
+    return {"version": 1, "partitions": parts}
+
+
+@pytest.mark.parametrize("variant", ["moves", "disallowed", "add_remove"])
+def test_many_distinct_broker_lists(variant):
+    P, B = 100_000, 200
+    pl = _many_sets_plist(7, P, B, disallowed=0.0005 if variant == "disallowed" else 0.0,
+                          nrvar=0.0003 if variant == "add_remove" else 0.0)
+    nsets = len({tuple(p["brokers"]) for p in pl["partitions"]})
+    assert nsets > 90_000, nsets                     # past the 15-bit field (32767) and LDS
+    cfg = default_cfg(allow_leader=True, min_unbalance=0.0)
+    ech = check_plan(pl, cfg, 25)
+    assert len(ech) == 25
+    if variant == "disallowed":
+        assert any(c["step"] == "MoveDisallowedReplicas" for c in ech)
+    if variant == "add_remove":
+        assert {"RemoveExtraReplicas", "AddMissingReplicas"} & {c["step"] for c in ech}

@@ -9,4 +9,17 @@ for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY 
   timeout -k 5 -s KILL 150 rocprofv3 --kernel-trace --pmc $grp --output-format csv -d gpurun_out/${TAG}_p$i -o run \
       -- python3 bench.py --steps 200 --warmup 5 --no-cpu-baseline > gpurun_out/${TAG}_p$i.log 2>&1 || { echo "pass $i failed rc=$?"; tail -5 gpurun_out/${TAG}_p$i.log; exit 1; }
 done
-exit 0
+
+python3 - "$TAG" <<'PY'
+import csv, glob, collections, sys
+tag = sys.argv[1]
+for p in ("%s_p1" % tag, "%s_p2" % tag):
+    acc = collections.defaultdict(lambda: collections.defaultdict(list))
+    for f in glob.glob("gpurun_out/%s/**/*counter_collection.csv" % p, recursive=True):
+        for r in csv.DictReader(open(f)):
+            k = r["Kernel_Name"].split("(")[0][-14:]
+            acc[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    for k, d in acc.items():
+        if "k_step" in k or "k_scan" in k:
+            print(p, k, {c: round(sum(v) / len(v), 1) for c, v in d.items()})
+PY
