@@ -54,6 +54,7 @@ struct kb_engine {
     hipStream_t st = nullptr;
     bool own_st = false;
     int64_t P = 0, Ppad = 0, B = 0, nsets = 0, ntiles = 0, nscan = 0;
+    int twaves = SCAN_THREADS / 64;
     int rcap = 0, rc_dev = 1, K = 3, KR = 6, units = 1, W64 = 1, NP2 = 64;
     int sb_lds = 0, step_lds_bytes = 0;     // k_step: resident allowed-set words, dynamic LDS
     int sem = KB_SEM_APPLIED, allow_leader = 0, rebalance = 0;
@@ -371,7 +372,6 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
         delete e;
         return KB_ERR_INVALID;
     }
-    e->ntiles = (e->shard_end - e->shard_begin + TILE - 1) / TILE;
     // padding: the last tile of the shard may read up to TILE past shard_end
     e->Ppad = ((n + TILE - 1) / TILE) * TILE + 2 * TILE;
 
@@ -471,6 +471,17 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
     // one wave of resident workgroups; each loops over its tiles
     int per_cu = scan_blocks_per_cu(e->rc_dev, e->lds_sets, e->scan_lds);
     if (per_cu < 1) per_cu = 1;
+    // a tile is twaves blocks of BLK partitions, one per scoring wave: the full 16 when the
+    // shard fills every resident workgroup slot with whole tiles, fewer on small shards
+    // (c2's 10k partitions: 79 workgroups of one scoring wave instead of 5 of 16 -- the
+    // census walks of an all-ties cluster spread over 79 CUs)
+    {
+        const int64_t nblk = (e->shard_end - e->shard_begin + BLK - 1) / BLK;
+        const int64_t slots = (int64_t)per_cu * ncu;
+        e->twaves = (int)std::max<int64_t>(1, std::min<int64_t>(SCAN_THREADS / 64, nblk / std::max<int64_t>(slots, 1)));
+        if (const char* v = getenv("KB_TWAVES")) if (atoi(v) > 0) e->twaves = std::min(atoi(v), SCAN_THREADS / 64);  // diagnostic
+        e->ntiles = (nblk + e->twaves - 1) / e->twaves;
+    }
     e->nscan = std::min<int64_t>(e->ntiles, (int64_t)per_cu * ncu);
     if (const char* v = getenv("KB_NSCAN")) if (atoi(v) > 0) e->nscan = std::min<int64_t>(e->ntiles, atoi(v));  // diagnostic
     if (const char* v = getenv("KB_DEBUG_SCAN")) e->dbg_scan = atoi(v);                                   // diagnostic
@@ -590,7 +601,7 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
 static void fill_scan_args(kb_engine* e, ScanArgs& s) {
     s.ctl = e->ctl; s.w = e->w; s.rep = e->rep; s.meta = e->meta;
     s.Ppad = e->Ppad; s.shard_begin = e->shard_begin; s.shard_end = e->shard_end;
-    s.ntiles = (int)e->ntiles; s.nscan = (int)e->nscan;
+    s.ntiles = (int)e->ntiles; s.nscan = (int)e->nscan; s.twaves = e->twaves;
     s.B = (int)e->B; s.nsets = (int)e->nsets; s.W64 = e->W64; s.units = e->units;
     s.setbits = e->setbits; s.setrec = e->setrec; s.r = e->r; s.blm = e->blm; s.posm = e->posm;
     s.allow_leader = e->allow_leader; s.rebalance = e->rebalance; s.sem_go = e->sem == KB_SEM_GO;

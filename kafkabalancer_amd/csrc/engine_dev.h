@@ -8,7 +8,10 @@ namespace kbe {
 
 constexpr int MAXB = 4096;          // dense broker universe limit (sorted in LDS)
 constexpr int MAXR = 16;            // replica slots per partition
-constexpr int SCAN_THREADS = 1024;  // k_scan workgroup (one per CU)
+#ifndef KB_SCAN_THREADS
+#define KB_SCAN_THREADS 1024
+#endif
+constexpr int SCAN_THREADS = KB_SCAN_THREADS;  // k_scan workgroup (one per CU at 1024)
 constexpr int PER_LANE = 2;         // consecutive partitions per lane (vector loads)
 constexpr int TILE = SCAN_THREADS * PER_LANE;   // 2048 partitions per scan tile
 constexpr int SHARD_ALIGN = 1024;   // shard boundaries (multi-GPU) are multiples of this

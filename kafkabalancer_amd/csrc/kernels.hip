@@ -832,7 +832,7 @@ __device__ __forceinline__ void scan_round(const ScanArgs& a, const ScanParams& 
     auto unit = [&](long long k) -> long long {     // base of this wave's k-th unit, or -1
         if (!INCR || !q.incr) {
             const long long t = (long long)tile + k * a.nscan;
-            return t < a.ntiles ? a.shard_begin + t * TILE + (long long)widu * BLK : -1;
+            return t < a.ntiles && widu < a.twaves ? a.shard_begin + t * ((long long)a.twaves * BLK) + (long long)widu * BLK : -1;
         }
         const long long i = i0 + k * istep;
         if (i >= a.nblk) return -1;
@@ -1003,10 +1003,13 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
         if (LSETS) TR.set = ldobj(a.setrec + ((int)threadIdx.x < nu ? (int)threadIdx.x : 0));
     }
     PartRaw<RC> A;
-    const long long a0 = a.shard_begin + (long long)blockIdx.x * TILE + (long long)threadIdx.x * PER_LANE;
+    const bool own0 = (int)blockIdx.x < a.ntiles && (int)(threadIdx.x >> 6) < a.twaves;
+    const long long a0 = own0 ? a.shard_begin + (long long)blockIdx.x * a.twaves * BLK + (long long)threadIdx.x * PER_LANE
+                              : a.shard_begin + (long long)threadIdx.x * PER_LANE;
     // (unconditional: a branch here would make the table loads wait for the tile's;
-    // every scanning workgroup has a tile, and the arrays are padded by two tiles)
-    if (!INCR) load_parts<RC, LSETS>(a, (int)blockIdx.x < a.ntiles ? a0 : a.shard_begin + (long long)threadIdx.x * PER_LANE, A);
+    // every scanning wave has a first unit, an idle wave loads the shard's first tile,
+    // and the arrays are padded by two tiles)
+    if (!INCR) load_parts<RC, LSETS>(a, a0, A);
     __builtin_amdgcn_sched_barrier(0);                 // (no use of a control word moves above the loads)
     // incremental kernel: this wave's first block descriptor goes out with the control
     // block; the block's partition words follow as soon as both are in (two round trips
@@ -1022,7 +1025,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
     q.incr = INCR && (a.ubpass ? c_ub_sub > 0 : c_incr_ok);
     q.wskip = INCR && !a.ubpass ? c_wskip : 0.0;
     long long c0 = -1;
-    if (INCR && !q.incr && (int)blockIdx.x < a.ntiles) load_parts<RC, LSETS>(a, a0, A);
+    if (INCR && !q.incr && own0) load_parts<RC, LSETS>(a, a0, A);
     if (INCR && q.incr && d0.wmax >= q.wskip) {
         c0 = d0.blk * BLK;
         load_parts<RC, LSETS>(a, c0 + (long long)(threadIdx.x & 63) * PER_LANE, A);
@@ -1114,21 +1117,9 @@ __device__ double incr_wskip(double rlo, double rhi, double thr, double avg, dou
     return ws * iav <= best ? ws : 0.0;
 }
 
-// Copy nbytes (16-B granules; the source is readable to the next granule) from global
-// memory to LDS by LDS-DMA: global_load_lds_dwordx4 moves 1 KB per wave instruction
-// without registers and without a wait per load.  Chunk c of all the copies of one
-// staging pass goes to wave (k + c) % nw; returns the next chunk number.  The caller
-// waits with s_waitcnt vmcnt(0) and a barrier before reading.
-__device__ __forceinline__ int dma_lds(void* dst, const void* src, int nbytes, int k, int wid, int lane, int nw) {
-    typedef __attribute__((address_space(3))) void lds_void;
-    for (int c = 0; c * 1024 < nbytes; c++, k++) {
-        if (k % nw != wid) continue;
-        const int off = c * 1024 + lane * 16;
-        if (off < nbytes)
-            __builtin_amdgcn_global_load_lds((const char*)src + off, (lds_void*)((char*)dst + c * 1024), 16, 0, 0);
-    }
-    return k;
-}
+#ifndef KB_CLIST
+#define KB_CLIST 1   // exact folds over a compact contender list (0: the table walk only; A/B)
+#endif
 
 // the control block lives in LDS for the whole k_step (one load round trip at the
 // start, stores only at the end): the serial code never waits on a global RMW
@@ -1196,20 +1187,23 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
     const int B = a.B;
 
     // ---- one memory round trip: the control block, the broker state and the allowed-set
-    // words go straight to LDS by LDS-DMA (global_load_lds_dwordx4: 1 KB per wave
-    // instruction, no registers, no wait per load -- a plain load-then-LDS-write loop
-    // waits for each load before issuing the next, one round trip per iteration, and
-    // holding the values in registers instead costs the later phases their VGPRs); one
-    // vmcnt wait before the first barrier.  The record headers come to registers.
+    // words (plain loads then LDS writes: at B <= 1024 one load of each array per thread,
+    // all issued before the first LDS write; measured faster than LDS-DMA of the same
+    // bytes, 16.5 vs 19.9 us per k_step at c3).  The record headers come to registers.
     const unsigned long long ts_b = ctl->ts_beg, ts_e = ctl->ts_end;   // (kernel timing, tk_on)
-    {
-        int k = 0;                                    // chunk counter: chunks dealt round-robin to the waves
-        k = dma_lds(&C, ctl, CTL_WORDS * 4, k, wid, lane, NW);
-        k = dma_lds(s_ld, a.load, B * 8, k, wid, lane, NW);
-        k = dma_lds(s_e, a.eb, B * 8, k, wid, lane, NW);
-        k = dma_lds(s_ord, a.order, B * 4, k, wid, lane, NW);
-        k = dma_lds(s_fl, a.bfl, B, k, wid, lane, NW);
-        if (a.sb_lds) dma_lds(s_sb, a.setbits, a.nsets * a.W64 * 8, k, wid, lane, NW);
+    if (tid < CTL_WORDS) ((uint32_t*)&C)[tid] = ((const uint32_t*)ctl)[tid];
+    for (int b = tid; b < B; b += STEP_THREADS) {
+        s_ld[b] = a.load[b];
+        s_e[b] = a.eb[b];
+        s_fl[b] = a.bfl[b];
+        s_ord[b] = a.order[b];
+    }
+    if (a.sb_lds) {
+        const int nq = a.nsets * a.W64;                   // 16-B loads (the rows are contiguous)
+        for (int q = 2 * tid; q < nq; q += 2 * STEP_THREADS) {
+            if (q + 1 < nq) *(uint4*)(s_sb + q) = *(const uint4*)(a.setbits + q);
+            else s_sb[q] = a.setbits[q];
+        }
     }
     KB_STAMP(ctl, 23);
     KB_STAMP(ctl, 27);
@@ -1227,7 +1221,6 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
     KB_STAMP(ctl, 28);
     dedup_clear(T);
     if (tid < 2) { s_nd[tid] = 0; s_li[tid] = -1; s_kfail[tid] = 0; }
-    __builtin_amdgcn_s_waitcnt(0);                 // (the LDS-DMA copies: vmcnt covers them)
     __syncthreads();                               // the control block copy
     if (tid == 0 && C.tk_on) {
         // kernel timing: the interval of the scan that ran before this launch (if any)
@@ -1688,6 +1681,41 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
                     exact = 1;
                     // exact su on wave 0 while the other waves fold the contenders
                     stage_exact();
+                    // the contenders of this kind as a compact list with their bl positions
+                    // (one pass over the key table by every thread and one round trip for the
+                    // positions, instead of each fold wave walking the 2048 table slots and
+                    // loading its contender's positions itself); kept in the set-mark words,
+                    // which only the prep uses.  More than CLMAX keys: the table walk below.
+                    constexpr int CLMAX = 640;
+                    uint16_t* s_cl = (uint16_t*)s_smark;
+                    int16_t* s_cps = (int16_t*)(s_cl + CLMAX);
+                    int16_t* s_cpt = s_cps + CLMAX;
+                    static_assert(3 * CLMAX * 2 <= (int)sizeof(s_smark), "contender list fits the mark words");
+                    static_assert(DEDUP_STEP == 2 * STEP_THREADS, "two table slots per thread");
+                    __shared__ int s_cwc[NW], s_ncl;
+                    if (KB_CLIST && !fail && ndist != 1 && have) {
+                        const int h0 = tid, h1 = tid + STEP_THREADS;
+                        const bool v0 = s_key[h0] != NONE32 && (int)(s_key[h0] >> 30) == kind;
+                        const bool v1 = s_key[h1] != NONE32 && (int)(s_key[h1] >> 30) == kind;
+                        const unsigned long long m0 = __ballot(v0), m1 = __ballot(v1);
+                        const unsigned long long lt = (1ull << lane) - 1ull;
+                        if (lane == 0) s_cwc[wid] = (int)(__popcll(m0) + __popcll(m1));
+                        __syncthreads();
+                        const int wc = lane < NW ? s_cwc[lane] : 0;
+                        const int woff = wave_sum(lane < wid ? wc : 0), tot = wave_sum(wc);
+                        if (tot <= CLMAX) {
+                            auto put = [&](int pos, int h) {
+                                s_cl[pos] = (uint16_t)h;
+                                const uint32_t k = s_key[h];
+                                s_cps[pos] = (int16_t)(int32_t)ld32(a.posm + ((k >> 15) & 0x7FFF));
+                                s_cpt[pos] = (int16_t)(int32_t)ld32(a.posm + (k & 0x7FFF));
+                            };
+                            if (v0) put(woff + (int)__popcll(m0 & lt), h0);
+                            if (v1) put(woff + (int)__popcll(m0) + (int)__popcll(m1 & lt), h1);
+                        }
+                        if (tid == 0) s_ncl = tot;
+                        __syncthreads();
+                    }
                     if (wid == 0) su_wave();
                     if (!fail && ndist == 1) {
                         if (wid == 1) {
@@ -1709,7 +1737,18 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
                         auto better = [&](double u, const Contender& c) {
                             if (u < bu || (u == bu && c.iter < bi)) { bu = u; bi = c.iter; bs = c.s; bt = c.t; bw = c.w; }
                         };
-                        if (!fail) {
+                        if (KB_CLIST && !fail && s_ncl <= CLMAX) {
+                            // one contender per wave (waves 1..NW-1) from the compact list
+                            const int ncl = s_ncl;
+                            if (wid > 0)
+                                for (int i = wid - 1; i < ncl; i += NW - 1) {
+                                    const Contender c = dedup_entry(T, (int)s_cl[i]);
+                                    const double u = exact_unbalance_wave(s_Lm, nblm0, (int)s_cps[i], (int)s_cpt[i],
+                                                                          s_ld[c.s] - c.w, s_ld[c.t] + c.w, s_fold + 64 * wid);
+                                    if (lane == 0) nf++;
+                                    better(u, c);
+                                }
+                        } else if (!fail) {
                             // one contender per wave (waves 1..NW-1; the table slot is wave-uniform)
                             if (wid > 0)
                                 for (int h = wid - 1; h < DEDUP_STEP; h += NW - 1) {

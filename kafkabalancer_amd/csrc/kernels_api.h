@@ -21,7 +21,8 @@ struct ScanArgs {
     const uint16_t* rep;      // [RC][Ppad] slot-major dense broker ids
     const uint32_t* meta;     // [Ppad]
     long long Ppad, shard_begin, shard_end;
-    int ntiles, nscan;        // tiles of TILE partitions; workgroups that scan
+    int ntiles, nscan;        // tiles of twaves * BLK partitions; workgroups that scan
+    int twaves;               // waves of a workgroup that score (a tile's blocks; the rest idle)
     int B, nsets, W64, units; // units: 16-B words per set record
     const uint64_t* setbits;
     const uint4* setrec;
