@@ -177,7 +177,11 @@ def drop_in(args):
         with open(jpath, "wb") as f:
             f.write(json.dumps(synth.to_plist(cl), separators=(",", ":")).encode())
         gen_s = time.perf_counter() - t0
-        cmd = [cli_bin, "-input-json", "-input", jpath, "-max-reassign", str(args.cli_reassign)]
+        # -complete-partition defaults to true (balancer.go:30): past -max-reassign the
+        # reference keeps stepping until the last partition is complete, which on c3's
+        # MoveLeaders ping-pong never happens -- the drop-in run turns it off
+        cmd = [cli_bin, "-input-json", "-input", jpath, "-max-reassign", str(args.cli_reassign),
+               "-complete-partition=false"]
         if cfg.get("allow_leader"):
             cmd.append("-allow-leader")
         cmd += ["-min-unbalance", repr(float(cfg.get("min_unbalance", 0.01)))]

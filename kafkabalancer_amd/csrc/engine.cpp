@@ -116,6 +116,8 @@ struct kb_engine {
     double kms[TK_N] = {0, 0, 0};
     int64_t klaunch[TK_N] = {0, 0, 0};
     int64_t refreshes = 0;
+    bool rf_stream = false;        // in-stream refreshes (ScanArgs.rfpass / StepArgs.rf_final)
+    RefreshArgs* rf_dev = nullptr; // the refresh's arguments in device memory (ScanArgs.rf)
     int dbg_scan = 0;
     int incr = 0;                  // incremental mode (kb_engine_set_incremental)
     BlockDesc* bdesc = nullptr;    // partition blocks of the shard by wmax descending
@@ -160,6 +162,8 @@ template <typename T>
 static hipError_t dalloc(T** p, size_t n) {
     return hipMalloc((void**)p, (n ? n : 1) * sizeof(T));
 }
+
+static int upload_rf(kb_engine* e);   // (step launch section)
 
 static const int kRcChoices[] = {1, 2, 3, 4, 6, 8, 12, 16};
 
@@ -468,6 +472,10 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
     e->lds_sets = setbytes <= (size_t)LDS_SETS_MAX;
     const size_t pbytes = ((size_t)e->B * 2 + 15) & ~(size_t)15;
     e->scan_lds = rbytes + 2 * pbytes + (e->lds_sets ? setbytes : 0) + dedup;
+    // (room for the in-stream refresh's two fold buffers: ScanArgs.rfpass)
+    e->rf_stream = !e->integral;
+    if (const char* v = getenv("KB_RF_STREAM")) if (*v == '0') e->rf_stream = false;   // diagnostic
+    if (e->rf_stream) e->scan_lds = std::max(e->scan_lds, (size_t)RF_LDS_BYTES);
     // one wave of resident workgroups; each loops over its tiles
     int per_cu = scan_blocks_per_cu(e->rc_dev, e->lds_sets, e->scan_lds);
     if (per_cu < 1) per_cu = 1;
@@ -577,6 +585,7 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
             HIPCHK(hipMemcpy(e->L.lcap, hlc.data(), hlc.size() * 4, hipMemcpyHostToDevice));
         }
         HIPCHK(hipMemcpy(e->L.lent, hle.data(), hle.size() * 4, hipMemcpyHostToDevice));
+        if (const int rc = upload_rf(e); rc != KB_OK) { *out = e; return rc; }
     }
     DevCtl z;
     memset(&z, 0, sizeof z);
@@ -598,6 +607,22 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
 
 // ---------------------------------------------------------- step launch
 
+static void fill_refresh_args(kb_engine* e, RefreshArgs& ra) {
+    ra.ctl = e->ctl; ra.w = e->w; ra.rep = e->rep; ra.meta = e->meta; ra.nc = e->nc;
+    ra.load = e->load; ra.lerr = e->lerr; ra.eb = e->eb; ra.bfl = e->bfl; ra.B = (int)e->B;
+    ra.L = e->L;
+}
+
+// the refresh arguments as the in-stream refresh reads them (after create and relist)
+static int upload_rf(kb_engine* e) {
+    if (e->integral) return KB_OK;
+    RefreshArgs ra;
+    fill_refresh_args(e, ra);
+    if (!e->rf_dev) HIPCHK(dalloc(&e->rf_dev, 1));
+    HIPCHK(hipMemcpy(e->rf_dev, &ra, sizeof ra, hipMemcpyHostToDevice));
+    return KB_OK;
+}
+
 static void fill_scan_args(kb_engine* e, ScanArgs& s) {
     s.ctl = e->ctl; s.w = e->w; s.rep = e->rep; s.meta = e->meta;
     s.Ppad = e->Ppad; s.shard_begin = e->shard_begin; s.shard_end = e->shard_end;
@@ -613,6 +638,8 @@ static void fill_scan_args(kb_engine* e, ScanArgs& s) {
     s.L = e->L;
     s.incr = e->incr; s.nblk = (int)e->nblk; s.bdesc = e->bdesc;
     s.pset = e->pset;
+    s.rfpass = 0;
+    s.rf = e->rf_dev;
 }
 
 static void fill_step_args(kb_engine* e, StepArgs& a, const Recs& R, int use_spill) {
@@ -634,6 +661,7 @@ static void fill_step_args(kb_engine* e, StepArgs& a, const Recs& R, int use_spi
     a.ubdesc = e->ubdesc;
     a.ub_heavy = e->nubdesc > 2 * std::max<int64_t>(e->nscan, STEP_THREADS) ? 1 : 0;
     a.pset = e->pset;
+    a.rf_final = 0;
 }
 
 static const int kStepBatch = 64;
@@ -669,20 +697,22 @@ static void harvest(kb_engine* e) {
     e->tev_used = 0;
 }
 
-static void enqueue_scan(kb_engine* e) {
+static void enqueue_scan(kb_engine* e, bool rf = false) {
     if (e->nscan == 0 && e->integral) return;
     ScanArgs s;
     fill_scan_args(e, s);
+    s.rfpass = rf && e->rf_stream && e->nscan > 0;
     if (e->nscan == 0) s.listwg = 1;
     launch_scan(s, e->rc_dev, e->lds_sets, e->scan_lds, e->st);
 }
 
 // the first step after a full prep has no best keys to bound its minimum: a
 // census-free scan (no list op) plus k_ubinit sets ub to the step's own minima
-static void enqueue_ubinit(kb_engine* e) {
+static void enqueue_ubinit(kb_engine* e, bool rf = false) {
     if (e->nscan == 0) return;
     ScanArgs s;
     fill_scan_args(e, s);
+    s.rfpass = rf && e->rf_stream;
     s.listwg = 0;
     s.dbg |= 1;
     s.ubpass = 1;
@@ -695,18 +725,21 @@ static void enqueue_ubinit(kb_engine* e) {
     launch_ubinit(e->ctl, scan_recs(e->recs, (int)e->nscan), e->allow_leader, e->st);
 }
 
-static void enqueue_step(kb_engine* e) {
+static void enqueue_step(kb_engine* e, bool rf = false) {
     StepArgs a;
     fill_step_args(e, a, scan_recs(e->recs, (int)e->nscan), 1);
+    a.rf_final = rf && e->rf_stream && e->nscan > 0;
     launch_step(a, e->st);
 }
 
 // one Balance(): scan (if prepped) then resolve + apply + prep of the next step
-static void enqueue_pair(kb_engine* e) {
+// (rf: this pair may follow a step halted for exact loads: the pair's first scan launch
+// refolds the loads and its k_step resumes; rf_scan: the main scan is that first launch)
+static void enqueue_pair(kb_engine* e, bool rf = false, bool rf_scan = false) {
     mark(e, TK_SCAN);
-    enqueue_scan(e);
+    enqueue_scan(e, rf && rf_scan);
     mark(e, TK_STEP);
-    enqueue_step(e);
+    enqueue_step(e, rf);
 }
 
 // Lay the per-broker partition lists out again from the device's partition words
@@ -745,6 +778,7 @@ static int relist(kb_engine* e) {
     HIPCHK(hipMemcpy(e->L.lstart, hls.data(), hls.size() * 4, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(e->L.llen, hll.data(), hll.size() * 4, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(e->L.lcap, hlc.data(), hlc.size() * 4, hipMemcpyHostToDevice));
+    if (const int rc = upload_rf(e); rc != KB_OK) return rc;
     e->relists++;
     return KB_OK;
 }
@@ -766,9 +800,7 @@ static int refresh(kb_engine* e) {
         HIPCHK(hipMemcpy(e->ctl, &c, sizeof c, hipMemcpyHostToDevice));
     }
     RefreshArgs ra;
-    ra.ctl = e->ctl; ra.w = e->w; ra.rep = e->rep; ra.meta = e->meta; ra.nc = e->nc;
-    ra.load = e->load; ra.lerr = e->lerr; ra.eb = e->eb; ra.bfl = e->bfl; ra.B = (int)e->B;
-    ra.L = e->L;
+    fill_refresh_args(e, ra);
     mark(e, TK_REFRESH);
     launch_refresh(ra, e->st);
     mark(e, -1);
@@ -933,8 +965,11 @@ static int run_steps(kb_engine* e, int64_t max_steps) {
         for (int64_t s = 0; s < pairs; s++) {
             // pair 0 ran the full prep; once a step had to re-scan (no surviving best
             // keys bound the next minimum), every scan gets the conditional bound pass
-            if ((s == 1 && !prepped) || (e->ub_mode && (s > 0 || prepped))) enqueue_ubinit(e);
-            enqueue_pair(e);
+            // (a halt for exact loads in pair s - 1 is refolded by pair s's first scan launch)
+            const bool ubp = (s == 1 && !prepped) || (e->ub_mode && (s > 0 || prepped));
+            const bool rf = s > 0;
+            if (ubp) enqueue_ubinit(e, rf);
+            enqueue_pair(e, rf, !ubp);
         }
         mark(e, -1);
         HIPCHK(hipGetLastError());
@@ -1087,7 +1122,7 @@ extern "C" int kb_engine_stats(kb_engine* e, kb_stats* o) {
     o->n_sets = e->nsets;
     o->integral = e->integral ? 1 : 0;
     o->max_replicas = e->rc_dev;
-    o->refreshes = e->refreshes;
+    o->refreshes = e->refreshes + (int64_t)c.total_rf_stream;
     o->exact_halts = (int64_t)c.total_exact_halts;
     o->scan_workgroups = e->nscan;
     o->retries = (int64_t)c.total_retries;
@@ -1291,7 +1326,7 @@ extern "C" void kb_engine_destroy(kb_engine* e) {
     void* ptrs[] = {e->w, e->rep, e->meta, e->pset, e->nc, e->load, e->lerr, e->eb, e->bfl, e->cnt,
                     e->setbits, e->setrec, e->order, e->posu, e->blm, e->posm, e->r,
                     e->bset_off, e->bset_ids, e->recs, e->cont, e->ctl, e->log, e->bdesc, e->ubdesc,
-                    e->L.lstart, e->L.llen, e->L.lcap, e->L.lent};
+                    e->L.lstart, e->L.llen, e->L.lcap, e->L.lent, e->rf_dev};
     for (void* p : ptrs) if (p) hipFree(p);
     if (e->h_ctl) hipHostFree(e->h_ctl);
     if (e->h_log) hipHostFree(e->h_log);

@@ -32,6 +32,8 @@ constexpr int SUMMARY_KEYS_MAX = 2048;
 constexpr int DEDUP_STEP = 2048;    // LDS key table of k_step / k_summary
 constexpr int DEDUP_SCAN = 256;     // LDS key table of one k_scan workgroup
 constexpr int TMAX = 2 * MAXR + 4;  // brokers touched by one applied change (bound)
+constexpr int RF_CHUNK = 2048;       // in-stream refresh: contributions per fold chunk (two buffers)
+constexpr int RF_LDS_BYTES = 2 * RF_CHUNK * 8;
 constexpr int BLK = 128;            // partitions of one wave in a scan tile = one block of
                                     // the incremental mode (64 lanes x PER_LANE)
 
@@ -195,6 +197,8 @@ struct DevCtl {
     unsigned long long total_blocks;    // partition blocks the incremental scans read
     double rlo, rhi;                    // range of r[] (every broker; k_step's prep): the scan's
                                         // lower-bound prune reads it instead of reducing r[]
+    unsigned long long total_rf_stream; // exact refolds run in the stream (the next pair's first
+                                        // scan refolds, its k_step resumes: no host round trip)
     // diagnostic phase stamps (builds with -DKB_STAMPS): accumulated
     // shader-clock ticks (clock64) per phase of k_step; [24]/[25] the wall-clock
     // (100 MHz) and shader-clock length of k_step; [26] one stamp's own cost

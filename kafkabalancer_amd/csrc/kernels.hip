@@ -957,12 +957,27 @@ __device__ __forceinline__ void scan_round(const ScanArgs& a, const ScanParams& 
     }
 }
 
+__device__ __attribute__((noinline)) void refresh_in_scan(const RefreshArgs* rfp, int pend, int kind, int from, int to,
+                                                          uint32_t part, double* buf);   // (k_refresh below)
+
 template <int RC, bool LSETS, bool INCR>
 __global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
     extern __shared__ __align__(16) unsigned char smem[];
     __shared__ int s_li;
     DevCtl* ctl = a.ctl;
-    if (a.listwg && (int)blockIdx.x == a.nscan) { if (!(a.dbg & 8)) do_list_op(ctl, a.L, &s_li); return; }
+    // (rfpass: if the last k_step halted for exact loads, this launch is the refresh,
+    // refresh_in_scan; the scanning workgroups decide with their control words below)
+    auto rf_run = [&]() {
+        refresh_in_scan(a.rf, ctl->pending_list, ctl->pl_kind, ctl->pl_from, ctl->pl_to, (uint32_t)ctl->pl_part,
+                        (double*)smem);
+    };
+    if (a.listwg && (int)blockIdx.x == a.nscan) {
+        // (the pending list edit of a step halted for exact loads waits for its refresh)
+        const int h = ctl->halted;
+        if (a.rfpass && h == H_NEED_EXACT && !ctl->list_overflow) rf_run();
+        else if (!(a.dbg & 8) && h != H_NEED_EXACT) do_list_op(ctl, a.L, &s_li);
+        return;
+    }
     const unsigned long long t_in = wall_clock64();
     // the control words the round reads do not change while a scan runs (it writes only
     // the spill counters, the timing interval and the list flags): read through the
@@ -975,7 +990,11 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
     // any partition word is loaded (it runs before every scan once a plan retried)
     if (a.ubpass) {
         const double ubL = cc->ub[0], ubN = cc->ub[1];
-        if (!(ubN == HUGE_VAL || (a.allow_leader && ubL == HUGE_VAL))) return;
+        const int h = cc->halted, lovf = cc->list_overflow;
+        if (!(ubN == HUGE_VAL || (a.allow_leader && ubL == HUGE_VAL))) {
+            if (a.rfpass && h == H_NEED_EXACT && !lovf) rf_run();
+            return;
+        }
     }
     // One round trip: the control words, the lookup tables and the first tile, issued in
     // that order in one straight-line block (no short-circuit between the control words,
@@ -990,7 +1009,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
     q.heavy = cc->heavy; q.nblm = cc->nblm;
     q.tk_on = cc->tk_on;
     q.rlo = cc->rlo; q.rhi = cc->rhi;
-    const int c_incr_ok = cc->incr_ok, c_ub_sub = cc->ub_sub;
+    const int c_incr_ok = cc->incr_ok, c_ub_sub = cc->ub_sub, c_lovf = cc->list_overflow;
     const double c_wskip = cc->wskip;
     TabRaw TR;
     const int nu = LSETS ? a.nsets * sr_units(RC) : 0;
@@ -1019,6 +1038,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
     const long long i0 = (long long)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) * a.nscan + blockIdx.x;
     if (INCR && i0 < a.nblk) d0 = ldobj(a.bdesc + i0);
     q.run = c_halted == H_RUN && c_prepped && c_steps < c_budget;
+    if (a.rfpass && c_halted == H_NEED_EXACT && !c_lovf) { rf_run(); return; }   // (the tile loads are dropped)
     q.ubpass = 0;
     // (a conditional bound pass launched on the block list of the last records' best
     // keys: those blocks only, when k_step left one, else every tile)
@@ -1222,6 +1242,20 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
     dedup_clear(T);
     if (tid < 2) { s_nd[tid] = 0; s_li[tid] = -1; s_kfail[tid] = 0; }
     __syncthreads();                               // the control block copy
+    {
+        // this pair's first scan refolded the loads of a step halted for exact loads
+        // (refresh_in_scan): resume as the host's refresh would, with a full prep
+        const bool rfin = a.rf_final && C.halted == H_NEED_EXACT && !C.list_overflow;
+        if (rfin) {
+            __syncthreads();
+            if (tid == 0) {
+                C.halted = H_RUN; C.prepped = 0; C.full_prep = 1; C.ndirty = 0; C.want_refresh = 0;
+                C.pending_list = 0;
+                C.total_rf_stream++;
+            }
+            __syncthreads();
+        }
+    }
     if (tid == 0 && C.tk_on) {
         // kernel timing: the interval of the scan that ran before this launch (if any)
         const unsigned long long b = ts_b, e = ts_e;
@@ -2938,34 +2972,46 @@ __global__ __launch_bounds__(1024) void k_listop(DevCtl* ctl, Lists L) {
 
 constexpr int REFRESH_THREADS = 256;
 constexpr int REFRESH_CHUNK = 1024;
-// One workgroup per dirty broker: the exact getBrokerLoad fold (utils.go:92-105) of its
-// contributions in partition order.  Double-buffered: while wave 0 folds chunk j (a
-// broadcast-LDS chain, one dependent add each), waves 1.. gather
-// chunk j + 1 from the partition list.
-__global__ __launch_bounds__(REFRESH_THREADS) void k_refresh(RefreshArgs a) {
-    const int b = blockIdx.x;
-    if (b >= a.B || !(a.bfl[b] & BF_DIRTY)) return;
-    __shared__ __align__(16) double s_c[2][REFRESH_CHUNK];
+// The exact getBrokerLoad fold (utils.go:92-105) of broker b's contributions in partition
+// order by one workgroup of NT threads (every thread calls; the result is wave 0's).
+// Double-buffered: while wave 0 folds chunk j (a broadcast-LDS add chain), waves 1..
+// gather chunk j + 1 from the partition list -- every list load of a thread first, then
+// the partition words they index, then the LDS writes (two round trips per chunk, not
+// two per element).  buf: 2 * CH doubles of LDS.
+template <int NT, int CH>
+__device__ __forceinline__ double refold_broker(const RefreshArgs& a, int b, double* buf) {
+    constexpr int GT = NT - 64, PER = (CH + GT - 1) / GT;
     const uint32_t st = a.L.lstart[b], n = a.L.llen[b];
     const int tid = threadIdx.x, wid = tid >> 6;
-    auto gather = [&](uint32_t c0, double* dst, int t0, int nt) {
-        const uint32_t m = n - c0 < (uint32_t)REFRESH_CHUNK ? n - c0 : (uint32_t)REFRESH_CHUNK;
-        for (uint32_t i = (uint32_t)t0; i < m; i += (uint32_t)nt) {
-            const uint32_t q = a.L.lent[st + c0 + i];
-            const uint32_t mq = a.meta[q];
-            const double w = a.w[q];
-            // slot 0 carries the leader weight W * (len(R) + NumConsumers)
-            dst[i] = (a.rep[q] == (uint16_t)b) ? w * (double)((int)meta_nrep(mq) + a.nc[q]) : w;
+    auto gather = [&](uint32_t c0, double* dst) {
+        const int t = tid - 64;
+        uint32_t q[PER];
+#pragma unroll
+        for (int k = 0; k < PER; k++) {
+            const uint32_t i = (uint32_t)(t + k * GT);
+            q[k] = i < (uint32_t)CH && c0 + i < n ? a.L.lent[st + c0 + i] : NONE32;
         }
+        double w[PER];
+        uint32_t mq[PER];
+        int32_t ncq[PER];
+        uint16_t r0[PER];
+#pragma unroll
+        for (int k = 0; k < PER; k++) {
+            const uint32_t qq = q[k] != NONE32 ? q[k] : 0u;
+            w[k] = a.w[qq]; mq[k] = a.meta[qq]; ncq[k] = a.nc[qq]; r0[k] = a.rep[qq];
+        }
+#pragma unroll
+        for (int k = 0; k < PER; k++)
+            if (q[k] != NONE32)   // slot 0 carries the leader weight W * (len(R) + NumConsumers)
+                dst[t + k * GT] = r0[k] == (uint16_t)b ? w[k] * (double)((int)meta_nrep(mq[k]) + ncq[k]) : w[k];
     };
     double acc = 0.0;
-    if (n) gather(0, s_c[0], tid, REFRESH_THREADS);
+    if (wid > 0 && n) gather(0, buf);
     __syncthreads();
-    for (uint32_t c0 = 0, j = 0; c0 < n; c0 += REFRESH_CHUNK, j++) {
-        const uint32_t m = n - c0 < (uint32_t)REFRESH_CHUNK ? n - c0 : (uint32_t)REFRESH_CHUNK;
-        if (wid > 0 && c0 + REFRESH_CHUNK < n)
-            gather(c0 + REFRESH_CHUNK, s_c[(j + 1) & 1], tid - 64, REFRESH_THREADS - 64);
-        if (wid == 0) acc = chain_lds(acc, (const lds_f64*)s_c[j & 1], (int)m);
+    for (uint32_t c0 = 0, j = 0; c0 < n; c0 += CH, j++) {
+        const uint32_t m = n - c0 < (uint32_t)CH ? n - c0 : (uint32_t)CH;
+        if (wid > 0 && c0 + CH < n) gather(c0 + CH, buf + ((j + 1) & 1) * CH);
+        if (wid == 0) acc = chain_lds(acc, (const lds_f64*)(buf + (j & 1) * CH), (int)m);
         __syncthreads();
     }
     if (tid == 0) {
@@ -2973,6 +3019,48 @@ __global__ __launch_bounds__(REFRESH_THREADS) void k_refresh(RefreshArgs a) {
         a.lerr[b] = gamma_n((int)n) * acc;
         a.eb[b] = 0.0;
         a.bfl[b] = a.bfl[b] & ~BF_DIRTY;
+    }
+    return acc;
+}
+
+// One workgroup per dirty broker (the host's refresh after a batch halted for exact loads)
+__global__ __launch_bounds__(REFRESH_THREADS) void k_refresh(RefreshArgs a) {
+    const int b = blockIdx.x;
+    if (b >= a.B || !(a.bfl[b] & BF_DIRTY)) return;
+    __shared__ __align__(16) double s_c[2 * REFRESH_CHUNK];
+    refold_broker<REFRESH_THREADS, REFRESH_CHUNK>(a, b, s_c);
+}
+
+// The same refresh inside the stream: the first scan launch of the pair after a k_step
+// that halted for exact loads (ScanArgs.rfpass) refolds the dirty brokers instead of
+// scanning -- workgroup 0 first applies the pending per-broker list edit and then folds
+// the edited lists' brokers itself; every workgroup folds the dirty brokers of its
+// grid stride -- and the pair's k_step resumes with a full prep (StepArgs.rf_final).
+// No host round trip, and the pairs enqueued behind the halt do real steps.  (The
+// arguments come from device memory, not the kernel-argument struct: a by-value copy
+// passed to this call would give every scan wave a stack frame.)
+__device__ __attribute__((noinline)) void refresh_in_scan(const RefreshArgs* rfp, int pend, int kind, int from, int to,
+                                                          uint32_t part, double* buf) {
+    const RefreshArgs rf = *rfp;
+    __shared__ int s_i;
+    const int g = blockIdx.x, ng = gridDim.x;
+    const bool ef = pend && kind != 3 && from >= 0, et = pend && kind != 2 && to >= 0;
+    if (g == 0 && pend) {
+        bool ok = true;
+        if (kind == 1) { list_remove(rf.L, from, part, &s_i); ok = list_insert(rf.L, to, part, &s_i); }
+        else if (kind == 2) list_remove(rf.L, from, part, &s_i);
+        else if (kind == 3) ok = list_insert(rf.L, to, part, &s_i);
+        if (!ok && threadIdx.x == 0) rf.ctl->list_overflow = 1;   // the host relists (refresh)
+        __syncthreads();
+    }
+    for (int b = g; b < rf.B; b += ng) {
+        if (g != 0 && ((ef && b == from) || (et && b == to))) continue;   // workgroup 0's
+        if (!(rf.bfl[b] & BF_DIRTY)) continue;                           // (uniform)
+        refold_broker<SCAN_THREADS, RF_CHUNK>(rf, b, buf);
+    }
+    if (g == 0) {
+        if (ef && from % ng != 0 && (rf.bfl[from] & BF_DIRTY)) refold_broker<SCAN_THREADS, RF_CHUNK>(rf, from, buf);
+        if (et && to % ng != 0 && to != from && (rf.bfl[to] & BF_DIRTY)) refold_broker<SCAN_THREADS, RF_CHUNK>(rf, to, buf);
     }
 }
 

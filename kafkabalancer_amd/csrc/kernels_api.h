@@ -15,6 +15,20 @@ struct Lists {
     uint32_t* lent;
 };
 
+struct RefreshArgs {
+    DevCtl* ctl;
+    const double* w;
+    const uint16_t* rep;
+    const uint32_t* meta;
+    const int32_t* nc;
+    double* load;
+    double* lerr;
+    double* eb;
+    uint8_t* bfl;
+    int B;
+    Lists L;
+};
+
 struct ScanArgs {
     DevCtl* ctl;
     const double* w;
@@ -39,6 +53,9 @@ struct ScanArgs {
     int ubpass;               // 1: census-free bound pass (k_ubinit follows); returns at once
                               //    unless a relevant upper bound is +inf
     int dbg;                  // diagnostic only (KB_DEBUG_SCAN): 1 = skip the census
+    int rfpass;               // 1: if the last k_step halted for exact loads (H_NEED_EXACT),
+                              //    this launch refolds the dirty brokers instead of scanning
+    const RefreshArgs* rf;    //    (with the pending list edit) and the pair's k_step resumes
     Lists L;
     int incr;                 // incremental mode: block descriptors (DevCtl.incr_ok decides per step)
     int nblk;
@@ -83,21 +100,10 @@ struct StepArgs {
     BlockDesc* ubdesc;        // [2 * R.n] the blocks of the records' best keys (bound pass subset)
     int ub_heavy;             // 1: ubdesc also lists the heaviest blocks (the subset is never empty)
     const uint32_t* pset;     // [Ppad] allowed-set index per partition, or null (the meta word's field)
+    int rf_final;             // 1: a halt for exact loads was refolded by this pair's first scan
+                              //    (rfpass): resume with a full prep
 };
 
-struct RefreshArgs {
-    DevCtl* ctl;
-    const double* w;
-    const uint16_t* rep;
-    const uint32_t* meta;
-    const int32_t* nc;
-    double* load;
-    double* lerr;
-    double* eb;
-    uint8_t* bfl;
-    int B;
-    Lists L;
-};
 
 struct SumArgs {
     DevCtl* ctl;

@@ -182,3 +182,27 @@ def test_uniform_4096_full_size():
     check_moves(ch)
     check_loads(eng, cl, ch)
     eng.close()
+
+
+@pytest.mark.gpu
+def test_in_stream_refresh_matches_host_refresh(monkeypatch):
+    """c5's shape at 1M partitions x 4096 brokers, 150 steps: the steps that halt for exact
+    loads are refolded inside the stream (the next pair's first scan launch refolds the
+    dirty brokers' loads, its k_step resumes with a full prep) -- the same plan, bit for
+    bit, and the same final loads as the host's refresh between batches (KB_RF_STREAM=0),
+    and the loads equal getBrokerLoad of the replayed plan."""
+    cl, cfg, _ = synth.config("c5", scale=0.1)
+    eng = E.Engine(cl, cfg)
+    ch, err = eng.plan(150)
+    assert err is None, err
+    st = eng.stats()
+    monkeypatch.setenv("KB_RF_STREAM", "0")
+    ref = E.Engine(cl, cfg)
+    rch, rerr = ref.plan(150)
+    assert rerr is None, rerr
+    assert st["exact_halts"] > 0 and st["refreshes"] > 0, st
+    assert ch == rch
+    assert eng.loads() == ref.loads()
+    check_loads(eng, cl, ch)
+    eng.close()
+    ref.close()
