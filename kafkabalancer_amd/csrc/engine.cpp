@@ -193,29 +193,46 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
     }
     if (c->partition_id) e->pids.assign(c->partition_id, c->partition_id + n);
 
-    // dense broker universe = sorted unique ids (so dense order == BrokerID order)
-    std::vector<int64_t> all;
+    // dense broker universe = sorted unique ids (so dense order == BrokerID order).
+    // An open-addressing id table (at most MAXB distinct ids, else unsupported) instead of
+    // sorting every replica id: one hash probe per replica (c3: 3M) and a sort of the
+    // few distinct ids.
     int64_t nrep_total = n ? c->replica_off[n] - c->replica_off[0] : 0;
-    all.reserve((size_t)nrep_total + 64);
-    for (int64_t i = 0; i < nrep_total; i++) all.push_back(c->replica_ids[c->replica_off[0] + i]);
+    constexpr uint32_t HCAP = 1u << 14;                  // > 2 * MAXB: short probe chains
+    std::vector<int64_t> hkey(HCAP);
+    std::vector<int32_t> hval(HCAP, -1);
+    std::vector<int64_t> all;
+    all.reserve(MAXB + 1);
+    auto hslot = [&](int64_t id) -> uint32_t {
+        uint64_t x = (uint64_t)id * 0x9E3779B97F4A7C15ull;
+        uint32_t h = (uint32_t)(x >> 50);                // top 14 bits
+        while (hval[h] >= 0 && hkey[h] != id) h = (h + 1) & (HCAP - 1);
+        return h;
+    };
+    auto add_id = [&](int64_t id) {
+        const uint32_t h = hslot(id);
+        if (hval[h] < 0 && (int64_t)all.size() <= MAXB) { hkey[h] = id; hval[h] = 0; all.push_back(id); }
+    };
+    for (int64_t i = 0; i < nrep_total && (int64_t)all.size() <= MAXB; i++) add_id(c->replica_ids[c->replica_off[0] + i]);
     if (c->n_sets > 0 && c->set_off)
-        for (int64_t i = c->set_off[0]; i < c->set_off[c->n_sets]; i++) all.push_back(c->set_ids[i]);
+        for (int64_t i = c->set_off[0]; i < c->set_off[c->n_sets] && (int64_t)all.size() <= MAXB; i++) add_id(c->set_ids[i]);
     if (!cfg->brokers_nil)
-        for (int64_t i = 0; i < cfg->n_brokers; i++) all.push_back(cfg->brokers[i]);
-    std::sort(all.begin(), all.end());
-    all.erase(std::unique(all.begin(), all.end()), all.end());
+        for (int64_t i = 0; i < cfg->n_brokers && (int64_t)all.size() <= MAXB; i++) add_id(cfg->brokers[i]);
     if ((int64_t)all.size() > MAXB) {
         e->last_err = "engine supports at most 4096 distinct brokers";
         *out = e;
         return KB_ERR_UNSUPPORTED;
     }
+    std::sort(all.begin(), all.end());
+    for (size_t i = 0; i < all.size(); i++) hval[hslot(all[i])] = (int)i;
     e->ids = all;
     e->B = (int64_t)all.size();
-    std::unordered_map<int64_t, int> idmap;
-    idmap.reserve(all.size() * 2 + 1);
-    for (size_t i = 0; i < all.size(); i++) idmap[all[i]] = (int)i;
+    auto dense_of = [&](int64_t id) -> int { return hval[hslot(id)]; };
+    // replicas as dense ids, per partition (one lookup per replica, reused below)
+    std::vector<uint16_t> dense((size_t)nrep_total);
+    for (int64_t i = 0; i < nrep_total; i++) dense[i] = (uint16_t)dense_of(c->replica_ids[c->replica_off[0] + i]);
+    auto dn = [&](int64_t i, int k) -> int { return dense[c->replica_off[i] - c->replica_off[0] + k]; };
 
-    // replicas as dense ids, per partition
     std::vector<int> len(n);
     std::vector<double> wt(c->weight, c->weight + n);
     std::vector<int64_t> want(n), ncon(n, 0);
@@ -249,10 +266,12 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
                 e->pending_msg = std::string("ValidateWeights: partition ") + part_string(e, i, reps_of(i)) + " has negative weight";
             }
         }
+        // (duplicates by dense id: the id map is a bijection; pairwise, no allocation)
         for (int64_t i = 0; i < n && !e->pending; i++) {
-            std::vector<int64_t> r = reps_of(i);
-            std::sort(r.begin(), r.end());
-            if (std::adjacent_find(r.begin(), r.end()) != r.end()) {
+            bool dup = false;
+            for (int k = 1; k < len[i] && !dup; k++)
+                for (int q = 0; q < k && !dup; q++) dup = dn(i, k) == dn(i, q);
+            if (dup) {
                 e->pending = KB_ERR_STEP; e->pending_step = 1;
                 e->pending_msg = std::string("ValidateReplicas: partition ") + part_string(e, i, reps_of(i)) + " has duplicated replicas";
             }
@@ -269,16 +288,16 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
     for (int64_t i = 0; i < n; i++) if (!c->set_idx || c->set_idx[i] < 0) need_default = true;
     std::vector<std::vector<int>> sets((size_t)nsets_in + (need_default ? 1 : 0));
     for (int64_t s = 0; s < nsets_in; s++)
-        for (int64_t k = c->set_off[s]; k < c->set_off[s + 1]; k++) sets[s].push_back(idmap[c->set_ids[k]]);
+        for (int64_t k = c->set_off[s]; k < c->set_off[s + 1]; k++) sets[s].push_back(dense_of(c->set_ids[k]));
     int64_t def_set = -1;
     if (need_default) {
         def_set = nsets_in;
         if (!cfg->brokers_nil) {
-            for (int64_t k = 0; k < cfg->n_brokers; k++) sets[def_set].push_back(idmap[cfg->brokers[k]]);
+            for (int64_t k = 0; k < cfg->n_brokers; k++) sets[def_set].push_back(dense_of(cfg->brokers[k]));
         } else {
             // getBrokerList (utils.go:49-64): every broker holding a replica
             std::vector<char> seen(e->B, 0);
-            for (int64_t i = 0; i < nrep_total; i++) seen[idmap[c->replica_ids[c->replica_off[0] + i]]] = 1;
+            for (int64_t i = 0; i < nrep_total; i++) seen[dense[i]] = 1;
             for (int64_t b = 0; b < e->B; b++) if (seen[b]) sets[def_set].push_back((int)b);
         }
     }
@@ -335,11 +354,9 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
     // exact initial loads: getBrokerLoad fold in partition order (utils.go:92-105)
     std::vector<double> ld(e->B, 0.0);
     std::vector<int32_t> cn(e->B, 0);
-    std::vector<uint16_t> dense((size_t)nrep_total);
     for (int64_t i = 0; i < n; i++) {
         for (int k = 0; k < len[i]; k++) {
-            int b = idmap[rid(i, k)];
-            dense[c->replica_off[i] - c->replica_off[0] + k] = (uint16_t)b;
+            const int b = dn(i, k);
             if (k == 0) ld[b] += wt[i] * (double)(len[i] + ncon[i]);
             else ld[b] += wt[i];
             cn[b]++;
@@ -421,7 +438,7 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
     }
     std::vector<uint8_t> hin(e->B, 0);
     if (!cfg->brokers_nil)
-        for (int64_t k = 0; k < cfg->n_brokers; k++) hin[idmap[cfg->brokers[k]]] = 1;
+        for (int64_t k = 0; k < cfg->n_brokers; k++) hin[dense_of(cfg->brokers[k])] = 1;
     // broker -> sets containing it (incremental set-record upkeep)
     std::vector<int32_t> hbo(e->B + 1, 0), hbi;
     {
