@@ -974,7 +974,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
     if (a.listwg && (int)blockIdx.x == a.nscan) {
         // (the pending list edit of a step halted for exact loads waits for its refresh)
         const int h = ctl->halted;
-        if (a.rfpass && h == H_NEED_EXACT && !ctl->list_overflow) rf_run();
+        if (a.rfpass && h == H_NEED_EXACT) rf_run();
         else if (!(a.dbg & 8) && h != H_NEED_EXACT) do_list_op(ctl, a.L, &s_li);
         return;
     }
@@ -990,9 +990,9 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
     // any partition word is loaded (it runs before every scan once a plan retried)
     if (a.ubpass) {
         const double ubL = cc->ub[0], ubN = cc->ub[1];
-        const int h = cc->halted, lovf = cc->list_overflow;
+        const int h = cc->halted;
         if (!(ubN == HUGE_VAL || (a.allow_leader && ubL == HUGE_VAL))) {
-            if (a.rfpass && h == H_NEED_EXACT && !lovf) rf_run();
+            if (a.rfpass && h == H_NEED_EXACT) rf_run();
             return;
         }
     }
@@ -1009,7 +1009,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
     q.heavy = cc->heavy; q.nblm = cc->nblm;
     q.tk_on = cc->tk_on;
     q.rlo = cc->rlo; q.rhi = cc->rhi;
-    const int c_incr_ok = cc->incr_ok, c_ub_sub = cc->ub_sub, c_lovf = cc->list_overflow;
+    const int c_incr_ok = cc->incr_ok, c_ub_sub = cc->ub_sub;
     const double c_wskip = cc->wskip;
     TabRaw TR;
     const int nu = LSETS ? a.nsets * sr_units(RC) : 0;
@@ -1038,7 +1038,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
     const long long i0 = (long long)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) * a.nscan + blockIdx.x;
     if (INCR && i0 < a.nblk) d0 = ldobj(a.bdesc + i0);
     q.run = c_halted == H_RUN && c_prepped && c_steps < c_budget;
-    if (a.rfpass && c_halted == H_NEED_EXACT && !c_lovf) { rf_run(); return; }   // (the tile loads are dropped)
+    if (a.rfpass && c_halted == H_NEED_EXACT) { rf_run(); return; }   // (the tile loads are dropped)
     q.ubpass = 0;
     // (a conditional bound pass launched on the block list of the last records' best
     // keys: those blocks only, when k_step left one, else every tile)
@@ -3042,6 +3042,9 @@ __global__ __launch_bounds__(REFRESH_THREADS) void k_refresh(RefreshArgs a) {
 __device__ __attribute__((noinline)) void refresh_in_scan(const RefreshArgs* rfp, int pend, int kind, int from, int to,
                                                           uint32_t part, double* buf) {
     const RefreshArgs rf = *rfp;
+    // (a list that overflowed earlier: the host relists and refreshes; k_step leaves the
+    // halt to it, StepArgs.rf_final)
+    if (rf.ctl->list_overflow) return;
     __shared__ int s_i;
     const int g = blockIdx.x, ng = gridDim.x;
     const bool ef = pend && kind != 3 && from >= 0, et = pend && kind != 2 && to >= 0;
