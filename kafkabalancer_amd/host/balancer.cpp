@@ -4,6 +4,7 @@
 #include "balancer.hpp"
 
 #include <algorithm>
+#include <unordered_set>
 #include <map>
 
 namespace kbh {
@@ -87,19 +88,24 @@ void Planner::fill_defaults() {
     filled_ = true;
     if (pl_.partitions[0].weight == 0)
         for (auto& p : pl_.partitions) p.weight = 1.0;
+    // (the default list only when some partition has none: c3's partitions all carry
+    // their own, and collecting + sorting every replica id cost 0.1 s of the plan)
+    bool need = false;
+    for (auto& p : pl_.partitions) if (p.brokers.nil()) { need = true; break; }
     Slice brokers;
-    if (!cfg_.brokers_nil) {
+    if (need && !cfg_.brokers_nil) {
         brokers = Slice::of(cfg_.brokers);
-    } else {
-        std::vector<int64_t> all;
+    } else if (need) {
+        std::unordered_set<int64_t> seen;
         for (auto& p : pl_.partitions)
-            for (size_t k = 0; k < p.replicas.len; k++) all.push_back(p.replicas.at(k));
+            for (size_t k = 0; k < p.replicas.len; k++) seen.insert(p.replicas.at(k));
+        std::vector<int64_t> all(seen.begin(), seen.end());
         std::sort(all.begin(), all.end());
-        all.erase(std::unique(all.begin(), all.end()), all.end());
         if (!all.empty()) brokers = Slice::of(all);           // getBrokerList: nil when empty
     }
-    for (auto& p : pl_.partitions)
-        if (p.brokers.nil()) p.brokers = brokers;
+    if (need)
+        for (auto& p : pl_.partitions)
+            if (p.brokers.nil()) p.brokers = brokers;
     for (auto& p : pl_.partitions)
         if (p.num_replicas == 0) p.num_replicas = (int64_t)p.replicas.len;
 }
