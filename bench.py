@@ -7,16 +7,18 @@ Balance() call (balancer.go:49-65) executed device-resident by kb_engine_plan;
 `value` counts the candidates the reference would score (SURVEY.md 8d metric 1)
 over the timed steps, per wall second.
 
-Roofline: the dominant streaming kernel is k_scan; `achieved` =
-its algorithmic bytes per launch / its in-plan duration (device clock: earliest
-scan-workgroup start to latest end, per step).  The isolated figure (HIP events
-around back-to-back launches on the final state) and the whole-step fraction
-(8d bytes per step / ms_per_step / 8 TB/s) are reported beside it.  `traffic` is
-the rocprofv3 PMC figure for the same workload (profiles/pmc_traffic.json, keyed by
-workload).
+Roofline: the streaming kernel is k_scan; `achieved` = its algorithmic
+bytes per launch / its average in-plan launch duration, timed with HIP events around
+every launch on the engine's stream (dispatch included: the interval rocprofv3
+--kernel-trace reports, so profiles/*/c3_kernel_stats.csv recomputes it).  The
+device-clock duration (first scan workgroup start to last end) and the whole-step
+fraction `frac_step` (SURVEY 8(d) bytes per step / ms_per_step / 8 TB/s) are reported
+beside it.  `traffic` is the rocprofv3 PMC figure for the same workload
+(profiles/pmc_traffic.json, keyed by workload, stamped with the git head it ran on).
 
-Multi-GPU (torchrun): kafkabalancer_amd.dist.bench_main (c5: a fixed 10M partitions
-sharded N ways, strong scaling; other workloads weak by default).
+Multi-GPU: under torch.distributed.run (WORLD_SIZE set) kafkabalancer_amd.dist.bench_main;
+`--gpus N` without a launcher starts N ranks itself (spawn_ranks).  c5: a fixed 10M
+partitions sharded N ways, strong scaling; other workloads weak by default.
 """
 import argparse
 import json
@@ -44,18 +46,23 @@ def cpu_model():
     return platform.processor() or "unknown"
 
 
-def cpu_baseline(cl, cfg, seconds=12.0):
-    """The reference's algorithm on the host: the oracle (C restatement of steps.go
-    move(), single thread like the Go balancer) on a bounded sample -- the first k
-    partitions of the same cluster, leader step (the step the reference runs first with
-    -allow-leader) -- plus the engine's own algorithm on the CPU (tools/cpu_engine,
-    OpenMP) over whole steps of the same plan."""
+def _oracle_pl(cl):
     from oracle import oracle as O
     P = cl.n
-    opl = O.OraclePL.from_soa(b"t", np.zeros(P + 1, np.int64), np.arange(P, dtype=np.int64),
-                              cl.replica_ids, cl.replica_off, np.where(cl.weight == 0, 1.0, cl.weight),
-                              np.where(cl.num_replicas == 0, np.diff(cl.replica_off), cl.num_replicas),
-                              cl.set_ids, cl.set_off, cl.set_idx, cl.num_consumers)
+    return O.OraclePL.from_soa(b"t", np.zeros(P + 1, np.int64), np.arange(P, dtype=np.int64),
+                               cl.replica_ids, cl.replica_off, np.where(cl.weight == 0, 1.0, cl.weight),
+                               np.where(cl.num_replicas == 0, np.diff(cl.replica_off), cl.num_replicas),
+                               cl.set_ids, cl.set_off, cl.set_idx, cl.num_consumers)
+
+
+def _move_sample(cl, cfg, seconds):
+    """The oracle's move() (C restatement of steps.go:145-232, one thread like the Go
+    balancer) over the first k partitions of the cluster, k grown until the sample takes
+    about `seconds`: (candidates, seconds, k, leaders)."""
+    from oracle import oracle as O
+    O.set_threads(1)
+    opl = _oracle_pl(cl)
+    P = cl.n
     leaders = bool(cfg.get("allow_leader"))
     k = 16
     while True:
@@ -71,11 +78,64 @@ def cpu_baseline(cl, cfg, seconds=12.0):
         n, _ = O.move_sample(opl, cfg, leaders, k2)
         dt = time.perf_counter() - t0
         k = k2
-    out = {"value": n / dt, "unit": "candidates/s", "cores": 1, "kind": "port",
-           "sample": "oracle move(%s) over the first %d of %d partitions: %d candidates in %.1f s "
-                     "(extrapolated per candidate; reference Go not buildable: no Go toolchain)"
-                     % ("leaders" if leaders else "non-leaders", k, P, n, dt),
-           "cpu_model": cpu_model(), "nproc": os.cpu_count()}
+    return n, dt, k, leaders
+
+
+def _plan_sample(cl, cfg, seconds, steps_max):
+    """Whole Balance() steps of the plan on the oracle (balancer.go:49-65 per step, one
+    thread), from the cluster's initial state, until the plan ends, steps_max steps ran
+    or about `seconds` passed: (the oracle's changes, seconds)."""
+    from oracle import oracle as O
+    O.set_threads(1)
+    opl = _oracle_pl(cl)
+    out = []
+    t0 = time.perf_counter()
+    while len(out) < steps_max and time.perf_counter() - t0 < seconds:
+        r = O.balance(opl, cfg, O.SEM_APPLIED)
+        if r["status"] != 1:
+            break
+        out.append(r)
+    return out, time.perf_counter() - t0
+
+
+def cpu_baseline(cl, cfg, desc, plan_cand_per_step, seconds=12.0):
+    """The reference's algorithm on the host cores: the C oracle, single
+    thread like the Go balancer (kind "port"; the Go reference is not buildable here),
+    on a bounded sample of the same workload:
+      * c2 / c4: whole steps of the plan from the initial state (c2 ends within the budget:
+        the full 100-move plan); the sample's steps are checked against the GPU engine's
+        plan of the same steps, whose candidate counts are the metric's numerator;
+      * c3 / c5: move() over the first k partitions (one step costs far too long on one
+        core), extrapolated per candidate to ms per step with the timed plan's candidates.
+    Plus the engine's own algorithm on the host (tools/cpu_engine, OpenMP) over whole steps."""
+    wl = desc.get("workload")
+    out = {"cores": 1, "kind": "port", "cpu_model": cpu_model(), "nproc": os.cpu_count()}
+    if wl in ("c2", "c4"):
+        from kafkabalancer_amd import engine as E
+        och, dt = _plan_sample(cl, cfg, seconds, int(desc.get("max_reassign", 1000)))
+        k = len(och)
+        eng = E.Engine(cl, cfg, device=0)
+        ech, err = eng.plan(k)
+        cand = eng.stats()["candidates"]
+        eng.close()
+        same = [(c["step"], c["pidx"], c["from_"], c["to"]) for c in ech] == \
+               [(c["step"], c["pidx"], c["from_"], c["to"]) for c in och]
+        out.update(ms_per_step=1e3 * dt / max(k, 1), steps=k, plan_matches_gpu=same,
+                   sample="oracle Balance() x %d steps of the %s plan from its initial state (%.1f s)"
+                          % (k, wl, dt))
+        if cand > 0:
+            out.update(value=cand / dt, unit="candidates/s")
+        else:
+            # (c4: Remove / Add / Disallowed stages only, move() never runs: no candidates)
+            out.update(value=1e3 * dt / max(k, 1), unit="ms/step")
+    else:
+        n, dt, k, leaders = _move_sample(cl, cfg, seconds)
+        cps = n / dt
+        out.update(value=cps, unit="candidates/s",
+                   ms_per_step_extrapolated=1e3 * plan_cand_per_step / cps if plan_cand_per_step else None,
+                   sample="oracle move(%s) over the first %d of %d partitions: %d candidates in %.1f s; "
+                          "ms_per_step_extrapolated = the timed plan's candidates per step / this rate"
+                          % ("leaders" if leaders else "non-leaders", k, cl.n, n, dt))
     # the engine's algorithm on the CPU (O(1) deltas + exact verification, OpenMP)
     try:
         sys.path.insert(0, os.path.join(ROOT, "tools", "cpu_engine"))
@@ -105,13 +165,14 @@ def cpu_baseline(cl, cfg, seconds=12.0):
 
 
 def pmc_traffic(workload, kernel):
-    """HBM-side bytes per launch from the committed rocprofv3 PMC passes (tools/pmc_bench.sh)."""
+    """HBM-side bytes per launch from the committed rocprofv3 PMC passes (tools/pmc_bench.sh,
+    tools/pmc_summarise.py): (bytes, the git head the passes ran on) or (None, None)."""
     try:
         with open(os.path.join(ROOT, "profiles", "pmc_traffic.json")) as f:
             d = json.load(f)
-        return d[workload][kernel]["traffic_bytes_per_launch"]
+        return d[workload][kernel]["traffic_bytes_per_launch"], d[workload].get("git_head")
     except (OSError, KeyError, ValueError, TypeError):
-        return None
+        return None, None
 
 
 def bytes_8d(cl, changes, nsets, B, rmax, full_steps):
@@ -206,6 +267,33 @@ def drop_in(args):
     print(json.dumps(out))
 
 
+def spawn_ranks(args):
+    """`bench.py --gpus N` without a launcher: run N ranks under torch.distributed.run as a
+    child process (one process per GPU, rendezvous on 127.0.0.1) and exit with its status.
+    Nothing here touches the GPU: the ranks initialise their own devices."""
+    import socket
+    import subprocess
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(args.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def kernel_times(eng, steps, mode):
+    """Per-kernel (us per launch, launches) over `steps` more steps of the plan, timing
+    mode 1 (device clock for k_scan / k_step) or 2 (HIP events around every launch)."""
+    eng.set_timing(mode)
+    _, err = eng.plan(steps)
+    assert err is None, err
+    tk = eng.timings()
+    eng.set_timing(False)
+    return {k: (1e3 * v[0] / max(v[1], 1), v[1]) for k, v in tk.items()}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -221,6 +309,11 @@ def main():
                          "lower-bound certificate keeps); a separate line, not the full-scan roofline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--isolated-scan", action="store_true",
+                    help="also time 200 back-to-back k_scan launches on the final state (kept out of "
+                         "the default run so a rocprofv3 trace of it averages in-plan launches only)")
+    ap.add_argument("--plan-out", default=None,
+                    help="write the timed plan's changes (rank 0) to this JSON file")
     ap.add_argument("--stamps", action="store_true",
                     help="diagnostic: load the -DKB_STAMPS build and print per-phase times (not a bench line)")
     ap.add_argument("--drop-in", action="store_true",
@@ -231,6 +324,8 @@ def main():
                     help="diagnostic: k_step alone on a fixed input after the warm-up plan "
                          "(kb_engine_bench_step; with a -DKB_STOP_AT=k library: the cost up to phase k)")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return spawn_ranks(args)
     if args.drop_in:
         return drop_in(args)
     if args.step_alone:
@@ -287,33 +382,34 @@ def main():
     changes, err = eng.changes(*raw)            # (Python dicts, outside the timed region)
     assert err is None, err
     st1 = eng.stats()
+    if args.plan_out:
+        with open(args.plan_out, "w") as f:
+            json.dump(changes, f)
     steps = len(changes) + (0 if len(changes) == args.steps else 1)
     cand = st1["candidates"] - st0["candidates"]
     dev_s = st1["device_ms"] / 1e3
     ms_per_step = 1e3 * wall / max(steps, 1)
-    # per-kernel durations over a second stretch of the same plan (device clock: every
-    # scan workgroup stamps its start/end, k_step folds the interval), outside the
-    # headline timing above
-    eng.set_timing(True)
+    # per-kernel durations over two more stretches of the same plan, outside the headline
+    # timing: (a) HIP events around every launch -- dispatch included, the interval
+    # rocprofv3 --kernel-trace reports (the roofline's figure); (b) the device clock (each
+    # scan workgroup stamps its start / end, k_step folds the interval), a side figure
     kt_steps = min(args.steps, 200)
     stk0 = eng.stats()
-    _, err = eng.plan(kt_steps)
-    assert err is None, err
+    kev = kernel_times(eng, kt_steps, 2)
     stk1 = eng.stats()
-    tk = eng.timings()
-    scan_ms, scan_n = tk["scan"]
-    scan_clock_us = 1e3 * scan_ms / max(scan_n, 1)
-    eng.set_timing(False)
-    scan_iso_us = eng.bench_scan(200)
+    kdc = kernel_times(eng, kt_steps, 1)
+    scan_us, scan_n = kev["scan"]
+    scan_clock_us = kdc["scan"][0]
+    scan_iso_us = eng.bench_scan(200) if args.isolated_scan else None
     bytes_scan = st1["scan_bytes"]
     if incr:
         # bytes the incremental scans actually read: their blocks' partition words
-        # (+ the 16-B block descriptors), per scan launch of the timing stretch
+        # (+ the 16-B block descriptors), per scan launch of the events stretch
         per_part = bytes_scan / max(cl.n, 1)
         nscans = max(scan_n, 1)
         blk = stk1["blocks_scanned"] - stk0["blocks_scanned"]
         bytes_scan = blk * 128 * per_part / nscans + 16 * blk / nscans
-    achieved = bytes_scan / (scan_clock_us * 1e-6) / 1e9
+    achieved = bytes_scan / (scan_us * 1e-6) / 1e9
     rmax = st1["max_replicas"]
     b8d = bytes_8d(cl, changes, st1["n_sets"], st1["n_brokers"], rmax, steps)
     whole_gbs = b8d / max(wall, 1e-12) / 1e9
@@ -321,6 +417,31 @@ def main():
                      for c in changes)
     weights = "Zipf-like weights w = r^-1.1, r ~ U[1, 1e6]" if desc.get("weights") == "zipf" else \
         "weights absent (FillDefaults -> 1.0: uniform, exact ties)"
+    traffic, traffic_git = (None, None) if incr else pmc_traffic(args.workload, "k_scan")
+    roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+            "kernel": "k_scan", "bytes_per_launch": bytes_scan,
+            "bytes_per_launch_def": ("engine layout: per partition 8 w + 4 meta + 2*%d rep" % rmax) +
+                                    (" x the blocks the incremental scans read (+16 B per block "
+                                     "descriptor); the full scan reads %d" % st1["scan_bytes"]
+                                     if incr else ""),
+            "avg_launch_us": scan_us,
+            "timing": "HIP events around each in-plan k_scan launch (dispatch included, the interval "
+                      "rocprofv3 --kernel-trace reports), %d launches" % scan_n,
+            "avg_launch_us_device_clock": scan_clock_us,
+            "frac_device_clock": bytes_scan / (scan_clock_us * 1e-6) / 1e9 / HBM_PEAK_GBS,
+            "frac_step": whole_gbs / HBM_PEAK_GBS,
+            "frac_step_def": "SURVEY.md 8(d) algorithmic bytes of the timed steps / their wall time / 8 TB/s"
+                             + (" (early-exit stages counted to their hit: ms_per_step is the headline, "
+                                "GB/s informational)" if early_exit else ""),
+            "bytes_8d_per_step": b8d / max(steps, 1),
+            "traffic_source": "profiles/pmc_traffic.json[%s] (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE per "
+                              "launch, separate passes)" % args.workload,
+            "traffic_git_head": traffic_git}
+    if scan_iso_us is not None:
+        roof.update(avg_launch_us_isolated=scan_iso_us,
+                    frac_isolated=bytes_scan / (scan_iso_us * 1e-6) / 1e9 / HBM_PEAK_GBS,
+                    isolated_timing="HIP events around 200 back-to-back k_scan launches on the final state")
     out = {
         "metric": "candidate moves scored/sec (+ ms per reassignment step)",
         "value": cand / wall,
@@ -336,27 +457,10 @@ def main():
         "data": "synthetic (numpy PCG64 seed 0x5EED000%s), %s" % (args.workload[-1], weights),
         "config": dict(desc, parallelism="single-gpu", device_ms_per_step=1e3 * dev_s / max(steps, 1),
                        mode=args.mode),
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None if incr else pmc_traffic(args.workload, "k_scan"),
-                     "kernel": "k_scan", "bytes_per_launch": bytes_scan,
-                     "bytes_per_launch_def": ("engine layout: per partition 8 w + 4 meta + 2*%d rep" % rmax) +
-                                             (" x the blocks the incremental scans read (+16 B per block "
-                                              "descriptor); the full scan reads %d" % st1["scan_bytes"]
-                                              if incr else ""),
-                     "avg_launch_us": scan_clock_us,
-                     "timing": "in-plan device clock (earliest scan workgroup start .. latest end), "
-                               "%d steps" % scan_n,
-                     "avg_launch_us_isolated": scan_iso_us,
-                     "frac_isolated": bytes_scan / (scan_iso_us * 1e-6) / 1e9 / HBM_PEAK_GBS,
-                     "isolated_timing": "HIP events around 200 back-to-back k_scan launches on the final state",
-                     "traffic_source": "profiles/pmc_traffic.json[%s] (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE "
-                                       "per launch)" % args.workload,
-                     "whole_step": {"bytes_8d_per_step": b8d / max(steps, 1), "achieved": whole_gbs,
-                                    "frac": whole_gbs / HBM_PEAK_GBS,
-                                    "def": "SURVEY.md 8(d) algorithmic bytes of the timed steps / wall time"
-                                           + (" (early-exit stages counted to their hit: ms_per_step is "
-                                              "the headline, GB/s informational)" if early_exit else "")}},
-        "kernels_us_per_step": {k: 1e3 * v[0] / max(v[1], 1) for k, v in tk.items()},
+        "roofline": roof,
+        "kernels_us_per_launch": {k: v[0] for k, v in kev.items() if v[1]},
+        "kernels_launches": {k: v[1] for k, v in kev.items() if v[1]},
+        "kernels_us_per_launch_device_clock": {k: kdc[k][0] for k in ("scan", "step")},
         "incremental": ({"blocks_per_scan": (stk1["blocks_scanned"] - stk0["blocks_scanned"]) / max(scan_n, 1),
                          "blocks_total": (cl.n + 127) // 128} if incr else None),
         "kernel_timing_steps": kt_steps,
@@ -378,12 +482,16 @@ def main():
                           "counts_per_step": {k: st[i] / n for k, i in counts.items()},
                           "stats": eng.stats()}))
         return
-    if not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(cl, cfg, args.cpu_seconds)
-        out["speedup_vs_cpu"] = out["value"] / out["cpu_baseline"]["value"]
-    print(json.dumps(out))
     eng.close()
+    if not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(cl, cfg, desc, cand / max(steps, 1), args.cpu_seconds)
+        cb = out["cpu_baseline"]
+        if cb.get("unit") == "candidates/s" and cb.get("value"):
+            out["speedup_vs_cpu"] = out["value"] / cb["value"]
+        elif cb.get("unit") == "ms/step":
+            out["speedup_vs_cpu"] = cb["value"] / ms_per_step
+    print(json.dumps(out))
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

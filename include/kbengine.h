@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define KB_ABI_VERSION 7
+#define KB_ABI_VERSION 8
 
 /* step indices == position in the reference's steps table (balancer.go:34-44) */
 enum kb_step {
@@ -37,6 +37,9 @@ enum kb_step {
     KB_STEP_MOVE_LEADERS = 7,         /* steps.go:292-298 -> move(leaders=true) */
     KB_STEP_MOVE_NON_LEADERS = 8      /* steps.go:286-288 -> move(leaders=false) */
 };
+/* step masks of kb_engine_step: bit (1u << kb_step) per entry of the steps table */
+#define KB_STEP_BIT(s) (1u << (s))
+#define KB_STEPS_ALL 0x1FFu
 
 /* kb_change.status / return value of kb_engine_balance */
 enum { KB_NOCHANGE = 0, KB_CHANGE = 1,
@@ -141,6 +144,8 @@ typedef struct {
                                        brokers; the step ran again, ABI 5) */
     int64_t blocks_scanned;         /* incremental mode: 128-partition blocks the scans read
                                        (kb_engine_set_incremental, ABI 6) */
+    int64_t relists;                /* per-broker partition lists laid out again after one ran
+                                       out of slack (kb_config.list_slack, ABI 8) */
 } kb_stats;
 
 typedef struct kb_engine kb_engine;
@@ -155,8 +160,21 @@ int kb_engine_create(const kb_cluster *cluster, const kb_config *cfg, kb_engine 
 
 /* One Balance() call: runs the fused step pipeline on the device, applies the
  * change to the device state (per cfg->semantics), returns KB_CHANGE /
- * KB_NOCHANGE or < 0.  Equivalent of balancer.go:49-65 + the aliasing write. */
+ * KB_NOCHANGE or < 0.  Equivalent of balancer.go:49-65 + the aliasing write.
+ * Same as kb_engine_step(e, KB_STEPS_ALL, out). */
 int kb_engine_balance(kb_engine *e, kb_change *out);
+
+/* One Balance() restricted to the steps whose bit is set in step_mask, in the reference's
+ * order (balancer.go:34-44): with a single bit it is that step function alone, e.g.
+ * KB_STEP_BIT(KB_STEP_MOVE_NON_LEADERS) = MoveNonLeaders(pl, cfg) (steps.go:286-288), so a
+ * host that keeps the reference's steps table and Balance() binds each entry to one call
+ * (INTEGRATION.md).  Returns KB_CHANGE (out = the change, applied on the device per
+ * cfg->semantics), KB_NOCHANGE (the step returned nil, nil) or < 0 ("<Step>: <msg>" in
+ * kb_engine_last_error).  ValidateWeights / FillDefaults ran at create: their bits change
+ * nothing (a create-time validation error is returned by its own step and every later
+ * one).  After a KB_NOCHANGE the next call resolves the same scan of the unchanged state
+ * (no second scan): a host walking the table pays one scan per Balance(). */
+int kb_engine_step(kb_engine *e, uint32_t step_mask, kb_change *out);
 
 /* Device-resident plan: up to max_steps Balance() calls without host
  * round trips (run()'s loop with -complete-partition=false,
@@ -176,12 +194,16 @@ double kb_engine_unbalance(kb_engine *e);
 
 int kb_engine_stats(kb_engine *e, kb_stats *out);
 
-/* Per-kernel device time of the last kb_engine_plan when cfg->time_kernels was
- * set: ms[k] = summed duration of kernel k over the plan, launches[k] = count,
- * for k in {0 k_step (resolve + apply + prep), 1 k_scan, 2 k_refresh}.  Returns 3. */
+/* Per-kernel device time of the last kb_engine_plan when timing was on: ms[k] = summed
+ * duration of kernel k over the plan, launches[k] = count, for k in {0 k_step (resolve +
+ * apply + prep), 1 k_scan, 2 k_refresh, 3 the conditional bound pass (k_scan ubpass +
+ * k_ubinit; mode 2 only)}.  Returns 4. */
 int kb_engine_timings(kb_engine *e, double *ms, int64_t *launches, int n);
 
-/* Turn the per-kernel events on or off for the following plans (resets the sums). */
+/* Kernel timing for the following plans (resets the sums): 0 off; 1 k_scan / k_step from
+ * the device clock (first workgroup start .. last end, no events between them), the rest
+ * from HIP events; 2 HIP events around every launch (dispatch included: the interval
+ * rocprofv3 --kernel-trace reports; the kernels run as in production). */
 int kb_engine_set_timing(kb_engine *e, int32_t on);
 
 /* Incremental rescoring mode (single GPU, off by default): after a

@@ -47,7 +47,7 @@ static const char* kStepNames[9] = {
     "AddMissingReplicas", "MoveDisallowedReplicas", "ReassignLeaders",
     "MoveLeaders", "MoveNonLeaders"};
 
-enum { TK_STEP = 0, TK_SCAN = 1, TK_REFRESH = 2, TK_N = 3 };
+enum { TK_STEP = 0, TK_SCAN = 1, TK_REFRESH = 2, TK_BOUND = 3, TK_N = 4 };
 
 struct kb_engine {
     int dev = 0;
@@ -113,8 +113,8 @@ struct kb_engine {
     std::vector<hipEvent_t> tev;
     std::vector<int> tkind;           // kernel kind between tev[i] and tev[i+1]
     int tev_used = 0;
-    double kms[TK_N] = {0, 0, 0};
-    int64_t klaunch[TK_N] = {0, 0, 0};
+    double kms[TK_N] = {0, 0, 0, 0};
+    int64_t klaunch[TK_N] = {0, 0, 0, 0};
     int64_t refreshes = 0;
     bool rf_stream = false;        // in-stream refreshes (ScanArgs.rfpass / StepArgs.rf_final)
     RefreshArgs* rf_dev = nullptr; // the refresh's arguments in device memory (ScanArgs.rf)
@@ -129,6 +129,12 @@ struct kb_engine {
     bool ub_mode = false;          // a step re-scanned: enqueue the conditional bound pass per scan
     uint32_t list_slack = 1024;        // free entries per broker list (doubled on every re-layout)
     int64_t relists = 0;
+    const void* gath = nullptr;        // the last gathered rank summaries (device) and their count
+    int gath_n = 0;                    //   (grow_summary reads their shared flags)
+    uint32_t step_mask = SM_ALL;       // steps the running Balance() may take (kb_engine_step)
+    bool recs_fresh = false;           // the scan records describe the current state (a masked
+                                       //   step changed nothing): the next masked step reuses them
+    bool reuse_now = false;            //   (the run about to start takes them)
     std::string last_err;
 };
 
@@ -266,11 +272,16 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
                 e->pending_msg = std::string("ValidateWeights: partition ") + part_string(e, i, reps_of(i)) + " has negative weight";
             }
         }
-        // (duplicates by dense id: the id map is a bijection; pairwise, no allocation)
+        // (duplicates by dense id: the id map is a bijection; one epoch mark per broker, the
+        // partition index, so a partition costs O(len) like toBrokerSet's map)
+        std::vector<int64_t> seen_in(e->B ? e->B : 1, -1);
         for (int64_t i = 0; i < n && !e->pending; i++) {
             bool dup = false;
-            for (int k = 1; k < len[i] && !dup; k++)
-                for (int q = 0; q < k && !dup; q++) dup = dn(i, k) == dn(i, q);
+            for (int k = 0; k < len[i] && !dup; k++) {
+                const int b = dn(i, k);
+                dup = seen_in[b] == i;
+                seen_in[b] = i;
+            }
             if (dup) {
                 e->pending = KB_ERR_STEP; e->pending_step = 1;
                 e->pending_msg = std::string("ValidateReplicas: partition ") + part_string(e, i, reps_of(i)) + " has duplicated replicas";
@@ -609,6 +620,7 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
     z.logcap = e->logcap;
     z.full_prep = 1;
     z.tk_on = e->time_kernels;
+    z.step_mask = SM_ALL;
     z.ts_beg = NONE64;
     HIPCHK(hipMemcpy(e->ctl, &z, sizeof z, hipMemcpyHostToDevice));
     HIPCHK(hipEventCreate(&e->ev0));
@@ -686,9 +698,11 @@ static const int64_t kLogChunk = 16384;   // steps per device step log (kb_engin
 
 static void mark(kb_engine* e, int kind_next) {
     if (!e->time_kernels) return;
-    if (kind_next == TK_SCAN || kind_next == TK_STEP) return;   // device-clock timed (no events between them)
+    // mode 1: k_scan / k_step are device-clock timed (no events between them); mode 2:
+    // HIP events around every launch (dispatch included, the interval rocprofv3 reports)
+    if (e->time_kernels == 1 && (kind_next == TK_SCAN || kind_next == TK_STEP || kind_next == TK_BOUND)) return;
     if (e->tev.empty()) {
-        e->tev.resize((size_t)kStepBatch * 2 + 8);
+        e->tev.resize((size_t)kStepBatch * 4 + 16);
         e->tkind.resize(e->tev.size());
         for (auto& v : e->tev) hipEventCreate(&v);
     }
@@ -727,6 +741,7 @@ static void enqueue_scan(kb_engine* e, bool rf = false) {
 // census-free scan (no list op) plus k_ubinit sets ub to the step's own minima
 static void enqueue_ubinit(kb_engine* e, bool rf = false) {
     if (e->nscan == 0) return;
+    mark(e, TK_BOUND);
     ScanArgs s;
     fill_scan_args(e, s);
     s.rfpass = rf && e->rf_stream;
@@ -795,6 +810,14 @@ static int relist(kb_engine* e) {
     HIPCHK(hipMemcpy(e->L.lstart, hls.data(), hls.size() * 4, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(e->L.llen, hll.data(), hll.size() * 4, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(e->L.lcap, hlc.data(), hlc.size() * 4, hipMemcpyHostToDevice));
+    // every broker holding a replica is refolded from the new lists by the refresh that
+    // follows (a load folded from an edit the old lists dropped must not survive them)
+    if (e->B) {
+        std::vector<uint8_t> fl(e->B);
+        HIPCHK(hipMemcpy(fl.data(), e->bfl, e->B, hipMemcpyDeviceToHost));
+        for (int64_t b = 0; b < e->B; b++) if (cnt[b] > 0) fl[b] |= 4;   // BF_DIRTY (kernels.hip)
+        HIPCHK(hipMemcpy(e->bfl, fl.data(), e->B, hipMemcpyHostToDevice));
+    }
     if (const int rc = upload_rf(e); rc != KB_OK) return rc;
     e->relists++;
     return KB_OK;
@@ -802,7 +825,7 @@ static int relist(kb_engine* e) {
 
 // exact refolds of the approximate loads (k_refresh), then a full prep
 static int refresh(kb_engine* e) {
-    if (e) e->ctl_mirror = false;            // (the device block changes behind the host copy)
+    if (e) { e->ctl_mirror = false; e->recs_fresh = false; }            // (the device block changes behind the host copy)
     roctxMark("kb:refresh (exact refolds of the approximate loads)");
     if (e->integral) return KB_OK;
     mark(e, -1);
@@ -849,6 +872,9 @@ static int reset_ctl(kb_engine* e, int64_t budget_steps) {
     c.halted = H_RUN;
     c.logpos = 0;
     c.logcap = e->logcap;
+    c.step_mask = e->step_mask;
+    if (!e->reuse_now) { c.ncont = 0; c.cont_overflow = 0; }   // (a scan runs first: an empty spill)
+    e->recs_fresh = false;
     const long long bud = (long long)c.steps + budget_steps;
     c.budget = bud > 0x7FFFFFFF ? 0x7FFFFFFF : (int32_t)bud;
     *e->h_ctl = c;
@@ -929,7 +955,7 @@ static int ensure_log(kb_engine* e, int64_t max_steps) {
 // halted step runs again.  Only past kContMax is it a capacity error.
 static const uint32_t kContMax = 1u << 26;   // 64M candidates (2 GiB)
 static int grow_spill(kb_engine* e) {
-    if (e) e->ctl_mirror = false;            // (the device block changes behind the host copy)
+    if (e) { e->ctl_mirror = false; e->recs_fresh = false; }            // (the device block changes behind the host copy)
     roctxMark("kb:grow_spill (near-tie buffer x8, step runs again)");
     if (e->cont_cap >= kContMax) {
         e->last_err = "engine capacity: more than " + std::to_string(kContMax) + " near-tied candidates in one step";
@@ -967,7 +993,12 @@ static int run_steps(kb_engine* e, int64_t max_steps) {
         HIPCHK(hipHostMalloc((void**)&e->h_log, (size_t)e->logcap * sizeof(ChangeDev), hipHostMallocDefault));
         e->h_logcap = e->logcap;
     }
-    if (const int rc = reset_ctl(e, max_steps); rc != KB_OK) return rc;
+    // (kb_engine_step: the scan records of a masked step that changed nothing describe the
+    // state still; the first pair reuses them)
+    bool reuse = e->reuse_now && e->h_ctl->prepped;
+    if (const int rc = reset_ctl(e, max_steps); rc != KB_OK) { e->reuse_now = false; return rc; }
+    e->reuse_now = false;
+    reuse = reuse && e->h_ctl->prepped && e->h_ctl->halted == H_RUN;
     const int steps0 = e->h_ctl->steps;
     bool prepped = e->h_ctl->prepped != 0;
     bool fresh = false;                 // h_ctl holds the device block after the last batch
@@ -985,6 +1016,11 @@ static int run_steps(kb_engine* e, int64_t max_steps) {
             // (a halt for exact loads in pair s - 1 is refolded by pair s's first scan launch)
             const bool ubp = (s == 1 && !prepped) || (e->ub_mode && (s > 0 || prepped));
             const bool rf = s > 0;
+            if (s == 0 && reuse) {           // kb_engine_step: the last masked step's records
+                mark(e, TK_STEP);
+                enqueue_step(e);
+                continue;
+            }
             if (ubp) enqueue_ubinit(e, rf);
             enqueue_pair(e, rf, !ubp);
         }
@@ -1001,6 +1037,7 @@ static int run_steps(kb_engine* e, int64_t max_steps) {
         HIPCHK(hipStreamSynchronize(e->st));
         roctxRangePop();
         fresh = true;
+        reuse = false;
         harvest(e);
         const DevCtl& c = *e->h_ctl;
         if (c.total_retries > 0) e->ub_mode = true;
@@ -1041,12 +1078,46 @@ static int run_steps(kb_engine* e, int64_t max_steps) {
 
 extern "C" int kb_engine_balance(kb_engine* e, kb_change* out) {
     if (!e || !out) return KB_ERR_INVALID;
-    if (e->pending) return pending_result(e, out);
+    return kb_engine_step(e, KB_STEPS_ALL, out);
+}
+
+// One Balance() restricted to the steps in step_mask (bit k = kb_step k, in the reference's
+// order, balancer.go:34-44): a Go steps table whose entries are cgo calls
+// calls it once per entry.  ValidateWeights and FillDefaults ran at create (the weights and
+// defaults never change on the device); ValidateReplicas can fail later only under Go
+// aliasing (a remove duplicates a replica), so under KB_SEM_APPLIED it is host
+// work too.  A masked step that changes nothing keeps the prep and its scan records, and the
+// next masked step resolves them again without a scan (the state has not changed).
+extern "C" int kb_engine_step(kb_engine* e, uint32_t step_mask, kb_change* out) {
+    if (!e || !out || (step_mask & ~(uint32_t)KB_STEPS_ALL)) return KB_ERR_INVALID;
+    auto nochange = [&]() {
+        memset(out, 0, sizeof *out);
+        out->status = KB_NOCHANGE; out->step = -1; out->partition = -1;
+        out->from_broker = out->to_broker = out->err_broker = -1;
+        return KB_NOCHANGE;
+    };
+    if (e->pending) {
+        // a validation error (create): returned by its own step and by every later one (the
+        // engine holds no state past a failed validation); earlier steps change nothing
+        if (step_mask >> e->pending_step) return pending_result(e, out);
+        return nochange();
+    }
+    uint32_t dev = step_mask & ~(uint32_t)(SM_VALIDATE_WEIGHTS | SM_FILL_DEFAULTS);
+    if (e->sem != KB_SEM_GO) dev &= ~(uint32_t)SM_VALIDATE_REPLICAS;
+    if (!dev) return nochange();                  // (no device work: the records stay)
     e->last_ms = 0;
+    e->step_mask = step_mask;                     // (k_step never tests bits 0 and 2)
+    dev = step_mask;
+    e->reuse_now = e->recs_fresh;
     const int nlog = run_steps(e, 1);
+    e->step_mask = SM_ALL;
     if (nlog < 0) return nlog;
-    if (nlog == 0) { memset(out, 0, sizeof *out); out->status = KB_NOCHANGE; return KB_NOCHANGE; }
-    return convert(e, e->h_log[0], out);
+    if (nlog == 0) return nochange();
+    const ChangeDev& d = e->h_log[0];
+    const int rc = convert(e, d, out);
+    // the records stay valid for the next masked step when this one changed nothing
+    e->recs_fresh = dev != SM_ALL && d.status == 0 && e->h_ctl->halted == H_DONE && e->h_ctl->prepped;
+    return rc;
 }
 
 extern "C" int kb_engine_plan(kb_engine* e, int64_t max_steps, kb_change* out, int64_t* n_out) {
@@ -1104,7 +1175,7 @@ extern "C" int64_t kb_engine_loads(kb_engine* e, int64_t* ids, double* loads, in
 }
 
 extern "C" double kb_engine_unbalance(kb_engine* e) {
-    if (e) e->ctl_mirror = false;            // (the device block changes behind the host copy)
+    if (e) { e->ctl_mirror = false; e->recs_fresh = false; }            // (the device block changes behind the host copy)
     if (!e || e->B == 0) return 0.0;
     if (make_exact(e) != KB_OK) return NAN;
     std::vector<double> ld(e->B);
@@ -1145,6 +1216,7 @@ extern "C" int kb_engine_stats(kb_engine* e, kb_stats* o) {
     o->retries = (int64_t)c.total_retries;
     o->spill_grows = e->spill_grows;
     o->blocks_scanned = (int64_t)c.total_blocks;
+    o->relists = e->relists;
     return KB_OK;
 }
 
@@ -1152,7 +1224,7 @@ extern "C" int kb_engine_stats(kb_engine* e, kb_stats* o) {
 // clears the device's permission flag, so the next scan is a full one and refreshes
 // the cached candidate counts.
 extern "C" int kb_engine_set_incremental(kb_engine* e, int32_t on) {
-    if (e) e->ctl_mirror = false;            // (the device block changes behind the host copy)
+    if (e) { e->ctl_mirror = false; e->recs_fresh = false; }            // (the device block changes behind the host copy)
     if (!e) return KB_ERR_INVALID;
     if (on && !e->lds_sets) {       // (the incremental scan kernel keeps the set records in LDS)
         e->last_err = "incremental mode needs the allowed-set records in LDS (too many sets or brokers)";
@@ -1181,8 +1253,10 @@ extern "C" int kb_engine_timings(kb_engine* e, double* ms, int64_t* launches, in
     double kms[TK_N];
     int64_t kn[TK_N];
     for (int k = 0; k < TK_N; k++) { kms[k] = e->kms[k]; kn[k] = e->klaunch[k]; }
-    kms[TK_STEP] = (double)c.tk_sum[1] * tick_ms; kn[TK_STEP] = (int64_t)c.tk_n[1];
-    kms[TK_SCAN] = (double)c.tk_sum[0] * tick_ms; kn[TK_SCAN] = (int64_t)c.tk_n[0];
+    if (e->time_kernels == 1) {
+        kms[TK_STEP] = (double)c.tk_sum[1] * tick_ms; kn[TK_STEP] = (int64_t)c.tk_n[1];
+        kms[TK_SCAN] = (double)c.tk_sum[0] * tick_ms; kn[TK_SCAN] = (int64_t)c.tk_n[0];
+    }
     for (int k = 0; k < TK_N && k < n; k++) {
         if (ms) ms[k] = kms[k];
         if (launches) launches[k] = kn[k];
@@ -1191,15 +1265,15 @@ extern "C" int kb_engine_timings(kb_engine* e, double* ms, int64_t* launches, in
 }
 
 extern "C" int kb_engine_set_timing(kb_engine* e, int32_t on) {
-    if (e) e->ctl_mirror = false;            // (the device block changes behind the host copy)
+    if (e) { e->ctl_mirror = false; e->recs_fresh = false; }            // (the device block changes behind the host copy)
     if (!e) return KB_ERR_INVALID;
     HIPCHK(hipStreamSynchronize(e->st));
     e->tev_used = 0;
     for (int k = 0; k < TK_N; k++) { e->kms[k] = 0; e->klaunch[k] = 0; }
-    e->time_kernels = on ? 1 : 0;
+    e->time_kernels = on == 2 ? 2 : (on ? 1 : 0);
     DevCtl c;
     HIPCHK(hipMemcpy(&c, e->ctl, sizeof c, hipMemcpyDeviceToHost));
-    c.tk_on = e->time_kernels;
+    c.tk_on = e->time_kernels == 1;                 // (mode 2: events only, production kernels)
     c.tk_sum[0] = c.tk_sum[1] = c.tk_n[0] = c.tk_n[1] = 0;
     c.ts_beg = NONE64;
     c.ts_end = 0;
@@ -1219,7 +1293,7 @@ extern "C" int kb_engine_stamps(kb_engine* e, uint64_t* out, int n) {
 // Diagnostic: average device time of k_scan over `iters` back-to-back launches on
 // the current prepped state (the scan only writes its records and spill buffer).
 extern "C" int kb_engine_bench_scan(kb_engine* e, int iters, double* avg_us) {
-    if (e) e->ctl_mirror = false;            // (the device block changes behind the host copy)
+    if (e) { e->ctl_mirror = false; e->recs_fresh = false; }            // (the device block changes behind the host copy)
     if (!e || iters < 1 || !avg_us) return KB_ERR_INVALID;
     if (e->pending) return e->pending;
     if (const int rc = reset_ctl(e, 1); rc != KB_OK) return rc;
@@ -1281,7 +1355,7 @@ extern "C" int kb_engine_bench_scan(kb_engine* e, int iters, double* avg_us) {
 // Run on -DKB_STOP_AT=k builds (kernels.hip, KB_STOP: return after phase k), the
 // cumulative times give the phase costs without instrumenting the production kernel.
 extern "C" int kb_engine_bench_step(kb_engine* e, int iters, double* avg_us) {
-    if (e) e->ctl_mirror = false;
+    if (e) { e->ctl_mirror = false; e->recs_fresh = false; }
     if (!e || iters < 1 || !avg_us) return KB_ERR_INVALID;
     if (e->pending) return e->pending;
     if (const int rc = reset_ctl(e, 1); rc != KB_OK) return rc;
@@ -1370,11 +1444,22 @@ static int grow_summary(kb_engine* e) {
     DevCtl c;
     HIPCHK(hipMemcpy(&c, e->ctl, sizeof c, hipMemcpyDeviceToHost));
     // The decision depends only on state every rank shares (sum_keys, identical on all
-    // ranks): at the summary limit every rank returns the capacity error, whatever its
-    // own spill state, so no rank re-enters the collective alone.  Below it every rank
-    // grows its summaries alike (the gathered layout needs one size) and the spill
-    // buffer only where this rank's scan overflowed it.
-    if (e->sum_keys >= SUMMARY_KEYS_MAX) {
+    // ranks, and the gathered summaries' flags): no rank re-enters the collective alone.
+    // Below the summary limit every rank grows its summaries alike (the gathered layout
+    // needs one size) and the spill buffer only where this rank's scan overflowed it.
+    // At the limit the step runs again only if some rank reported a spill overflow it
+    // can still grow (summary flag bit 2, k_summary); otherwise every rank returns the
+    // capacity error.
+    bool any_growable = false;
+    if (e->gath && e->gath_n > 0) {
+        const Recs G = summary_recs((unsigned char*)e->gath, e->gath_n, e->sum_keys);
+        for (int i = 0; i < e->gath_n && !any_growable; i++) {
+            uint32_t fl = 0;
+            HIPCHK(hipMemcpy(&fl, &G.h(i)->flags, 4, hipMemcpyDeviceToHost));
+            any_growable = (fl & 4u) != 0;
+        }
+    }
+    if (e->sum_keys >= SUMMARY_KEYS_MAX && !any_growable) {
         e->last_err = "engine capacity: more than " + std::to_string(SUMMARY_KEYS_MAX) +
                       " near-tied candidates in one rank summary";
         return KB_ERR_CAPACITY;
@@ -1395,7 +1480,7 @@ static int grow_summary(kb_engine* e) {
 }
 
 extern "C" int kb_engine_set_stream(kb_engine* e, void* s) {
-    if (e) e->ctl_mirror = false;            // (the device block changes behind the host copy)
+    if (e) { e->ctl_mirror = false; e->recs_fresh = false; }            // (the device block changes behind the host copy)
     if (!e) return KB_ERR_INVALID;
     if (e->own_st && e->st) hipStreamDestroy(e->st);
     e->st = (hipStream_t)s;
@@ -1404,7 +1489,7 @@ extern "C" int kb_engine_set_stream(kb_engine* e, void* s) {
 }
 
 extern "C" int kb_engine_step_begin(kb_engine* e, void* summary_dev) {
-    if (e) e->ctl_mirror = false;            // (the device block changes behind the host copy)
+    if (e) { e->ctl_mirror = false; e->recs_fresh = false; }            // (the device block changes behind the host copy)
     if (!e || !summary_dev) return KB_ERR_INVALID;
     if (e->pending) return e->pending;
     if (const int rc = reset_ctl(e, 1); rc != KB_OK) return rc;
@@ -1413,6 +1498,7 @@ extern "C" int kb_engine_step_begin(kb_engine* e, void* summary_dev) {
     SumArgs s;
     s.ctl = e->ctl; s.R = scan_recs(e->recs, (int)e->nscan); s.cont = e->cont; s.cont_cap = e->cont_cap;
     s.r = e->r; s.out = summary_recs((unsigned char*)summary_dev, 1, e->sum_keys);
+    s.spill_growable = e->cont_cap < kContMax ? 1 : 0;
     launch_summary(s, e->st);
     HIPCHK(hipGetLastError());
     return KB_OK;
@@ -1421,7 +1507,7 @@ extern "C" int kb_engine_step_begin(kb_engine* e, void* summary_dev) {
 // ---- batched multi-GPU steps: the host enqueues several (scan, summary, all-gather,
 // resolve) rounds without a host round trip; a halted step turns the rest into no-ops
 extern "C" int kb_engine_sharded_reset(kb_engine* e, int64_t budget_steps) {
-    if (e) e->ctl_mirror = false;            // (the device block changes behind the host copy)
+    if (e) { e->ctl_mirror = false; e->recs_fresh = false; }            // (the device block changes behind the host copy)
     if (!e || budget_steps < 1) return KB_ERR_INVALID;
     if (e->pending) return e->pending;
     if (const int rc = reset_ctl(e, budget_steps); rc != KB_OK) return rc;
@@ -1431,29 +1517,31 @@ extern "C" int kb_engine_sharded_reset(kb_engine* e, int64_t budget_steps) {
 }
 
 extern "C" int kb_engine_sharded_scan(kb_engine* e, void* summary_dev) {
-    if (e) e->ctl_mirror = false;            // (the device block changes behind the host copy)
+    if (e) { e->ctl_mirror = false; e->recs_fresh = false; }            // (the device block changes behind the host copy)
     if (!e || !summary_dev) return KB_ERR_INVALID;
     enqueue_scan(e);
     SumArgs s;
     s.ctl = e->ctl; s.R = scan_recs(e->recs, (int)e->nscan); s.cont = e->cont; s.cont_cap = e->cont_cap;
     s.r = e->r; s.out = summary_recs((unsigned char*)summary_dev, 1, e->sum_keys);
+    s.spill_growable = e->cont_cap < kContMax ? 1 : 0;
     launch_summary(s, e->st);
     HIPCHK(hipGetLastError());
     return KB_OK;
 }
 
 extern "C" int kb_engine_sharded_resolve(kb_engine* e, const void* gathered_dev, int32_t n_ranks) {
-    if (e) e->ctl_mirror = false;            // (the device block changes behind the host copy)
+    if (e) { e->ctl_mirror = false; e->recs_fresh = false; }            // (the device block changes behind the host copy)
     if (!e || !gathered_dev || n_ranks < 1) return KB_ERR_INVALID;
     StepArgs a;
     fill_step_args(e, a, summary_recs((unsigned char*)gathered_dev, n_ranks, e->sum_keys), 0);
     launch_step(a, e->st);
     HIPCHK(hipGetLastError());
+    e->gath = gathered_dev; e->gath_n = n_ranks;
     return KB_OK;
 }
 
 extern "C" int kb_engine_sharded_collect(kb_engine* e, kb_change* out, int64_t cap, int64_t* n_out) {
-    if (e) e->ctl_mirror = false;            // (the device block changes behind the host copy)
+    if (e) { e->ctl_mirror = false; e->recs_fresh = false; }            // (the device block changes behind the host copy)
     if (!e || !n_out || cap < 0) return KB_ERR_INVALID;
     *n_out = 0;
     HIPCHK(hipMemcpyAsync(e->h_ctl, e->ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, e->st));
@@ -1483,13 +1571,14 @@ extern "C" int kb_engine_sharded_collect(kb_engine* e, kb_change* out, int64_t c
 }
 
 extern "C" int kb_engine_step_finish(kb_engine* e, const void* gathered_dev, int32_t n_ranks, kb_change* out) {
-    if (e) e->ctl_mirror = false;            // (the device block changes behind the host copy)
+    if (e) { e->ctl_mirror = false; e->recs_fresh = false; }            // (the device block changes behind the host copy)
     if (!e || !gathered_dev || n_ranks < 1 || !out) return KB_ERR_INVALID;
     if (e->pending) return pending_result(e, out);
     StepArgs a;
     fill_step_args(e, a, summary_recs((unsigned char*)gathered_dev, n_ranks, e->sum_keys), 0);
     launch_step(a, e->st);
     HIPCHK(hipGetLastError());
+    e->gath = gathered_dev; e->gath_n = n_ranks;
     HIPCHK(hipMemcpyAsync(e->h_ctl, e->ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, e->st));
     HIPCHK(hipStreamSynchronize(e->st));
     const DevCtl c = *e->h_ctl;

@@ -163,6 +163,14 @@ struct ChangeDev {
     int32_t err_broker, pad;
 };
 
+// step-mask bits (1 << kb_step, include/kbengine.h): kb_engine_step runs a subset of the
+// reference's steps table (balancer.go:34-44)
+enum : uint32_t {
+    SM_VALIDATE_WEIGHTS = 1u << 0, SM_VALIDATE_REPLICAS = 1u << 1, SM_FILL_DEFAULTS = 1u << 2,
+    SM_REMOVE = 1u << 3, SM_ADD = 1u << 4, SM_DISALLOWED = 1u << 5, SM_REASSIGN = 1u << 6,
+    SM_MOVE_LEADERS = 1u << 7, SM_MOVE_NON_LEADERS = 1u << 8, SM_ALL = 0x1FFu
+};
+
 // halted codes
 // (H_NEED_SPILL: the near-tie spill buffer overflowed with the census bound already
 // at the step minimum; the host grows the buffer and the step runs again)
@@ -183,7 +191,8 @@ struct DevCtl {
     // kernel timing (tk_on): summed device-clock durations (100 MHz ticks) and launch
     // counts, {k_scan, k_step}; k_step folds in the scan's interval below
     unsigned long long tk_sum[2], tk_n[2];
-    int32_t tk_on, tk_pad;
+    int32_t tk_on;
+    uint32_t step_mask;             // steps the next Balance() may take (bit = kb_step; SM_ALL)
     // incremental mode (kb_engine_set_incremental): incr_ok = the next scan
     // may skip every partition block whose largest weight is below wskip (a lower-bound
     // certificate, see k_step); cand_cache = the candidate counts of the last full scan,

@@ -1265,6 +1265,9 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
     }
     const int halted = C.halted;
     const bool do_res = C.prepped && C.steps < C.budget;
+    // the steps this Balance() may take (kb_engine_step's mask; SM_ALL = the whole table)
+    const uint32_t sm = C.step_mask;
+    const bool lead_on = a.allow_leader && (sm & SM_MOVE_LEADERS), non_on = (sm & SM_MOVE_NON_LEADERS) != 0;
     const double eps = C.eps, inv_avg = C.inv_avg, U0h = C.U0;
     const int nblm0 = C.nblm, ndirty0 = C.ndirty;
     const bool pend = C.pending_list != 0;
@@ -1458,11 +1461,13 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
         __shared__ int s_fast;
         if (tid == 0) {
             const bool census_off = C.ub[0] == -HUGE_VAL || C.ub[1] == -HUGE_VAL;
-            int fast = !C.list_overflow && !s_fm && !a.rebalance && !(s_flags & 1u) && !a.exact_unb && !census_off;
+            int fast = !C.list_overflow && !s_fm && !(a.rebalance && (sm & SM_REASSIGN)) && !(s_flags & 1u) &&
+                       !a.exact_unb && !census_off;
             Decision d;
             d.status = 0; d.step = -1; d.kind = 0; d.slot = -1; d.part = -1; d.from = -1; d.to = -1;
             d.su = U0h; d.cu = U0h; d.w = 0.0; d.exact = 0; d.err = E_NONE; d.err_broker = -1; d.pad = 0;
-            for (int kind = a.allow_leader ? 0 : 1; fast && kind < 2; kind++) {
+            for (int kind = 0; fast && kind < 2; kind++) {
+                if (!(kind ? non_on : lead_on)) continue;
                 const int step = kind == 0 ? 7 : 8;
                 const int ndist = s_nd[kind];
                 if (s_kfail[kind] || ndist > 1) { fast = 0; break; }
@@ -1510,9 +1515,9 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
                     // a per-broker partition list ran out of slack: the host lays the
                     // lists out again (refresh) and the step runs again
                     s_exact_need = 1;
-                } else if (a.sem_go && F[F_DUP] != NONE32) {
+                } else if (a.sem_go && F[F_DUP] != NONE32 && (sm & SM_VALIDATE_REPLICAS)) {
                     D.status = -1; D.step = 1; D.err = E_DUP; D.part = F[F_DUP]; s_done = 1;
-                } else if (F[F_REMOVE] != NONE32) {                      // steps.go:70-89
+                } else if (F[F_REMOVE] != NONE32 && (sm & SM_REMOVE)) {  // steps.go:70-89
                     const uint32_t p = F[F_REMOVE];
                     const uint32_t m = a.meta[p];
                     const int nrep = (int)meta_nrep(m), set = (int)(BIG && a.pset ? a.pset[p] : meta_set(m));
@@ -1532,11 +1537,11 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
                         D.status = 1; D.kind = 2; D.slot = bslot; D.from = best; D.to = -1;
                     }
                     s_done = 1;
-                } else if (F[F_ADD] != NONE32) {                         // steps.go:93-113
+                } else if (F[F_ADD] != NONE32 && (sm & SM_ADD)) {       // steps.go:93-113
                     s_lkind = 2; s_lpart = F[F_ADD];                      // pick list below
-                } else if (F[F_DIS] != NONE32) {                         // steps.go:117-143
+                } else if (F[F_DIS] != NONE32 && (sm & SM_DISALLOWED)) { // steps.go:117-143
                     s_lkind = 1; s_lpart = F[F_DIS];
-                } else if (a.rebalance) {                                 // steps.go:234-282
+                } else if (a.rebalance && (sm & SM_REASSIGN)) {           // steps.go:234-282
                     // su < MinUnbalance decides; certify it against eps or use the exact su
                     const bool lo = su + 2.0 * eps < a.min_unbalance, hi = su - 2.0 * eps >= a.min_unbalance;
                     if (!lo && !hi) {
@@ -1647,7 +1652,8 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
             KB_STAMP(ctl, 3);
 
             // ---- move(): leader step (if allowed), then non-leader step (steps.go:284-298)
-            for (int kind = a.allow_leader ? 0 : 1; kind < 2 && !s_done && !s_exact_need; kind++) {
+            for (int kind = 0; kind < 2 && !s_done && !s_exact_need; kind++) {
+                if (!(kind ? non_on : lead_on)) continue;        // (uniform: the step mask)
                 const int step = kind == 0 ? 7 : 8;
                 const double g = s_g[kind];
                 if (tid == 0) {
@@ -1902,7 +1908,9 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
             const bool chg = D.status == 1;
             const long long p = D.part;
             const int kind = D.kind, slot = D.slot, to = D.to;
-            const bool fast = chg && kind == 1 && (D.step == 7 || D.step == 8);
+            // (a step mask without MoveDisallowedReplicas may run move() while some partition
+            // holds a disallowed replica: then the meta word can change, the general path)
+            const bool fast = chg && kind == 1 && (D.step == 7 || D.step == 8) && !(s_fm & (1u << F_DIS));
             bool upd = false, act = false;
             int b = -1, dcnt = 0, cv = 0;
             double oldc = 0.0, newc = 0.0, av = 0.0;
@@ -2094,12 +2102,14 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
             // reference candidate count of the steps that actually ran this iteration
             unsigned long long add = 0;
             if (D.step < 0 || D.step >= 7) {
-                if (a.allow_leader) add += s_cand[0];
-                if (D.step != 7) add += s_cand[1];
+                if (lead_on) add += s_cand[0];
+                if (D.step != 7 && non_on) add += s_cand[1];
             }
             C.total_cand += add;
             C.total_cont += (unsigned long long)(s_nd[0] + s_nd[1]);
-            if (D.status != 1) { C.halted = H_DONE; C.prepped = 0; }
+            // (a step mask's no-change leaves the state and its prep as they were: the
+            // next masked step resolves the same scan records, kb_engine_step)
+            if (D.status != 1) { C.halted = H_DONE; if (!(D.status == 0 && sm != SM_ALL)) C.prepped = 0; }
             }
         }
         __syncthreads();
@@ -3048,20 +3058,23 @@ __device__ __attribute__((noinline)) void refresh_in_scan(const RefreshArgs* rfp
     __shared__ int s_i;
     const int g = blockIdx.x, ng = gridDim.x;
     const bool ef = pend && kind != 3 && from >= 0, et = pend && kind != 2 && to >= 0;
+    bool ok = true;                       // (workgroup-uniform: list_insert reads llen / lcap)
     if (g == 0 && pend) {
-        bool ok = true;
         if (kind == 1) { list_remove(rf.L, from, part, &s_i); ok = list_insert(rf.L, to, part, &s_i); }
         else if (kind == 2) list_remove(rf.L, from, part, &s_i);
         else if (kind == 3) ok = list_insert(rf.L, to, part, &s_i);
         if (!ok && threadIdx.x == 0) rf.ctl->list_overflow = 1;   // the host relists (refresh)
         __syncthreads();
     }
+    // A failed insert left `to`'s list without the moved partition: neither edited broker
+    // is folded here, both stay dirty, and the host's refresh refolds them after the relist
+    // (the other workgroups' brokers have intact lists: their folds stand).
     for (int b = g; b < rf.B; b += ng) {
-        if (g != 0 && ((ef && b == from) || (et && b == to))) continue;   // workgroup 0's
-        if (!(rf.bfl[b] & BF_DIRTY)) continue;                           // (uniform)
+        if ((g != 0 || !ok) && ((ef && b == from) || (et && b == to))) continue;   // workgroup 0's
+        if (!(rf.bfl[b] & BF_DIRTY)) continue;                                     // (uniform)
         refold_broker<SCAN_THREADS, RF_CHUNK>(rf, b, buf);
     }
-    if (g == 0) {
+    if (g == 0 && ok) {
         if (ef && from % ng != 0 && (rf.bfl[from] & BF_DIRTY)) refold_broker<SCAN_THREADS, RF_CHUNK>(rf, from, buf);
         if (et && to % ng != 0 && to != from && (rf.bfl[to] & BF_DIRTY)) refold_broker<SCAN_THREADS, RF_CHUNK>(rf, to, buf);
     }
@@ -3175,6 +3188,7 @@ __global__ __launch_bounds__(1024) void k_summary(SumArgs a) {
         out->nkeys = s_n < (uint32_t)a.out.cap ? s_n : (uint32_t)a.out.cap;
         out->flags = ((ran && ctl->cont_overflow) || s_fail || s_n > (uint32_t)a.out.cap) ? 1u : 0u;
         if (ran) out->flags |= 2u;
+        if (ran && ctl->cont_overflow && a.spill_growable) out->flags |= 4u;   // (grow_summary)
         out->nkk[0] = (uint16_t)min(s_nkk[0], 0xFFFFu);
         out->nkk[1] = (uint16_t)min(s_nkk[1], 0xFFFFu);
         uint32_t m = 0;

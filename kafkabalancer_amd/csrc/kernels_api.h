@@ -112,6 +112,7 @@ struct SumArgs {
     uint32_t cont_cap;
     const double* r;
     Recs out;                 // one summary (summary_recs layout)
+    int spill_growable;       // 1: this rank's spill buffer can still grow (summary flag bit 2)
 };
 
 void launch_scan(const ScanArgs& a, int rc, bool lds_sets, size_t lds_bytes, hipStream_t st);

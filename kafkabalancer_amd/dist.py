@@ -176,6 +176,9 @@ def bench_main(args, world, rank, local):
     torch.cuda.synchronize()
     dist.barrier()
     torch.cuda.synchronize()
+    if rank == 0 and getattr(args, "plan_out", None):
+        with open(args.plan_out, "w") as f:
+            json.dump(changes, f)
     dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64,
                       device="cuda" if backend == "nccl" else "cpu")
     dist.all_reduce(dt, op=dist.ReduceOp.MAX)

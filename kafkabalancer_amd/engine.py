@@ -20,6 +20,7 @@ STEP_NAMES = ["ValidateWeights", "ValidateReplicas", "FillDefaults", "RemoveExtr
               "AddMissingReplicas", "MoveDisallowedReplicas", "ReassignLeaders", "MoveLeaders",
               "MoveNonLeaders"]
 KIND_NAMES = {0: "none", 1: "replace", 2: "remove", 3: "add", 4: "swap"}
+KB_STEPS_ALL = 0x1FF
 
 EXPORTS = ["kb_abi_version", "kb_engine_create", "kb_engine_balance", "kb_engine_plan",
            "kb_engine_replicas", "kb_engine_loads", "kb_engine_unbalance", "kb_engine_stats",
@@ -27,7 +28,7 @@ EXPORTS = ["kb_abi_version", "kb_engine_create", "kb_engine_balance", "kb_engine
            "kb_engine_last_error", "kb_engine_destroy", "kb_engine_summary_bytes",
            "kb_engine_step_begin", "kb_engine_step_finish", "kb_engine_set_stream",
            "kb_engine_sharded_reset", "kb_engine_sharded_scan", "kb_engine_sharded_resolve",
-           "kb_engine_sharded_collect", "kb_engine_set_incremental"]
+           "kb_engine_sharded_collect", "kb_engine_set_incremental", "kb_engine_step"]
 
 P64 = C.POINTER(C.c_int64)
 PD = C.POINTER(C.c_double)
@@ -62,7 +63,7 @@ class kb_stats(C.Structure):
                 ("n_brokers", C.c_int64), ("n_sets", C.c_int64), ("integral", C.c_int32),
                 ("max_replicas", C.c_int32), ("refreshes", C.c_int64), ("exact_halts", C.c_int64),
                 ("scan_workgroups", C.c_int64), ("retries", C.c_int64), ("spill_grows", C.c_int64),
-                ("blocks_scanned", C.c_int64)]
+                ("blocks_scanned", C.c_int64), ("relists", C.c_int64)]
 
 
 _lib = None
@@ -81,6 +82,8 @@ def lib():
         L.kb_engine_create.restype = C.c_int
         L.kb_engine_balance.argtypes = [vp, C.POINTER(kb_change)]
         L.kb_engine_balance.restype = C.c_int
+        L.kb_engine_step.argtypes = [vp, C.c_uint32, C.POINTER(kb_change)]
+        L.kb_engine_step.restype = C.c_int
         L.kb_engine_plan.argtypes = [vp, C.c_int64, C.POINTER(kb_change), P64]
         L.kb_engine_plan.restype = C.c_int
         L.kb_engine_replicas.argtypes = [vp, C.c_int64, P64, C.c_int64]
@@ -126,7 +129,7 @@ def lib():
         if hasattr(L, "kb_engine_set_incremental"):
             L.kb_engine_set_incremental.argtypes = [vp, C.c_int32]
             L.kb_engine_set_incremental.restype = C.c_int
-        if L.kb_abi_version() != 7 and not any_abi:
+        if L.kb_abi_version() != 8 and not any_abi:
             raise ImportError("libkbengine.so ABI mismatch")
         _lib = L
     return _lib
@@ -261,7 +264,11 @@ class Engine:
             self.close()
             raise EngineError(rc, "%s: %s" % (ERRORS.get(rc, rc), msg))
         if incremental:
-            self.set_incremental(True)
+            try:
+                self.set_incremental(True)
+            except EngineError:
+                self.close()          # (the handle created above: no leaked device memory)
+                raise
 
     def set_incremental(self, on):
         """Incremental rescoring mode: scans read only the partition blocks
@@ -279,6 +286,21 @@ class Engine:
         """One Balance() step; returns the change dict, None for no change; raises EngineError."""
         ch = kb_change()
         rc = lib().kb_engine_balance(self.h, C.byref(ch))
+        if rc == KB_NOCHANGE:
+            return None
+        if rc == KB_CHANGE:
+            return _change_dict(ch)
+        raise EngineError(rc, self.last_error(), _change_dict(ch))
+
+    def step(self, mask):
+        """One Balance() restricted to the steps in `mask` (bit k = STEP_NAMES[k]; a name or a
+        list of names also works): the change dict, None for no change; raises EngineError."""
+        if isinstance(mask, str):
+            mask = [mask]
+        if not isinstance(mask, int):
+            mask = sum(1 << STEP_NAMES.index(n) for n in mask)
+        ch = kb_change()
+        rc = lib().kb_engine_step(self.h, mask, C.byref(ch))
         if rc == KB_NOCHANGE:
             return None
         if rc == KB_CHANGE:
@@ -332,18 +354,20 @@ class Engine:
         lib().kb_engine_stats(self.h, C.byref(s))
         return {f: getattr(s, f) for f, _ in s._fields_}
 
-    KERNELS = ("step", "scan", "refresh")
+    KERNELS = ("step", "scan", "refresh", "bound")
 
     def timings(self):
-        """{kernel: (total_ms, launches)} of the last plan (time_kernels=True)."""
-        ms = np.zeros(3)
-        n = np.zeros(3, np.int64)
-        lib().kb_engine_timings(self.h, ms.ctypes.data_as(PD), n.ctypes.data_as(P64), 3)
+        """{kernel: (total_ms, launches)} of the plans since set_timing (time_kernels=True)."""
+        ms = np.zeros(4)
+        n = np.zeros(4, np.int64)
+        lib().kb_engine_timings(self.h, ms.ctypes.data_as(PD), n.ctypes.data_as(P64), 4)
         return {k: (float(ms[i]), int(n[i])) for i, k in enumerate(self.KERNELS)}
 
     def set_timing(self, on):
-        """Per-kernel HIP events on/off for the following plans (resets the sums)."""
-        rc = lib().kb_engine_set_timing(self.h, int(bool(on)))
+        """Kernel timing for the following plans (resets the sums): False/0 off, True/1
+        device clock for k_scan / k_step, 2 HIP events around every launch (dispatch
+        included, what rocprofv3 reports)."""
+        rc = lib().kb_engine_set_timing(self.h, 2 if on == 2 else int(bool(on)))
         if rc != 0:
             raise EngineError(rc, self.last_error())
 

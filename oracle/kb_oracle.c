@@ -579,6 +579,29 @@ int or_balance(or_plist *pl, const or_config *cfg, int sem, or_result *res) {
     return 0;
 }
 
+/* One Balance() over the steps whose bit is set in mask (bit k = steps table entry k,
+ * balancer.go:34-44), in table order; the first non-nil result wins (balancer.go:49-65).
+ * mask = 0x1FF is or_balance. */
+int or_step(or_plist *pl, const or_config *cfg, int sem, unsigned mask, or_result *res) {
+    memset(res, 0, sizeof *res);
+    res->pidx = -1;
+    int rc;
+    if (mask & 1u) {
+        if (pl->n == 0) { set_err(res, 0, "panic: index out of range"); return -1; }
+        if ((rc = validate_weights(pl, res)) != 0) return rc;
+    }
+    if ((mask & 2u) && (rc = validate_replicas(pl, res)) != 0) return rc;
+    if (mask & 4u) fill_defaults(pl, cfg);
+    if ((mask & 8u) && (rc = remove_extra(pl, sem, res)) != 0) return rc;
+    if ((mask & 16u) && (rc = add_missing(pl, sem, res)) != 0) return rc;
+    if ((mask & 32u) && (rc = move_disallowed(pl, sem, res)) != 0) return rc;
+    if ((mask & 64u) && cfg->rebalance_leaders && (rc = distribute_leaders(pl, cfg, sem, res)) != 0) return rc;
+    if ((mask & 128u) && cfg->allow_leader && (rc = move_impl(pl, cfg, 1, sem, res, -1, NULL, NULL)) != 0) return rc;
+    if ((mask & 256u) && (rc = move_impl(pl, cfg, 0, sem, res, -1, NULL, NULL)) != 0) return rc;
+    res->status = 0;
+    return 0;
+}
+
 int64_t or_move_sample(or_plist *pl, const or_config *cfg, int leaders, int64_t max_parts, double *cu) {
     or_result res; memset(&res, 0, sizeof res);
     int64_t cnt = 0;

@@ -70,6 +70,8 @@ typedef struct {
 } or_result;
 
 int  or_balance(or_plist *pl, const or_config *cfg, int semantics, or_result *res);
+/* Balance() over the steps in mask only (bit k = steps table entry k); 0x1FF = or_balance */
+int  or_step(or_plist *pl, const or_config *cfg, int semantics, unsigned mask, or_result *res);
 
 /* run() main loop (kafkabalancer.go:177-233) after parsing.  Writes the
  * output JSON (Go encoding/json format, trailing newline) into *out (malloc'd)

@@ -69,6 +69,8 @@ def lib():
                                      P(C.c_int64), P(C.c_int64)]
         L.or_balance.argtypes = [P(_PL), P(_Cfg), C.c_int, P(_Res)]
         L.or_balance.restype = C.c_int
+        L.or_step.argtypes = [P(_PL), P(_Cfg), C.c_int, C.c_uint, P(_Res)]
+        L.or_step.restype = C.c_int
         L.or_run_plan.argtypes = [P(_PL), P(_Cfg), C.c_int64, C.c_int, C.c_int, C.c_int, C.c_int,
                                   P(C.c_void_p), C.c_char_p, C.c_size_t, P(C.c_int64)]
         L.or_run_plan.restype = C.c_int
@@ -223,6 +225,19 @@ def balance(opl, cfg, sem=SEM_GO):
     res = _Res()
     c = make_cfg(cfg)
     lib().or_balance(opl.pl, C.byref(c), sem, C.byref(res))
+    out = {"status": res.status, "step": STEP_NAMES[res.step] if res.status else None,
+           "err": res.err.decode() if res.status < 0 else None}
+    if res.status == 1:
+        out.update(pidx=res.pidx, kind=KIND_NAMES[res.kind], from_=res.from_, to=res.to,
+                   slot=res.slot, partition=_part_to_dict(res.part), su=res.su, cu=res.cu)
+    return out
+
+
+def step(opl, cfg, mask, sem=SEM_GO):
+    """Balance() over the steps whose bit is set in mask (bit k = STEP_NAMES[k]) only."""
+    res = _Res()
+    c = make_cfg(cfg)
+    lib().or_step(opl.pl, C.byref(c), sem, mask, C.byref(res))
     out = {"status": res.status, "step": STEP_NAMES[res.step] if res.status else None,
            "err": res.err.decode() if res.status < 0 else None}
     if res.status == 1:

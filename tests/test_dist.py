@@ -8,9 +8,12 @@ rank applies the identical change, against the single-process oracle plan.
 GPU: two device engines on disjoint shards of one cluster on one GPU, their
 summaries concatenated as the all-gather would, against one unsharded engine.
 """
+import json
 import os
 import random
 import socket
+import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -437,7 +440,7 @@ def test_sharded_summary_capacity_is_the_same_verdict_on_every_rank(monkeypatch)
     e1 = E.Engine(pl, cfg, shard=shard_bounds(n, world, 1))
     engs = [e0, e1]
     verdicts = []
-    for _ in range(12):
+    for _ in range(16):
         nb = engs[0].summary_bytes()
         assert engs[1].summary_bytes() == nb
         bufs = [torch.zeros(nb, dtype=torch.uint8, device="cuda") for _ in range(world)]
@@ -458,7 +461,9 @@ def test_sharded_summary_capacity_is_the_same_verdict_on_every_rank(monkeypatch)
             break
     last = verdicts[-1]
     assert isinstance(last[0], tuple) and isinstance(last[1], tuple), verdicts
-    assert sum(v[0] == "grow" for v in verdicts) == 2              # 56 -> 448 -> 2048 keys
+    # 56 -> 448 -> 2048 keys; at 2048 the step runs again while rank 0's spill buffer (the
+    # one that overflowed) can still grow -- summary flag bit 2, the same verdict on both
+    assert sum(v[0] == "grow" for v in verdicts) >= 2
     for e in engs:
         assert "near-tied candidates in one rank summary" in e.last_error()
 
@@ -509,3 +514,31 @@ def test_rccl_world1_matches_oracle():
     assert oerr is None
     assert ch == [(c["step"], c["pidx"], c["kind"], c["from_"], c["to"], c["slot"]) for c in och]
     assert st == opl.state()
+
+
+@pytest.mark.gpu
+def test_bench_gpus2_spawns_two_ranks(tmp_path):
+    """`bench.py --gpus 2` with no launcher starts two ranks itself (torch.distributed.run as
+    a child process, before any GPU call in the parent); KB_DIST_BACKEND=gloo lets both
+    ranks share the box's one GPU.  The line says n_gpus 2, and the timed plan of the
+    strong-scaled (one cluster, two shards) run equals one engine's plan of the same steps."""
+    from kafkabalancer_amd import engine as E
+    from kafkabalancer_amd import synth
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = tmp_path / "plan.json"
+    env = dict(os.environ, KB_DIST_BACKEND="gloo")
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--workload", "c3",
+                        "--scale", "0.02", "--scaling", "strong", "--steps", "30", "--warmup", "5",
+                        "--no-cpu-baseline", "--plan-out", str(out)],
+                       cwd=root, env=env, capture_output=True, text=True, timeout=400)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["scaling"] == "strong", line
+    got = json.load(open(out))
+    cl, cfg, _ = synth.config("c3", scale=0.02)
+    eng = E.Engine(cl, cfg)
+    want, err = eng.plan(35)
+    assert err is None
+    key = lambda c: (c["step"], c["pidx"], c["kind"], c["from_"], c["to"], c["slot"])
+    assert [key(c) for c in got] == [key(c) for c in want[5:35]]
+    eng.close()

@@ -206,3 +206,28 @@ def test_in_stream_refresh_matches_host_refresh(monkeypatch):
     check_loads(eng, cl, ch)
     eng.close()
     ref.close()
+
+
+@pytest.mark.gpu
+def test_list_overflow_relists_match_host_refresh(monkeypatch):
+    """c5's shape (1M x 4096) with one free entry per broker list (kb_config.list_slack = 1):
+    the per-broker partition lists run out of room again and again -- also inside the
+    in-stream refresh, whose pending list edit then fails (neither edited broker may be
+    refolded from the incomplete list; the host relists and refolds them).  The plan and
+    the loads equal the default-slack engine's with host refreshes, and getBrokerLoad of
+    the replayed plan."""
+    cl, cfg, _ = synth.config("c5", scale=0.1)
+    eng = E.Engine(cl, cfg, list_slack=1)
+    ch, err = eng.plan(150)
+    assert err is None, err
+    st = eng.stats()
+    monkeypatch.setenv("KB_RF_STREAM", "0")
+    ref = E.Engine(cl, cfg)
+    rch, rerr = ref.plan(150)
+    assert rerr is None, rerr
+    assert st["relists"] > 0 and st["exact_halts"] > 0, st
+    assert ch == rch
+    assert eng.loads() == ref.loads()
+    check_loads(eng, cl, ch)
+    eng.close()
+    ref.close()
