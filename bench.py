@@ -8,12 +8,13 @@ Balance() call (balancer.go:49-65) executed device-resident by kb_engine_plan;
 over the timed steps, per wall second.
 
 Roofline: the streaming kernel is k_scan; `achieved` = its algorithmic
-bytes per launch / its average in-plan launch duration, timed with HIP events around
-every launch on the engine's stream (dispatch included: the interval rocprofv3
---kernel-trace reports, so profiles/*/c3_kernel_stats.csv recomputes it).  The
-device-clock duration (first scan workgroup start to last end) and the whole-step
-fraction `frac_step` (SURVEY 8(d) bytes per step / ms_per_step / 8 TB/s) are reported
-beside it.  `traffic` is the rocprofv3 PMC figure for the same workload
+bytes per launch / its average in-plan launch duration, measured live on the engine's
+stream with the device clock: each launch's span from the end of the kernel before it to
+its own last workgroup's end (dispatch included: the interval rocprofv3 --kernel-trace
+reports, so the committed profiles/*/c3_kernel_stats.csv recomputes it; HIP events
+around each launch add ~2-3 us of their own and are reported as a side figure).  The
+inner duration (first scan workgroup start to last end) and the whole-step fraction
+`frac_step` (SURVEY 8(d) bytes per step / ms_per_step / 8 TB/s) are reported beside it.  `traffic` is the rocprofv3 PMC figure for the same workload
 (profiles/pmc_traffic.json, keyed by workload, stamped with the git head it ran on).
 
 Multi-GPU: under torch.distributed.run (WORLD_SIZE set) kafkabalancer_amd.dist.bench_main;
@@ -390,23 +391,28 @@ def main():
     dev_s = st1["device_ms"] / 1e3
     ms_per_step = 1e3 * wall / max(steps, 1)
     # per-kernel durations over two more stretches of the same plan, outside the headline
-    # timing: (a) HIP events around every launch -- dispatch included, the interval
-    # rocprofv3 --kernel-trace reports (the roofline's figure); (b) the device clock (each
-    # scan workgroup stamps its start / end, k_step folds the interval), a side figure
+    # timing: (a) the device clock (scan workgroups and k_step stamp the 100 MHz clock):
+    # each launch's span from the end of the kernel before it to its own end -- dispatch
+    # included, the interval rocprofv3 --kernel-trace reports, so the scan + step spans add
+    # up to the step time (the roofline's figure) -- and the inner interval, first workgroup
+    # start .. last end; (b) HIP events around every launch (each event adds its own
+    # ~2-3 us: an upper bound, a side figure)
     kt_steps = min(args.steps, 200)
     stk0 = eng.stats()
-    kev = kernel_times(eng, kt_steps, 2)
-    stk1 = eng.stats()
     kdc = kernel_times(eng, kt_steps, 1)
-    scan_us, scan_n = kev["scan"]
-    scan_clock_us = kdc["scan"][0]
+    stk1 = eng.stats()
+    kev = kernel_times(eng, kt_steps, 2)
+    scan_us, scan_n = kdc["scan"]
+    if not scan_n:                      # (no back-to-back launch: the inner interval)
+        scan_us, scan_n = kdc["scan_inner"]
+    scan_clock_us = kdc["scan_inner"][0]
     scan_iso_us = eng.bench_scan(200) if args.isolated_scan else None
     bytes_scan = st1["scan_bytes"]
     if incr:
         # bytes the incremental scans actually read: their blocks' partition words
         # (+ the 16-B block descriptors), per scan launch of the events stretch
         per_part = bytes_scan / max(cl.n, 1)
-        nscans = max(scan_n, 1)
+        nscans = max(kdc["scan_inner"][1], 1)
         blk = stk1["blocks_scanned"] - stk0["blocks_scanned"]
         bytes_scan = blk * 128 * per_part / nscans + 16 * blk / nscans
     achieved = bytes_scan / (scan_us * 1e-6) / 1e9
@@ -426,10 +432,14 @@ def main():
                                      "descriptor); the full scan reads %d" % st1["scan_bytes"]
                                      if incr else ""),
             "avg_launch_us": scan_us,
-            "timing": "HIP events around each in-plan k_scan launch (dispatch included, the interval "
-                      "rocprofv3 --kernel-trace reports), %d launches" % scan_n,
+            "timing": "device clock (100 MHz), in-plan launches back to back: the previous k_step's end "
+                      "to the last scan workgroup's end (dispatch included, the interval rocprofv3 "
+                      "--kernel-trace reports), %d launches" % scan_n,
             "avg_launch_us_device_clock": scan_clock_us,
+            "device_clock_def": "first scan workgroup start .. last end (no dispatch)",
             "frac_device_clock": bytes_scan / (scan_clock_us * 1e-6) / 1e9 / HBM_PEAK_GBS,
+            "avg_launch_us_events": kev["scan"][0],
+            "events_def": "HIP events around every launch (each event adds its own time: an upper bound)",
             "frac_step": whole_gbs / HBM_PEAK_GBS,
             "frac_step_def": "SURVEY.md 8(d) algorithmic bytes of the timed steps / their wall time / 8 TB/s"
                              + (" (early-exit stages counted to their hit: ms_per_step is the headline, "
@@ -458,10 +468,10 @@ def main():
         "config": dict(desc, parallelism="single-gpu", device_ms_per_step=1e3 * dev_s / max(steps, 1),
                        mode=args.mode),
         "roofline": roof,
-        "kernels_us_per_launch": {k: v[0] for k, v in kev.items() if v[1]},
-        "kernels_launches": {k: v[1] for k, v in kev.items() if v[1]},
-        "kernels_us_per_launch_device_clock": {k: kdc[k][0] for k in ("scan", "step")},
-        "incremental": ({"blocks_per_scan": (stk1["blocks_scanned"] - stk0["blocks_scanned"]) / max(scan_n, 1),
+        "kernels_us_per_launch": {k: v[0] for k, v in kdc.items() if v[1]},
+        "kernels_launches": {k: v[1] for k, v in kdc.items() if v[1]},
+        "kernels_us_per_launch_events": {k: v[0] for k, v in kev.items() if v[1]},
+        "incremental": ({"blocks_per_scan": (stk1["blocks_scanned"] - stk0["blocks_scanned"]) / max(kdc["scan_inner"][1], 1),
                          "blocks_total": (cl.n + 127) // 128} if incr else None),
         "kernel_timing_steps": kt_steps,
         "engine_events": {k: st1[k] - st0[k] for k in ("retries", "refreshes", "exact_halts", "exact_folds")},

@@ -194,16 +194,18 @@ double kb_engine_unbalance(kb_engine *e);
 
 int kb_engine_stats(kb_engine *e, kb_stats *out);
 
-/* Per-kernel device time of the last kb_engine_plan when timing was on: ms[k] = summed
- * duration of kernel k over the plan, launches[k] = count, for k in {0 k_step (resolve +
- * apply + prep), 1 k_scan, 2 k_refresh, 3 the conditional bound pass (k_scan ubpass +
- * k_ubinit; mode 2 only)}.  Returns 4. */
+/* Per-kernel device time of the plans since kb_engine_set_timing: ms[k] = summed duration
+ * of kernel k, launches[k] = count, for k in {0 k_step (resolve + apply + prep), 1 k_scan,
+ * 2 k_refresh, 3 the conditional bound pass (k_scan ubpass + k_ubinit; mode 2 only),
+ * 4 k_step and 5 k_scan first-workgroup-start .. last-end (mode 1 only)}.  In mode 1,
+ * k = 0 / 1 are device-clock spans from the end of the kernel before (dispatch included:
+ * the interval rocprofv3 --kernel-trace reports), over back-to-back launches.  Returns 6. */
 int kb_engine_timings(kb_engine *e, double *ms, int64_t *launches, int n);
 
 /* Kernel timing for the following plans (resets the sums): 0 off; 1 k_scan / k_step from
- * the device clock (first workgroup start .. last end, no events between them), the rest
- * from HIP events; 2 HIP events around every launch (dispatch included: the interval
- * rocprofv3 --kernel-trace reports; the kernels run as in production). */
+ * the device clock (workgroups stamp the 100 MHz clock; no events between them), the rest
+ * from HIP events; 2 HIP events around every launch (each event adds its own ~2-3 us to
+ * the interval around a launch). */
 int kb_engine_set_timing(kb_engine *e, int32_t on);
 
 /* Incremental rescoring mode (single GPU, off by default): after a

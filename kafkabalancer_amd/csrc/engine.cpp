@@ -918,6 +918,12 @@ static int convert(kb_engine* e, const ChangeDev& d, kb_change* o) {
             break;
         case E_CONT_OVERFLOW: e->last_err = step + ": engine capacity: near-tie buffer overflow"; rc = KB_ERR_CAPACITY; break;
         case E_LIST_OVERFLOW: e->last_err = step + ": engine capacity: broker list overflow"; rc = KB_ERR_CAPACITY; break;
+        case E_DUP_UNSUP:
+            e->last_err = step + ": engine: partition " + ps + " holds duplicated replicas (Go aliasing after a "
+                          "remove) and ValidateReplicas is not in the step mask; the engine's loads assume "
+                          "distinct replicas";
+            rc = KB_ERR_UNSUPPORTED;
+            break;
         default: e->last_err = step + ": error"; break;
     }
     o->status = rc;
@@ -1250,18 +1256,23 @@ extern "C" int kb_engine_timings(kb_engine* e, double* ms, int64_t* launches, in
     HIPCHK(hipStreamSynchronize(e->st));
     HIPCHK(hipMemcpy(&c, e->ctl, sizeof c, hipMemcpyDeviceToHost));
     const double tick_ms = 1e-5;
-    double kms[TK_N];
-    int64_t kn[TK_N];
+    double kms[TK_N + 2];
+    int64_t kn[TK_N + 2];
     for (int k = 0; k < TK_N; k++) { kms[k] = e->kms[k]; kn[k] = e->klaunch[k]; }
+    kms[TK_N] = kms[TK_N + 1] = 0; kn[TK_N] = kn[TK_N + 1] = 0;
     if (e->time_kernels == 1) {
-        kms[TK_STEP] = (double)c.tk_sum[1] * tick_ms; kn[TK_STEP] = (int64_t)c.tk_n[1];
-        kms[TK_SCAN] = (double)c.tk_sum[0] * tick_ms; kn[TK_SCAN] = (int64_t)c.tk_n[0];
+        // spans (dispatch included, rocprofv3's interval) and the inner device-clock
+        // intervals (first workgroup start .. last end)
+        kms[TK_STEP] = (double)c.tk_span[1] * tick_ms; kn[TK_STEP] = (int64_t)c.tk_span_n[1];
+        kms[TK_SCAN] = (double)c.tk_span[0] * tick_ms; kn[TK_SCAN] = (int64_t)c.tk_span_n[0];
+        kms[TK_N] = (double)c.tk_sum[1] * tick_ms; kn[TK_N] = (int64_t)c.tk_n[1];
+        kms[TK_N + 1] = (double)c.tk_sum[0] * tick_ms; kn[TK_N + 1] = (int64_t)c.tk_n[0];
     }
-    for (int k = 0; k < TK_N && k < n; k++) {
+    for (int k = 0; k < TK_N + 2 && k < n; k++) {
         if (ms) ms[k] = kms[k];
         if (launches) launches[k] = kn[k];
     }
-    return TK_N;
+    return TK_N + 2;
 }
 
 extern "C" int kb_engine_set_timing(kb_engine* e, int32_t on) {
@@ -1275,8 +1286,10 @@ extern "C" int kb_engine_set_timing(kb_engine* e, int32_t on) {
     HIPCHK(hipMemcpy(&c, e->ctl, sizeof c, hipMemcpyDeviceToHost));
     c.tk_on = e->time_kernels == 1;                 // (mode 2: events only, production kernels)
     c.tk_sum[0] = c.tk_sum[1] = c.tk_n[0] = c.tk_n[1] = 0;
+    c.tk_span[0] = c.tk_span[1] = c.tk_span_n[0] = c.tk_span_n[1] = 0;
     c.ts_beg = NONE64;
     c.ts_end = 0;
+    c.ts_prev_end = 0;
     HIPCHK(hipMemcpy(e->ctl, &c, sizeof c, hipMemcpyHostToDevice));
     *e->h_ctl = c;
     return KB_OK;

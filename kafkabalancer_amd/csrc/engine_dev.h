@@ -191,6 +191,11 @@ struct DevCtl {
     // kernel timing (tk_on): summed device-clock durations (100 MHz ticks) and launch
     // counts, {k_scan, k_step}; k_step folds in the scan's interval below
     unsigned long long tk_sum[2], tk_n[2];
+    // ... and the rocprofv3-comparable spans: a launch runs from the end of the kernel before
+    // it (its dispatch included) to its own end -- {k_scan: previous k_step end .. last scan
+    // workgroup end, k_step: scan end .. k_step end}; only launches queued back to back
+    // (first workgroup within 10 us of the previous end) are counted
+    unsigned long long tk_span[2], tk_span_n[2];
     int32_t tk_on;
     uint32_t step_mask;             // steps the next Balance() may take (bit = kb_step; SM_ALL)
     // incremental mode (kb_engine_set_incremental): incr_ok = the next scan
@@ -215,6 +220,7 @@ struct DevCtl {
     // the running scan's interval: earliest workgroup start, latest end (atomics;
     // outside the block k_step copies to LDS and back)
     unsigned long long ts_beg, ts_end;
+    unsigned long long ts_prev_end;     // the last k_step's end (100 MHz), for the spans
 };
 
 #ifdef KB_STAMPS
@@ -264,7 +270,8 @@ struct DevCtl {
 // errors recorded in ChangeDev.err_code
 enum {
     E_NONE = 0, E_DUP = 1, E_REMOVE = 2, E_ADD = 3, E_DIS = 4, E_PANIC = 5,
-    E_CONT_OVERFLOW = 6, E_LIST_OVERFLOW = 7
+    E_CONT_OVERFLOW = 6, E_LIST_OVERFLOW = 7,
+    E_DUP_UNSUP = 8     // kb_engine_step without ValidateReplicas on a state holding duplicates (Go sem)
 };
 
 }  // namespace kbe

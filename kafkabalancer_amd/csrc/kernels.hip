@@ -1155,17 +1155,22 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
     constexpr int NW = STEP_THREADS / 64;
     const unsigned long long t_in = wall_clock64();
     KB_STAMP_BEGIN();
+    __shared__ unsigned long long s_span_from;      // (kernel timing: the scan's end, or 0)
     auto write_back = [&]() {
         KB_STAMP_FLUSH(ctl);
         __syncthreads();
+        unsigned long long t_out = 0;
         if (tid == 0 && C.tk_on) {
             // kernel timing: this launch (the scan's interval was folded in at the start:
             // a load here would wait for every store this thread issued)
-            C.tk_sum[1] += wall_clock64() - t_in;
+            t_out = wall_clock64();
+            C.tk_sum[1] += t_out - t_in;
             C.tk_n[1]++;
+            if (s_span_from) { C.tk_span[1] += t_out - s_span_from; C.tk_span_n[1]++; }
         }
         __syncthreads();
         if (tid < CTL_WORDS) ((uint32_t*)ctl)[tid] = ((const uint32_t*)&C)[tid];
+        if (tid == 0 && t_out) ctl->ts_prev_end = t_out;
     };
     // diagnostic phase stops: a -DKB_STOP_AT=k build returns after phase k (the code
     // after it is dead there); kb_engine_bench_step times such builds on a fixed input
@@ -1211,6 +1216,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
     // all issued before the first LDS write; measured faster than LDS-DMA of the same
     // bytes, 16.5 vs 19.9 us per k_step at c3).  The record headers come to registers.
     const unsigned long long ts_b = ctl->ts_beg, ts_e = ctl->ts_end;   // (kernel timing, tk_on)
+    const unsigned long long ts_pe = ctl->ts_prev_end;
     if (tid < CTL_WORDS) ((uint32_t*)&C)[tid] = ((const uint32_t*)ctl)[tid];
     for (int b = tid; b < B; b += STEP_THREADS) {
         s_ld[b] = a.load[b];
@@ -1256,10 +1262,19 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
             __syncthreads();
         }
     }
+    if (tid == 0) s_span_from = 0;
     if (tid == 0 && C.tk_on) {
-        // kernel timing: the interval of the scan that ran before this launch (if any)
+        // kernel timing: the interval of the scan that ran before this launch (if any), and
+        // the spans when the scan followed the last k_step and this launch the scan back to
+        // back (no host gap: the first workgroup within 10 us of the previous end)
         const unsigned long long b = ts_b, e = ts_e;
-        if (b != NONE64 && e > b) { C.tk_sum[0] += e - b; C.tk_n[0]++; }
+        if (b != NONE64 && e > b) {
+            C.tk_sum[0] += e - b; C.tk_n[0]++;
+            if (ts_pe && b > ts_pe && b - ts_pe < 1000 && t_in > e && t_in - e < 1000) {
+                C.tk_span[0] += e - ts_pe; C.tk_span_n[0]++;
+                s_span_from = e;
+            }
+        }
         ctl->ts_beg = NONE64;
         ctl->ts_end = 0;
     }
@@ -1517,6 +1532,12 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
                     s_exact_need = 1;
                 } else if (a.sem_go && F[F_DUP] != NONE32 && (sm & SM_VALIDATE_REPLICAS)) {
                     D.status = -1; D.step = 1; D.err = E_DUP; D.part = F[F_DUP]; s_done = 1;
+                } else if (a.sem_go && F[F_DUP] != NONE32 && (sm & (SM_ALL & ~7u))) {
+                    // a step mask without ValidateReplicas over duplicated replicas (a Go-aliased
+                    // remove): the reference goes on over them, the engine's loads and
+                    // lists hold distinct replicas only -- an explicit error, never a guess
+                    D.status = -1; D.step = __ffs(sm & (SM_ALL & ~7u)) - 1; D.err = E_DUP_UNSUP;
+                    D.part = F[F_DUP]; s_done = 1;
                 } else if (F[F_REMOVE] != NONE32 && (sm & SM_REMOVE)) {  // steps.go:70-89
                     const uint32_t p = F[F_REMOVE];
                     const uint32_t m = a.meta[p];
