@@ -10,6 +10,7 @@ from collections import defaultdict
 tag = sys.argv[1] if len(sys.argv) > 1 else "pmcb"
 out = sys.argv[2] if len(sys.argv) > 2 else None
 workload = sys.argv[3] if len(sys.argv) > 3 else "c3"
+git_head = sys.argv[4] if len(sys.argv) > 4 else None      # the tree the passes ran on
 
 
 def per_kernel(counter):
@@ -55,6 +56,8 @@ if out:
         merged = json.load(open(out))
     except (OSError, ValueError):
         merged = {}
+if git_head:
+    doc["git_head"] = git_head
 merged[workload] = doc
 merged["method"] = method + " Keyed by bench workload."
 s = json.dumps(merged, indent=1)
