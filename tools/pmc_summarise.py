@@ -13,6 +13,18 @@ workload = sys.argv[3] if len(sys.argv) > 3 else "c3"
 git_head = sys.argv[4] if len(sys.argv) > 4 else None      # the tree the passes ran on
 
 
+def kernel_key(name):
+    """k_scan = the full-scan instantiations (k_scan<RC, LSETS, false>); k_scan_bound = the
+    block-list instantiation (k_scan<RC, LSETS, true>: the conditional bound passes and the
+    incremental mode); k_step; k_ubinit."""
+    if "k_scan" in name:
+        return "k_scan_bound" if name.replace(" ", "").split(">")[0].endswith(",true") else "k_scan"
+    for k in ("k_step", "k_ubinit", "k_refresh", "k_summary"):
+        if k in name:
+            return k
+    return None
+
+
 def per_kernel(counter):
     files = glob.glob("gpurun_out/%s_%s/**/*counter_collection.csv" % (tag, counter), recursive=True)
     vals = defaultdict(dict)
@@ -20,8 +32,7 @@ def per_kernel(counter):
         for r in csv.DictReader(open(f)):
             if r["Counter_Name"] != counter:
                 continue
-            name = r["Kernel_Name"]
-            k = "k_scan" if "k_scan" in name else "k_step" if "k_step" in name else None
+            k = kernel_key(r["Kernel_Name"])
             if k:
                 d = int(r["Dispatch_Id"])
                 vals[k][d] = vals[k].get(d, 0.0) + float(r["Counter_Value"])
@@ -29,10 +40,10 @@ def per_kernel(counter):
     for k, m in vals.items():
         xs = [m[d] for d in sorted(m)][10:]
         if k == "k_scan" and xs:
-            # full scans only: the conditional bound passes (ubpass) return after their
-            # first-tile prefetch and would drag the mean below one scan's traffic
-            top = max(xs)
-            xs = [x for x in xs if x >= 0.5 * top]
+            # full scans only: a scan of a step that was already decided (a census-free
+            # retry, a halted pair's no-op launch) returns after its first-tile prefetch
+            med = sorted(xs)[len(xs) // 2]
+            xs = [x for x in xs if x >= 0.5 * med]
         res[k] = (sum(xs) / max(len(xs), 1), len(xs))
     return res
 
@@ -46,7 +57,8 @@ for k in sorted(set(fetch) & set(write)):
               "read_bytes_per_launch": rd, "write_bytes_per_launch": wr, "traffic_bytes_per_launch": rd + wr}
 doc["method"] = ("rocprofv3 --kernel-trace --pmc FETCH_SIZE, then --pmc WRITE_SIZE (separate passes) over "
                  "the bench command of the workload (tools/pmc_bench.sh, tools/gpu_bench_r02.sh); mean over "
-                 "dispatches after the first 10 (k_scan: full scans only, FETCH >= half the largest); FETCH_SIZE doubled per MI355X_MICROARCH.md (gfx950 reports half "
+                 "dispatches after the first 10 (k_scan = the full-scan instantiation, its launches with FETCH >= half "
+                 "the median; k_scan_bound = the block-list instantiation of the bound passes); FETCH_SIZE doubled per MI355X_MICROARCH.md (gfx950 reports half "
                  "of 16-B/lane streaming reads); KB = 1024 B. k_step's reads are not 16-B streaming, so its "
                  "doubled figure is an upper estimate.")
 method = doc.pop("method")
