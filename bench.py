@@ -63,6 +63,10 @@ def _move_sample(cl, cfg, seconds):
     from oracle import oracle as O
     O.set_threads(1)
     opl = _oracle_pl(cl)
+    # ValidateWeights / ValidateReplicas / FillDefaults first (steps.go:7-66): nil Brokers
+    # lists (c5's auto lists) become the default list, as before the reference's move()
+    r = O.step(opl, cfg, 0x7, O.SEM_APPLIED)
+    assert r["status"] == 0, r["err"]
     P = cl.n
     leaders = bool(cfg.get("allow_leader"))
     k = 16

@@ -1108,8 +1108,22 @@ extern "C" int kb_engine_step(kb_engine* e, uint32_t step_mask, kb_change* out) 
         if (step_mask >> e->pending_step) return pending_result(e, out);
         return nochange();
     }
+    // the steps that could change something: ValidateWeights / FillDefaults never (create
+    // ran them), ValidateReplicas only under Go aliasing, ReassignLeaders / MoveLeaders
+    // only with their flags (steps.go:292-307 return nil, nil otherwise); with the records
+    // of an unchanged state at hand, a first-index step whose predicate no partition
+    // holds (the last resolve's DevCtl.last_fm) changes nothing either
     uint32_t dev = step_mask & ~(uint32_t)(SM_VALIDATE_WEIGHTS | SM_FILL_DEFAULTS);
     if (e->sem != KB_SEM_GO) dev &= ~(uint32_t)SM_VALIDATE_REPLICAS;
+    if (!e->rebalance) dev &= ~(uint32_t)SM_REASSIGN;
+    if (!e->allow_leader) dev &= ~(uint32_t)SM_MOVE_LEADERS;
+    if (e->recs_fresh) {
+        const uint32_t fm = e->h_ctl->last_fm;
+        if (!(fm & (1u << F_DUP))) dev &= ~(uint32_t)SM_VALIDATE_REPLICAS;
+        if (!(fm & (1u << F_REMOVE))) dev &= ~(uint32_t)SM_REMOVE;
+        if (!(fm & (1u << F_ADD))) dev &= ~(uint32_t)SM_ADD;
+        if (!(fm & (1u << F_DIS))) dev &= ~(uint32_t)SM_DISALLOWED;
+    }
     if (!dev) return nochange();                  // (no device work: the records stay)
     e->last_ms = 0;
     e->step_mask = step_mask;                     // (k_step never tests bits 0 and 2)

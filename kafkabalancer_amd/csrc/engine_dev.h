@@ -205,6 +205,9 @@ struct DevCtl {
     int32_t incr_ok;
     int32_t ub_sub;                 // > 0: the conditional bound pass may scan only the blocks of
                                     // the last records' best keys (StepArgs.ubdesc), not all
+    uint32_t last_fm;               // first-index predicates the last resolved scan found (bit q:
+    int32_t last_fm_pad;            //   F_q somewhere; kb_engine_step answers a masked first-index
+                                    //   step whose predicate is absent without a launch)
 
     double wskip;
     unsigned long long cand_cache[2];
@@ -213,6 +216,12 @@ struct DevCtl {
                                         // lower-bound prune reads it instead of reducing r[]
     unsigned long long total_rf_stream; // exact refolds run in the stream (the next pair's first
                                         // scan refolds, its k_step resumes: no host round trip)
+    // frozen-average prep (k_step's fused incremental prep): between full recomputes of the
+    // load sum, avg / inv_avg stay fixed (the real sum is invariant under moves), so only the
+    // touched brokers' r[] change and U0 / V / E / R follow incrementally; uerr bounds the
+    // rounding those updates added to U0, frz_n counts the steps since the base (0: none)
+    double uerr, rm_bound;          // rm_bound: max |r| over bl_move (an upper bound when frozen)
+    int32_t frz_n, frz_pad;
     // diagnostic phase stamps (builds with -DKB_STAMPS): accumulated
     // shader-clock ticks (clock64) per phase of k_step; [24]/[25] the wall-clock
     // (100 MHz) and shader-clock length of k_step; [26] one stamp's own cost

@@ -1204,6 +1204,8 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
     uint64_t* s_sb = (uint64_t*)(dsm + LY.sb);       // allowed-set words (sb_lds)
     uint8_t* s_fl = dsm + LY.fl;                     // BF_* flags
     __shared__ int s_T[TMAX], s_posT[TMAX];
+    __shared__ double s_Lold[TMAX], s_ebold[TMAX];  // touched brokers' load / bound before the apply
+    __shared__ int s_memb;                          // the apply changed bl_move's membership
     __shared__ int s_cntT[TMAX];
     __shared__ uint64_t s_blmb[MAXB / 64], s_presb[MAXB / 64];
     __shared__ uint32_t s_smark[MAX_SETS / 32];
@@ -1291,7 +1293,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
     __shared__ uint32_t s_lpart;
     __shared__ int s_lrep[MAXR + 1];
     __shared__ unsigned long long s_lsb[64];
-    if (tid == 0) { s_nT = 0; s_done = 0; s_exact_need = 0; s_retry = 0; s_moved = -1; s_lkind = 0; }
+    if (tid == 0) { s_nT = 0; s_done = 0; s_exact_need = 0; s_retry = 0; s_moved = -1; s_lkind = 0; s_memb = 0; }
     if (tid < NF) s_first[tid] = NONE32;
     if (tid < 2) { s_kc[tid] = 0; s_sok[tid] = -1; }   // (s_sok: -1 = no record offered its best key)
     if (halted != H_RUN) return;
@@ -1350,6 +1352,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
                 s_g[0] = g0; s_g[1] = g1; s_cand[0] = c0; s_cand[1] = c1;
                 s_flags = flg | (a.use_spill && C.cont_overflow ? 1u : 0u);
                 s_fm = fm;
+                C.last_fm = fm;
             }
         }
         __syncthreads();
@@ -2062,11 +2065,16 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
                 const bool touched = act && oldc != newc;
                 const bool cnt_changes = act && dcnt != 0;
                 int dd = 0;
+                double Lold = 0.0, ebold = 0.0;
+                bool mchg = false;
                 if (touched || cnt_changes) {
                     const int cnew = cv + dcnt;
                     if (dcnt) a.cnt[b] = cnew;
                     if (touched) {
                         const double L = s_ld[b];
+                        Lold = L;
+                        ebold = s_e[b];
+                        const uint8_t fl0 = s_fl[b];
                         uint8_t fl = s_fl[b] & ~BF_PRESENT;
                         if (cnew > 0) fl |= BF_PRESENT;
                         double Ln, eb = 0.0;
@@ -2089,6 +2097,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
                         a.load[b] = Ln; s_ld[b] = Ln;
                         a.eb[b] = eb; s_e[b] = eb;
                         a.bfl[b] = fl; s_fl[b] = fl;
+                        mchg = ((fl0 ^ fl) & BF_PRESENT) && !(fl & BF_INCFG);
                     }
                 }
                 KB_STAMP(ctl, 22);
@@ -2096,8 +2105,9 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
                 const unsigned long long bt = __ballot(touched);
                 if (touched) {
                     const int k = (int)__popcll(bt & ((1ull << lane) - 1ull));
-                    if (k < TMAX) s_T[k] = b;
+                    if (k < TMAX) { s_T[k] = b; s_Lold[k] = Lold; s_ebold[k] = ebold; }
                 }
+                if (__ballot(mchg) && lane == 0) s_memb = 1;
                 nT = (int)__popcll(bt);
                 if (nT > TMAX) nT = TMAX;
                 if (lane == 0) {
@@ -2161,6 +2171,15 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
         constexpr int OT = STEP_THREADS - NRW * 64;     // order-wave threads
         constexpr int NQ = (MAXB + OT - 1) / OT;
         const int ot = tid - NRW * 64;                  // order-wave thread index (< 0: sum wave)
+        // frozen average: after a plain move (bl_move unchanged) the real load sum is what the
+        // last full recompute folded, so avg / inv_avg stay; only the touched brokers' r
+        // change, and U0 / V / E / R / the r range follow incrementally (the sums over every
+        // broker and their reductions are skipped).  eps doubles (the frozen fold's rounding
+        // next to a fresh fold's) plus uerr, the rounding of the incremental U0 updates.  A
+        // full recompute every FRZ_MAX steps, after a membership change and after a full prep.
+        constexpr int FRZ_MAX = 1024;
+        const bool frz = do_res && D.status == 1 && !s_memb && C.frz_n > 0 && C.frz_n < FRZ_MAX && !(KB_ABL & 32);
+        __shared__ double s_fz[6];                      // frozen step: dU, |updates|, dV, dE, r lo / hi
         __shared__ double s_fq[2][NRW], s_fq2[7][NW];
         __shared__ int s_fcnt[NRW];
         __shared__ int s_rt[MAXB / 64];                 // bl_move brokers per 64 universe positions
@@ -2203,15 +2222,18 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
         if (wid < NRW) {
             double sS = 0.0, sE = 0.0;
             int cn = 0;
-            for (int b0 = wid * 64; b0 < B; b0 += NRW * 64) {
+            for (int b0 = wid * 64; b0 < ((KB_ABL & 4) ? 0 : B); b0 += NRW * 64) {
                 const int b = b0 + lane;
                 const bool in = b < B && (s_fl[b] & (BF_PRESENT | BF_INCFG));
                 if (in) { sS += s_ld[b]; sE += s_e[b]; cn++; }
                 const unsigned long long m = __ballot(in);
                 if (lane == 0) s_blmb[b0 >> 6] = m;
             }
-            sS = wave_sum(sS); sE = wave_sum(sE); cn = wave_sum(cn);
-            if (lane == 0) { s_fq[0][wid] = sS; s_fq[1][wid] = sE; s_fcnt[wid] = cn; }
+            if (!frz) {
+                sS = wave_sum(sS); sE = wave_sum(sE); cn = wave_sum(cn);
+                if (KB_ABL & 4) { sS = wid ? 0.0 : C.S; sE = wid ? 0.0 : C.E; cn = wid ? 0 : C.nblm; }   // (timing only)
+                if (lane == 0) { s_fq[0][wid] = sS; s_fq[1][wid] = sE; s_fcnt[wid] = cn; }
+            }
         } else {
             if (nT > 0)
                 for (int i = ot; i < B; i += OT) {
@@ -2244,12 +2266,35 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
             // (the same fixed-order combination on every such wave: identical bits)
             const double S = ((s_fq[0][0] + s_fq[0][1]) + s_fq[0][2]) + s_fq[0][3];
             const int nblm = (s_fcnt[0] + s_fcnt[1]) + (s_fcnt[2] + s_fcnt[3]);
-            const double avg = S / (double)nblm;
-            const double iav = 1.0 / avg;
+            const double avg = frz ? C.avg : S / (double)nblm;
+            const double iav = frz ? C.inv_avg : 1.0 / avg;
             double su = 0.0, v = 0.0, rm = 0.0, rlo = HUGE_VAL, rhi = -HUGE_VAL;
-            if (wid < NRW) {
+            if (frz && wid == 0) {
+                // the touched brokers' new r (lane k: s_T[k]); lane 0 folds the updates
+                // (all of them in bl_move: membership is unchanged)
+                if (lane < nT) {
+                    const int b = s_T[lane];
+                    stdbl(a.r + b, rel_ld(s_ld, b, iav));
+                }
+                if (lane == 0) {
+                    double dU = 0.0, aU = 0.0, dV = 0.0, dE = 0.0, rl = HUGE_VAL, rh = -HUGE_VAL;
+                    for (int k = 0; k < nT; k++) {
+                        const int b = s_T[k];
+                        const double rn = rel_ld(s_ld, b, iav);
+                        const double ro = __fma_rn(s_Lold[k], iav, -1.0);   // the r[] the base wrote
+                        const double fn = fsq(rn), fo = fsq(ro);
+                        dU += fn - fo;
+                        aU += fn + fo;
+                        dV += fabs(rn) * (1.0 + fabs(rn)) - fabs(ro) * (1.0 + fabs(ro));
+                        dE += s_e[b] - s_ebold[k];
+                        rl = rn < rl ? rn : rl;
+                        rh = rn > rh ? rn : rh;
+                    }
+                    s_fz[0] = dU; s_fz[1] = aU; s_fz[2] = dV; s_fz[3] = dE; s_fz[4] = rl; s_fz[5] = rh;
+                }
+            } else if (!frz && wid < NRW) {
 #pragma unroll 4
-                for (int b = wid * 64 + lane; b < B; b += NRW * 64) {
+                for (int b = wid * 64 + lane; b < ((KB_ABL & 4) ? 0 : B); b += NRW * 64) {
                     double r = 0.0;
                     if (s_fl[b] & (BF_PRESENT | BF_INCFG)) {
                         r = rel_ld(s_ld, b, iav);
@@ -2293,9 +2338,10 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
                 }
             }
             ub0 = wave_min(ub0); ub1 = wave_min(ub1);
-            if (wid < NRW) {
+            if (!frz && wid < NRW) {
                 su = wave_sum(su); v = wave_sum(v); rm = wave_max(rm);
                 rlo = wave_min(rlo); rhi = wave_max(rhi);
+                if (KB_ABL & 4) { su = wid ? 0.0 : C.U0; v = wid ? 0.0 : C.V; rm = 1.0; rlo = C.rlo; rhi = C.rhi; }   // (timing only)
             }
             if (lane == 0) {
                 s_fq2[3][wid] = ub0; s_fq2[4][wid] = ub1;
@@ -2356,14 +2402,29 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
             }
         }
         if (wid == 0) {
-            const double S = ((s_fq[0][0] + s_fq[0][1]) + s_fq[0][2]) + s_fq[0][3];
-            const double E = ((s_fq[1][0] + s_fq[1][1]) + s_fq[1][2]) + s_fq[1][3];
-            const int nblm = (s_fcnt[0] + s_fcnt[1]) + (s_fcnt[2] + s_fcnt[3]);
-            const double avg = S / (double)nblm;
-            const double iav = 1.0 / avg;
-            const double U0 = ((s_fq2[0][0] + s_fq2[0][1]) + s_fq2[0][2]) + s_fq2[0][3];
-            const double V = ((s_fq2[1][0] + s_fq2[1][1]) + s_fq2[1][2]) + s_fq2[1][3];
-            const double Rm = fmax(fmax(s_fq2[2][0], s_fq2[2][1]), fmax(s_fq2[2][2], s_fq2[2][3]));
+            const double uu = DBL_EPSILON / 2;
+            double S, E, avg, iav, U0, V, Rm, uerr;
+            int nblm;
+            if (frz) {
+                // (the base's sum and average; the increments of this step's touched brokers,
+                // each bound grown by a few ulps so it stays a bound)
+                S = C.S; nblm = C.nblm; avg = C.avg; iav = C.inv_avg;
+                U0 = C.U0 + s_fz[0];
+                uerr = C.uerr + 8.0 * uu * (fabs(C.U0) + fabs(U0) + s_fz[1]);
+                V = (C.V + s_fz[2]) * (1.0 + 8.0 * uu);
+                E = (C.E + s_fz[3]) * (1.0 + 8.0 * uu);
+                Rm = fmax(C.rm_bound, fmax(fabs(s_fz[4]), fabs(s_fz[5])));
+            } else {
+                S = ((s_fq[0][0] + s_fq[0][1]) + s_fq[0][2]) + s_fq[0][3];
+                E = ((s_fq[1][0] + s_fq[1][1]) + s_fq[1][2]) + s_fq[1][3];
+                nblm = (s_fcnt[0] + s_fcnt[1]) + (s_fcnt[2] + s_fcnt[3]);
+                avg = S / (double)nblm;
+                iav = 1.0 / avg;
+                U0 = ((s_fq2[0][0] + s_fq2[0][1]) + s_fq2[0][2]) + s_fq2[0][3];
+                V = ((s_fq2[1][0] + s_fq2[1][1]) + s_fq2[1][2]) + s_fq2[1][3];
+                Rm = fmax(fmax(s_fq2[2][0], s_fq2[2][1]), fmax(s_fq2[2][2], s_fq2[2][3]));
+                uerr = 0.0;
+            }
             const double ub0 = wave_min(lane < NW ? s_fq2[3][lane] : HUGE_VAL);
             const double ub1 = wave_min(lane < NW ? s_fq2[4][lane] : HUGE_VAL);
             // (every lane: the incremental certificate below needs eps on the whole wave)
@@ -2373,15 +2434,18 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
             const double Ea = E * iav;
             double epsf = 64.0 * u * ((n + 8.0) * (U0 + 2.0 * V) + 4.0 * (1.0 + R) * (1.0 + R));
             double epsl = 16.0 * Ea * (V / (n > 0 ? n : 1.0) + R + 1.0) + 4.0 * Ea * Ea;
-            double ep = epsf + epsl;
+            double ep = frz ? 2.0 * (epsf + epsl) + uerr : epsf + epsl;
             if (!(ep > 1e-300)) ep = 1e-300;
             // incremental mode: after a move() with bl_move and the first-index predicates
             // unchanged, the next scan may skip the blocks lighter than wskip
             double ws = 0.0;
             const bool inc = a.incr && do_res && D.status == 1 && D.kind == 1 && (D.step == 7 || D.step == 8) &&
                              nblm == nblm0 && !s_fm && !a.rebalance && !a.sem_go && a.use_spill;
-            const double rlo = fmin(fmin(s_fq2[5][0], s_fq2[5][1]), fmin(s_fq2[5][2], s_fq2[5][3]));
-            const double rhi = fmax(fmax(s_fq2[6][0], s_fq2[6][1]), fmax(s_fq2[6][2], s_fq2[6][3]));
+            // (the r range over every broker: frozen steps widen the base's range by the new r)
+            const double rlo = frz ? fmin(C.rlo, s_fz[4])
+                                   : fmin(fmin(s_fq2[5][0], s_fq2[5][1]), fmin(s_fq2[5][2], s_fq2[5][3]));
+            const double rhi = frz ? fmax(C.rhi, s_fz[5])
+                                   : fmax(fmax(s_fq2[6][0], s_fq2[6][1]), fmax(s_fq2[6][2], s_fq2[6][3]));
             if (inc) {
                 const double ubP = a.allow_leader ? (ub0 > ub1 ? ub0 : ub1) : ub1;
                 ws = incr_wskip(rlo, rhi, ubP + 16.0 * ep, avg, iav, lane);
@@ -2393,6 +2457,8 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
                 C.ub_sub = a.ubdesc && a.R.n <= STEP_THREADS && (s_nsub > 0 || a.ub_heavy) ? 1 : 0;
                 C.S = S; C.avg = avg; C.inv_avg = iav; C.U0 = U0;
                 C.V = V; C.eps = ep; C.E = E; C.nblm = nblm;
+                C.uerr = uerr; C.rm_bound = Rm;
+                C.frz_n = frz ? C.frz_n + 1 : 1;
                 // after a first-index stage (Remove/Add/Disallowed) the next step is most
                 // likely one too: no census (ub = -inf; k_step re-scans if move() is reached)
                 const bool sup = a.use_spill && do_res && D.status == 1 && D.step >= 3 && D.step <= 5;
@@ -2475,7 +2541,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
         for (;;) {
             constexpr int G = 4;
             const int W64 = a.W64, KR = a.KR;
-            const int mn = s_mn;
+            const int mn = (KB_ABL & 8) ? 0 : s_mn;
             constexpr int MAXU = sr_units(MAXR);
             __shared__ __align__(16) uint16_t s_rs2[NW][G][8 * MAXU];
             for (int g = wid * G; g < mn; g += NW * G) {
@@ -2976,7 +3042,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
             KB_STAMP(ctl, 20);
         }
     }
-    if (tid == 0) { C.prepped = 1; C.full_prep = 0; }
+    if (tid == 0) { C.prepped = 1; C.full_prep = 0; C.frz_n = 0; }   // (no frozen base)
     KB_STAMP(ctl, 10);
     write_back();
 }

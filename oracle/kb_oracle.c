@@ -373,13 +373,40 @@ static int add_missing(or_plist *pl, int sem, or_result *res) {   /* steps.go:93
     return rc;
 }
 
+static int g_window;                      /* see or_set_window (move_window) */
+
+/* The first partition holding a replica outside getBrokerListByLoadBL(loads, p.Brokers)
+ * (utils.go:81-90): a replica always has a load, so that is a replica outside p.Brokers.
+ * One hash set per distinct Brokers slice; O(P R) instead of the list intersections. */
+static int64_t first_disallowed(const or_plist *pl) {
+    const int64_t *key = NULL;
+    int has_key = 0;
+    lmap set; lm_init(&set, 64);
+    int64_t first = pl->n;
+    for (int64_t i = 0; i < pl->n && first == pl->n; i++) {
+        const or_partition *p = &pl->parts[i];
+        if (!has_key || p->brokers.a != key) {
+            lm_free(&set); lm_init(&set, p->brokers.len + 1);
+            for (int64_t q = 0; q < p->brokers.len; q++) lm_slot(&set, p->brokers.a[q]);
+            key = p->brokers.a; has_key = 1;
+        }
+        for (int64_t r = 0; r < p->replicas.len; r++)
+            if (lm_find(&set, p->replicas.a[r]) < 0) { first = i; break; }
+    }
+    lm_free(&set);
+    return first;
+}
+
 static int move_disallowed(or_plist *pl, int sem, or_result *res) { /* steps.go:117-143 */
     lmap m; get_broker_load(pl, &m);
     int64_t nbl; bload *bl = get_bl(&m, &nbl);
     int64_t *A = (int64_t *)malloc((size_t)(nbl ? nbl : 1) * sizeof(int64_t));
     int rc = 0;
     int64_t i_start = 0;
-    if (g_threads > 1 && pl->n > 1) {
+    if (g_window) {
+        /* (golden generation: the partitions before the first hit pass untouched) */
+        i_start = first_disallowed(pl);
+    } else if (g_threads > 1 && pl->n > 1) {
         /* the first partition holding a replica outside getBrokerListByLoadBL's list
          * (every earlier one passes untouched); the loop below starts there */
         int64_t first = pl->n;
@@ -511,6 +538,158 @@ static int move_chunk(const or_plist *pl, const or_config *cfg, int leaders, blo
     return 0;
 }
 
+/* ------------------------------------------------ windowed exact move()
+ * or_set_window(1) (golden generation only, tests/golden/gen_scale.py): the same result
+ * as move_chunk's literal loop at a fraction of its cost on thousands of brokers.  Every
+ * candidate is first scored in O(1): U~ = su + [f((L_r - w)/avg - 1) - f(r_r)] +
+ * [f((L_t + w)/avg - 1) - f(r_t)] with avg and r_i = L_i/avg - 1 of the unchanged bl.  The
+ * reference's U of a candidate (getUnbalanceBL over bl with two loads changed, two
+ * sequential folds, utils.go:119-147) differs from the real value of the same expression
+ * by at most ~2 n u (|U| + V), u = 2^-53, V = sum |r_i|(1 + |r_i|): recursive summation
+ * errs by at most (n - 1) u sum|t_i| (Higham 4.2), the load sum's error moves every
+ * r_i by at most (n - 1) u (1 + |r_i|), i.e. a term by ~2 |r_i| (1 + |r_i|) n u; moving w
+ * between two brokers leaves the real load sum unchanged, so U~ (the unchanged bl's fold
+ * plus two exact-to-rounding term deltas) is within eps = 16 n u (|su| + V + 1) of the
+ * reference's U -- a window eight times the bound.  Any candidate with U~ > min U~ + 2 eps then has a
+ * larger U than the U~-minimum, so the reference's first strict minimum (steps.go:211,
+ * the lexicographic minimum of (U, iteration order) below su) lies among the candidates
+ * within 2 eps of min U~: those, and only those, are folded exactly like move_chunk does,
+ * in iteration order.  tests/test_oracle.py checks it against the literal loop. */
+static int g_window = 0;
+void or_set_window(int on) { g_window = on ? 1 : 0; }
+
+typedef struct { double ua; int64_t i, s, k, ridx; } wcand;
+typedef struct { wcand *v; int64_t n, cap; double best; } wlist;
+
+static void wl_push(wlist *L, wcand c) {
+    if (L->n == L->cap) { L->cap = L->cap ? 2 * L->cap : 1024; L->v = (wcand *)realloc(L->v, (size_t)L->cap * sizeof(wcand)); }
+    L->v[L->n++] = c;
+}
+static double f_unb(double r) { return r > 0 ? r * r : r * r / 2; }
+
+static int move_window(const or_plist *pl, const or_config *cfg, int leaders, bload *bl, int64_t n, double su,
+                       int64_t np, double *cu, int64_t *cp, int64_t *cr, int64_t *cb, int64_t *cnt_out) {
+    double sum = 0;
+    for (int64_t k = 0; k < n; k++) sum += bl[k].load;
+    const double avg = sum / (double)n;
+    double *fr = (double *)malloc((size_t)(n ? n : 1) * sizeof(double));
+    double V = 0;
+    for (int64_t k = 0; k < n; k++) {
+        const double r = bl[k].load / avg - 1.0;
+        fr[k] = f_unb(r);
+        V += fabs(r) * (1.0 + fabs(r));
+    }
+    const double eps = 16.0 * (double)(n + 1) * 0x1p-53 * (V + fabs(su) + 1.0);
+    /* bl position of every broker id, and one bitmap over bl positions per distinct
+       Brokers slice (partitions share the slice FillDefaults gave them) */
+    lmap pos; lm_init(&pos, n);
+    for (int64_t k = 0; k < n; k++) { int32_t q = lm_slot(&pos, bl[k].id); pos.loads[q] = (double)k; }
+    const int64_t W = (n + 63) / 64;
+    int32_t *sidx = (int32_t *)malloc((size_t)(np ? np : 1) * sizeof(int32_t));
+    uint64_t *bits = NULL;
+    const int64_t **skey = NULL;
+    int64_t nset = 0, setcap = 0, last = -1;
+    for (int64_t i = 0; i < np; i++) {
+        const int64_t *key = pl->parts[i].brokers.a;
+        int64_t j = last >= 0 && skey[last] == key ? last : -1;
+        for (int64_t q = 0; j < 0 && q < nset; q++) if (skey[q] == key) j = q;
+        if (j < 0) {
+            if (nset == setcap) {
+                setcap = setcap ? 2 * setcap : 16;
+                skey = (const int64_t **)realloc((void *)skey, (size_t)setcap * sizeof(int64_t *));
+                bits = (uint64_t *)realloc(bits, (size_t)(setcap * (W ? W : 1)) * sizeof(uint64_t));
+            }
+            j = nset++;
+            skey[j] = key;
+            uint64_t *b = bits + j * W;
+            memset(b, 0, (size_t)(W ? W : 1) * sizeof(uint64_t));
+            const or_partition *p = &pl->parts[i];
+            for (int64_t q = 0; q < p->brokers.len; q++) {
+                const int32_t m = lm_find(&pos, p->brokers.a[q]);
+                if (m >= 0) { const int64_t k = (int64_t)pos.loads[m]; b[k >> 6] |= 1ull << (k & 63); }
+            }
+        }
+        sidx[i] = (int32_t)j;
+        last = j;
+    }
+    int T = g_threads < 1 ? 1 : g_threads;
+    if (T > np) T = np > 0 ? (int)np : 1;
+    wlist *TL = (wlist *)calloc((size_t)T, sizeof(wlist));
+    int64_t *tcnt = (int64_t *)calloc((size_t)T, sizeof(int64_t));
+    int *terr = (int *)calloc((size_t)T, sizeof(int));
+#pragma omp parallel for num_threads(T) schedule(static, 1)
+    for (int t = 0; t < T; t++) {
+        wlist *L = &TL[t];
+        L->best = HUGE_VAL;
+        const int64_t i0 = np * t / T, i1 = np * (t + 1) / T;
+        int64_t rk[64];
+        for (int64_t i = i0; i < i1 && !terr[t]; i++) {
+            const or_partition *p = &pl->parts[i];
+            if (p->num_replicas < cfg->min_replicas) continue;
+            int64_t lo = 1, hi = p->replicas.len;
+            if (leaders) { lo = 0; hi = 1; }
+            if (p->replicas.len < lo || p->replicas.len < hi) { terr[t] = 1; break; }
+            const int64_t nr = p->replicas.len < 64 ? p->replicas.len : 64;
+            for (int64_t q = 0; q < nr; q++) {
+                const int32_t m = lm_find(&pos, p->replicas.a[q]);
+                rk[q] = m >= 0 ? (int64_t)pos.loads[m] : -1;
+            }
+            const uint64_t *b = bits + (int64_t)sidx[i] * W;
+            const double w = p->weight;
+            for (int64_t s = lo; s < hi; s++) {
+                const int64_t ridx = s < 64 ? rk[s] : -1;
+                if (ridx < 0) { terr[t] = 2; break; }
+                const double ds = f_unb((bl[ridx].load - w) / avg - 1.0) - fr[ridx];
+                for (int64_t k = 0; k < n; k++) {
+                    if (!((b[k >> 6] >> (k & 63)) & 1ull)) continue;
+                    int isrep = 0;
+                    for (int64_t q = 0; q < nr; q++) isrep |= rk[q] == k;
+                    if (isrep) continue;
+                    const double ua = su + ds + (f_unb((bl[k].load + w) / avg - 1.0) - fr[k]);
+                    tcnt[t]++;
+                    if (ua <= L->best + 2 * eps) {
+                        wcand c = {ua, i, s, k, ridx};
+                        wl_push(L, c);
+                        if (ua < L->best) L->best = ua;
+                    }
+                }
+            }
+        }
+    }
+    int err = 0;
+    double best = HUGE_VAL;
+    for (int t = 0; t < T && !err; t++) {
+        *cnt_out += tcnt[t];
+        if (terr[t]) { err = terr[t]; break; }          /* the first panic in order */
+        if (TL[t].best < best) best = TL[t].best;
+    }
+    if (!err) {
+        bload *b2 = (bload *)malloc((size_t)(n ? n : 1) * sizeof(bload));
+        if (n) memcpy(b2, bl, (size_t)n * sizeof(bload));
+        for (int t = 0; t < T; t++)
+            for (int64_t c = 0; c < TL[t].n; c++) {
+                const wcand x = TL[t].v[c];
+                if (!(x.ua <= best + 2 * eps)) continue;
+                const or_partition *p = &pl->parts[x.i];
+                const double rl = b2[x.ridx].load, tl = b2[x.k].load;
+                b2[x.ridx].load -= p->weight;                 /* as move_chunk does, in order */
+                b2[x.k].load += p->weight;
+                const double u = unbalance_bl(b2, n);
+                b2[x.ridx].load = rl; b2[x.k].load = tl;
+                if (u < *cu) { *cu = u; *cp = x.i; *cr = p->replicas.a[x.s]; *cb = b2[x.k].id; }
+            }
+        free(b2);
+    }
+    if (getenv("KB_ORACLE_WINDOW_DEBUG")) {
+        int64_t tot = 0, in = 0;
+        for (int t = 0; t < T; t++) { tot += TL[t].n; for (int64_t c = 0; c < TL[t].n; c++) in += TL[t].v[c].ua <= best + 2 * eps; }
+        fprintf(stderr, "window: eps %.3g best %.17g listed %lld folded %lld\n", eps, best, (long long)tot, (long long)in);
+    }
+    for (int t = 0; t < T; t++) free(TL[t].v);
+    free(TL); free(tcnt); free(terr); free(fr); free(bits); free((void *)skey); free(sidx); lm_free(&pos);
+    return err;
+}
+
 /* move (steps.go:145-232).  limit < 0 => all partitions. */
 static int move_impl(or_plist *pl, const or_config *cfg, int leaders, int sem, or_result *res,
                      int64_t limit, int64_t *ncand, double *cu_out) {
@@ -521,7 +700,9 @@ static int move_impl(or_plist *pl, const or_config *cfg, int leaders, int sem, o
     int err = 0;
     int T = g_threads;
     if (T > np) T = np > 0 ? (int)np : 1;
-    if (T <= 1) {
+    if (g_window && limit < 0 && n > 0) {
+        err = move_window(pl, cfg, leaders, bl, n, su, np, &cu, &cp, &cr, &cb, &cnt);
+    } else if (T <= 1) {
         int64_t ep = -1;
         err = move_chunk(pl, cfg, leaders, bl, n, 0, np, &cu, &cp, &cr, &cb, &cnt, &ep);
     } else {

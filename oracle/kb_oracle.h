@@ -98,6 +98,12 @@ void or_free(void *p);
  * count gives the identical result (chunked in order, merged in order). */
 void or_set_threads(int n);
 
+/* Golden generation only: move() scores every candidate in O(1) first and folds exactly
+ * (the reference's getUnbalanceBL) only those within a window that provably holds the
+ * reference's choice -- the same result as the literal loop (kb_oracle.c: move_window;
+ * tests/test_oracle.py checks it).  Default off. */
+void or_set_window(int on);
+
 /* Build a partition list from flat arrays.  Brokers lists are deduplicated
  * into sets; partitions with the same set_idx share one slice (as FillDefaults
  * makes them share in Go).  set_idx < 0 => nil Brokers. rep_nil may be NULL. */

@@ -84,6 +84,8 @@ def lib():
         L.or_free.argtypes = [C.c_void_p]
         L.or_set_threads.argtypes = [C.c_int]
         L.or_set_threads.restype = None
+        L.or_set_window.argtypes = [C.c_int]
+        L.or_set_window.restype = None
         _lib = L
     return _lib
 
@@ -272,6 +274,12 @@ def move_sample(opl, cfg, leaders, max_parts):
 def set_threads(n):
     """Worker threads of the oracle's move() (identical results for any n)."""
     lib().or_set_threads(int(n))
+
+
+def set_window(on):
+    """Golden generation only: move()'s windowed exact search (same results as the literal
+    loop, kb_oracle.c move_window)."""
+    lib().or_set_window(int(bool(on)))
 
 
 def format_float(x):

@@ -73,7 +73,20 @@ CASES = {
     # partitions, c3-shaped sets
     "rl20k": (dict(P=20000, B=1000, rf=3, weights="zipf", nsets=256, set_size=64, seed=0x5EED3003),
               dict(O.default_cfg(), allow_leader=True, rebalance_leaders=True, min_unbalance=0.0), 200),
+    # BASELINE.json configs[2]'s cluster without -allow-leader: MoveNonLeaders at 1M x 1000
+    # with 256 allowed sets of 64 (the headline config's leader 2-cycle never reaches it)
+    "c3nl_full": (dict(config="c3", scale=1.0), dict(O.default_cfg(), min_unbalance=0.0), 20),
+    # c5's broker width (4096, auto lists, Zipf) at 50k partitions
+    "b4096_50k": (dict(P=50000, B=4096, rf=3, weights="zipf", seed=0x5EED3005),
+                  dict(O.default_cfg(), min_unbalance=0.0), 40),
+    # BASELINE.json configs[4] at full size: 10M partitions x 4096 brokers, the first steps
+    "c5_full": (dict(config="c5", scale=1.0), None, 12),
 }
+
+# cases generated with the oracle's windowed exact move() (or_set_window: the literal
+# loop's result, tests/test_oracle.py::test_windowed_oracle_*; the literal loop would take
+# hours to days per step at these sizes)
+WINDOWED = {"c3nl_full", "b4096_50k", "c5_full"}
 
 
 def build(params):
@@ -121,6 +134,7 @@ def generate(name, threads):
     cfg = case_cfg(name)
     cl = build(params)
     O.set_threads(threads)
+    O.set_window(name in WINDOWED)
     o = oracle_pl(cl)
     changes, su, cu, err = [], [], [], None
     t0 = time.time()
@@ -138,7 +152,8 @@ def generate(name, threads):
             print(name, k, r["step"], "%.0fs" % (time.time() - t0), flush=True)
     # final replicas of every partition some change touched
     touched = sorted({c[1] for c in changes})
-    doc = {"name": name, "generator": "tests/golden/gen_scale.py (oracle/kb_oracle.c, %d threads)" % threads,
+    doc = {"name": name, "generator": "tests/golden/gen_scale.py (oracle/kb_oracle.c, %d threads%s)"
+                                      % (threads, ", windowed exact move()" if name in WINDOWED else ""),
            "params": params, "cfg": cfg, "steps": steps, "input_sha256": input_hash(cl),
            "changes": changes, "su": su, "cu": cu, "err": err,
            "final": {str(i): o.replicas(i) for i in touched}}

@@ -9,6 +9,7 @@
 """
 import copy
 import json
+import os
 import random
 import struct
 
@@ -17,7 +18,7 @@ import pytest
 from oracle import oracle as O
 from oracle import pyref
 
-from helpers import default_cfg, golden
+from helpers import GOLDEN, default_cfg, golden
 from test_gpu_parity_data import random_plist
 
 
@@ -240,3 +241,65 @@ def test_json_writer_matches_go_layout():
             '{"topic":"x","partition":0,"replicas":[1,2]}]}\n').encode()
     assert out == want
     json.loads(out)
+
+
+@pytest.mark.parametrize("seed", range(16))
+def test_windowed_oracle_matches_literal(seed):
+    """or_set_window(1) (golden generation: O(1) scores, exact folds only inside the window
+    that holds the reference's choice) -- the identical plan, su / cu bits and errors as the
+    literal move() loop, uniform exact-tie weights included."""
+    rng = random.Random(900 + seed)
+    pl = random_plist(rng, rng.choice([40, 90, 200]), rng.choice([3, 6, 12, 30]),
+                      rng.choice(["uniform", "int", "zipf"]), rng.choice(["none", "some", "all"]),
+                      rng.random() < 0.4, rng.random() < 0.3)
+    cfg = default_cfg(allow_leader=rng.random() < 0.5, rebalance_leaders=rng.random() < 0.2,
+                      min_replicas=rng.choice([1, 2, 3]), min_unbalance=rng.choice([0.0, 0.01]))
+    if rng.random() < 0.3:
+        cfg["brokers"] = list(range(1, 40))
+
+    def run(window, threads):
+        O.set_threads(threads)
+        O.set_window(window)
+        try:
+            o = O.OraclePL(pl)
+            out = []
+            for _ in range(25):
+                r = O.balance(o, cfg, O.SEM_APPLIED)
+                out.append((r["status"], r["step"], r.get("pidx"), r.get("from_"), r.get("to"),
+                            r.get("su"), r.get("cu"), r["err"]))
+                if r["status"] != 1:
+                    break
+            return out, o.state()
+        finally:
+            O.set_threads(1)
+            O.set_window(0)
+
+    assert run(0, 1) == run(1, 3)
+
+
+@pytest.mark.parametrize("name", ["b4096_zipf", "c3s_nonleader", "c3s_leader"])
+def test_windowed_oracle_reproduces_scale_goldens(name):
+    """The windowed search regenerates the committed large goldens the literal loop made
+    (4096 brokers; 20k partitions x 1000 brokers with 256 allowed sets, leader and
+    non-leader moves): every change and every su / cu bit."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("gen_scale", os.path.join(GOLDEN, "gen_scale.py"))
+    gs = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(gs)
+    g = golden("scale_%s.json" % name)
+    params, _, steps = gs.CASES[name]
+    cl = gs.build(params)
+    assert gs.input_hash(cl) == g["input_sha256"]
+    cfg = gs.case_cfg(name)
+    O.set_threads(min(8, os.cpu_count() or 1))
+    O.set_window(1)
+    try:
+        o = gs.oracle_pl(cl)
+        for k, want in enumerate(g["changes"][:60]):
+            r = O.balance(o, cfg, O.SEM_APPLIED)
+            assert r["status"] == 1, (k, r["err"])
+            assert [r["step"], r["pidx"], r["kind"], r["from_"], r["to"], r["slot"]] == want, k
+            assert r["su"] == g["su"][k] and r["cu"] == g["cu"][k], k
+    finally:
+        O.set_threads(1)
+        O.set_window(0)

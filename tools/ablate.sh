@@ -9,5 +9,5 @@ for v in "" $@; do
   python3 -c "
 import json
 d=[json.loads(l) for l in open('$O/abl$v.out') if l.startswith('{')][0]
-print('abl=$v', round(d['ms_per_step']*1e3,2), {k: round(x,2) for k,x in d['kernels_us_per_step'].items()}, d['engine_events'])"
+print('abl=$v', round(d['ms_per_step']*1e3,2), {k: round(x,2) for k,x in d['kernels_us_per_launch'].items()}, d['engine_events'])"
 done
