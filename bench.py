@@ -226,13 +226,28 @@ def drop_in(args):
         if eng.balance() is None:
             break
     per_call = (time.perf_counter() - t0) / n
+    # the reference's steps table walked on the host, one kb_engine_step per entry
+    # (INTEGRATION.md's per-step cgo binding; ValidateWeights / ValidateReplicas /
+    # FillDefaults stay Go code there and are not called here)
+    walk_calls = 0
+    t0 = time.perf_counter()
+    for _ in range(n):
+        for k in range(3, 9):
+            walk_calls += 1
+            if eng.step(1 << k) is not None:
+                break
+    per_walk = (time.perf_counter() - t0) / n
     t0 = time.perf_counter()
     buf, k, rc = eng.plan_raw(n)
     plan_step = (time.perf_counter() - t0) / max(k, 1)
     eng.close()
     out = {"metric": "drop-in cost (%s)" % args.workload, "unit": "us",
-           "balance_per_call_us": 1e6 * per_call, "plan_per_step_us": 1e6 * plan_step, "calls": n,
-           "balance_def": "kb_engine_balance via ctypes, one Balance() per call (enqueue + sync), after 5 warm calls"}
+           "balance_per_call_us": 1e6 * per_call, "steps_table_per_balance_us": 1e6 * per_walk,
+           "steps_table_calls_per_balance": walk_calls / n,
+           "plan_per_step_us": 1e6 * plan_step, "calls": n,
+           "balance_def": "kb_engine_balance via ctypes, one Balance() per call (enqueue + sync), after 5 warm calls",
+           "steps_table_def": "one Balance() as the reference's steps table walked on the host: kb_engine_step "
+                              "per GPU step (RemoveExtraReplicas .. MoveNonLeaders) until one changes something"}
     # the CLI on the same cluster as reassignment JSON
     cli_bin = os.path.join(ROOT, "kafkabalancer_amd", "lib", "kafkabalancer")
     tmp = tempfile.mkdtemp(prefix="kbdrop")

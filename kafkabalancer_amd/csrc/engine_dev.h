@@ -139,9 +139,10 @@ inline Recs summary_recs(unsigned char* base, int n, int keys) {
 }
 
 // dynamic LDS of k_step (byte offsets): loads [B], error bounds / sort keys [NP2],
-// universe order [NP2], allowed-set words of every set when resident [sbw], flags [B]
-struct StepLds { int e, ord, sb, fl, total; };
-__host__ __device__ inline StepLds step_lds(int B, int NP2, int sbw) {
+// universe order [NP2], allowed-set words of every set when resident [sbw], flags [B],
+// the records' best keys when staged [2 nbk] (Contender)
+struct StepLds { int e, ord, sb, fl, bk, total; };
+__host__ __device__ inline StepLds step_lds(int B, int NP2, int sbw, int nbk = 0) {
     auto al = [](int x) { return (x + 15) & ~15; };
     StepLds L;
     int o = al(B * 8);
@@ -149,6 +150,7 @@ __host__ __device__ inline StepLds step_lds(int B, int NP2, int sbw) {
     L.ord = o; o += al(NP2 * 4);
     L.sb = o;  o += al(sbw * 8);
     L.fl = o;  o += al(B);
+    L.bk = o;  o += 2 * nbk * 32;
     L.total = o;
     return L;
 }

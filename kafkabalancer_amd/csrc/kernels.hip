@@ -1196,13 +1196,14 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
     __shared__ uint32_t s_key[DEDUP_STEP];
     __shared__ unsigned long long s_wb[DEDUP_STEP], s_it[DEDUP_STEP];
     extern __shared__ __align__(16) unsigned char dsm[];
-    const StepLds LY = step_lds(a.B, a.NP2, a.sb_lds ? a.nsets * a.W64 : 0);
+    const StepLds LY = step_lds(a.B, a.NP2, a.sb_lds ? a.nsets * a.W64 : 0, a.bk_lds);
     double* s_ld = (double*)dsm;                     // loads by broker id
     double* s_e = (double*)(dsm + LY.e);             // load error bounds; zero whenever every load is
                                                      // exact, so then also sort keys / exact bl loads
     int32_t* s_ord = (int32_t*)(dsm + LY.ord);       // universe order by (load, id)
     uint64_t* s_sb = (uint64_t*)(dsm + LY.sb);       // allowed-set words (sb_lds)
     uint8_t* s_fl = dsm + LY.fl;                     // BF_* flags
+    Contender* s_bk = (Contender*)(dsm + LY.bk);     // records' best keys [2 R.n] (a.bk_lds)
     __shared__ int s_T[TMAX], s_posT[TMAX];
     __shared__ double s_Lold[TMAX], s_ebold[TMAX];  // touched brokers' load / bound before the apply
     __shared__ int s_memb;                          // the apply changed bl_move's membership
@@ -1219,6 +1220,24 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
     // bytes, 16.5 vs 19.9 us per k_step at c3).  The record headers come to registers.
     const unsigned long long ts_b = ctl->ts_beg, ts_e = ctl->ts_end;   // (kernel timing, tk_on)
     const unsigned long long ts_pe = ctl->ts_prev_end;
+    // (the record headers and, when staged, the best keys first: their loads share the
+    // tables' round trip -- the LDS writes below wait on the in-order vmcnt anyway)
+    double hd0 = HUGE_VAL, hd1 = HUGE_VAL;
+    unsigned long long hc0 = 0, hc1 = 0;
+    uint32_t hflg = 0, hfm = 0, hnk0 = 0, hnk1 = 0;
+    if (tid < a.R.n) {
+        const RecHdr* h = a.R.h(tid);
+        hd0 = ldd(&h->dmin[0]); hd1 = ldd(&h->dmin[1]);
+        hc0 = ldobj(&h->cand[0]); hc1 = ldobj(&h->cand[1]);
+        hflg = ld32(&h->flags) & 1u; hfm = ld32(&h->fmask);
+        const uint32_t nkk = ld32(&h->nkk[0]);
+        hnk0 = nkk & 0xFFFFu; hnk1 = nkk >> 16;
+    }
+    if (a.bk_lds)
+        for (int i = tid; i < a.R.n; i += STEP_THREADS) {
+            const Contender k0 = ldobj(&a.R.h(i)->best[0]), k1 = ldobj(&a.R.h(i)->best[1]);
+            s_bk[2 * i] = k0; s_bk[2 * i + 1] = k1;
+        }
     if (tid < CTL_WORDS) ((uint32_t*)&C)[tid] = ((const uint32_t*)ctl)[tid];
     for (int b = tid; b < B; b += STEP_THREADS) {
         s_ld[b] = a.load[b];
@@ -1235,17 +1254,6 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
     }
     KB_STAMP(ctl, 23);
     KB_STAMP(ctl, 27);
-    double hd0 = HUGE_VAL, hd1 = HUGE_VAL;
-    unsigned long long hc0 = 0, hc1 = 0;
-    uint32_t hflg = 0, hfm = 0, hnk0 = 0, hnk1 = 0;
-    if (tid < a.R.n) {
-        const RecHdr* h = a.R.h(tid);
-        hd0 = ldd(&h->dmin[0]); hd1 = ldd(&h->dmin[1]);
-        hc0 = ldobj(&h->cand[0]); hc1 = ldobj(&h->cand[1]);
-        hflg = ld32(&h->flags) & 1u; hfm = ld32(&h->fmask);
-        const uint32_t nkk = ld32(&h->nkk[0]);
-        hnk0 = nkk & 0xFFFFu; hnk1 = nkk >> 16;
-    }
     KB_STAMP(ctl, 28);
     dedup_clear(T);
     if (tid < 2) { s_nd[tid] = 0; s_li[tid] = -1; s_kfail[tid] = 0; }
@@ -1301,7 +1309,10 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
     // round trip so they are not held in registers through it
     Contender hb0, hb1;
     hb0.s = hb1.s = -1;
-    if (do_res && tid < a.R.n) { hb0 = ldobj(&a.R.h(tid)->best[0]); hb1 = ldobj(&a.R.h(tid)->best[1]); }
+    if (do_res && tid < a.R.n) {
+        if (a.bk_lds) { hb0 = s_bk[2 * tid]; hb1 = s_bk[2 * tid + 1]; }
+        else { hb0 = ldobj(&a.R.h(tid)->best[0]); hb1 = ldobj(&a.R.h(tid)->best[1]); }
+    }
     KB_STAMP(ctl, 12);
     KB_STOP(1);
     // ---- the scan records (or the gathered rank summaries): one per thread, reduced
@@ -2178,7 +2189,10 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
         // next to a fresh fold's) plus uerr, the rounding of the incremental U0 updates.  A
         // full recompute every FRZ_MAX steps, after a membership change and after a full prep.
         constexpr int FRZ_MAX = 1024;
-        const bool frz = do_res && D.status == 1 && !s_memb && C.frz_n > 0 && C.frz_n < FRZ_MAX && !(KB_ABL & 32);
+        // (replace / swap keep the real load sum: the weight changes brokers; a remove or an
+        // add changes it, and then the sums are folded again)
+        const bool frz = do_res && D.status == 1 && (D.kind == 1 || D.kind == 4) && !s_memb && C.frz_n > 0 &&
+                         C.frz_n < FRZ_MAX && !(KB_ABL & 32);
         __shared__ double s_fz[6];                      // frozen step: dU, |updates|, dV, dE, r lo / hi
         __shared__ double s_fq[2][NRW], s_fq2[7][NW];
         __shared__ int s_fcnt[NRW];
@@ -2216,7 +2230,12 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
         const bool bkeys = do_res && tid < a.R.n;
         Contender bk0, bk1;
         bk0.s = bk1.s = -1;
-        if (bkeys) { bk0 = ldobj(&a.R.h(tid)->best[0]); bk1 = ldobj(&a.R.h(tid)->best[1]); }
+#if KB_ABL & 64
+        if (bkeys) { bk0 = hb0; bk1 = hb1; }            // (variant: the resolve's registers)
+#else
+        if (bkeys && a.bk_lds) { bk0 = s_bk[2 * tid]; bk1 = s_bk[2 * tid + 1]; }
+        else if (bkeys) { bk0 = ldobj(&a.R.h(tid)->best[0]); bk1 = ldobj(&a.R.h(tid)->best[1]); }
+#endif
         if (tid < nT) { s_fl[s_T[tid]] |= BF_TOUCHED; s_cntT[tid] = 0; }
         if (tid == 0) { s_unc = 0; s_nsub = 0; }
         if (wid < NRW) {

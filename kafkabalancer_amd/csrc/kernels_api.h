@@ -72,7 +72,8 @@ struct StepArgs {
     long long Ppad;
     int RC, KR, K, units, W64, B, nsets, NP2;
     int sb_lds;               // 1: every set's allowed-set words are staged in LDS
-    int lds_bytes;            // dynamic LDS (step_lds(B, NP2, sb_lds ? nsets * W64 : 0).total)
+    int lds_bytes;            // dynamic LDS (step_lds(B, NP2, sb_lds ? nsets * W64 : 0, bk_lds).total)
+    int bk_lds;               // > 0: the records' best keys are staged in LDS (room for bk_lds records)
     const uint64_t* setbits;
     uint4* setrec;
     int32_t* order;           // [B] universe sorted by (load, id)
