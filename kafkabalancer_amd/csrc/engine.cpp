@@ -118,6 +118,7 @@ struct kb_engine {
     int64_t klaunch[TK_N] = {0, 0, 0, 0};
     int64_t refreshes = 0;
     bool rf_stream = false;        // in-stream refreshes (ScanArgs.rfpass / StepArgs.rf_final)
+    bool eager = false;            // eager refolds of the touched brokers (ScanArgs.eager)
     RefreshArgs* rf_dev = nullptr; // the refresh's arguments in device memory (ScanArgs.rf)
     int dbg_scan = 0;
     int incr = 0;                  // incremental mode (kb_engine_set_incremental)
@@ -519,7 +520,12 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
         if (const char* v = getenv("KB_TWAVES")) if (atoi(v) > 0) e->twaves = std::min(atoi(v), SCAN_THREADS / 64);  // diagnostic
         e->ntiles = (nblk + e->twaves - 1) / e->twaves;
     }
-    e->nscan = std::min<int64_t>(e->ntiles, (int64_t)per_cu * ncu);
+    // eager refolds (thousands of brokers, non-integral loads: the decisions there need exact
+    // folds often, and each then waited for a refresh of the approximate loads): EGW extra
+    // workgroups per scan launch, kept co-resident with the scan's (and its list workgroup)
+    e->eager = e->rf_stream && e->B >= 2048;
+    if (const char* v = getenv("KB_EAGER")) e->eager = e->rf_stream && *v == '1';          // diagnostic
+    e->nscan = std::min<int64_t>(e->ntiles, std::max<int64_t>(1, (int64_t)per_cu * ncu - (e->eager ? EGW + 1 : 0)));
     if (const char* v = getenv("KB_NSCAN")) if (atoi(v) > 0) e->nscan = std::min<int64_t>(e->ntiles, atoi(v));  // diagnostic
     if (const char* v = getenv("KB_DEBUG_SCAN")) e->dbg_scan = atoi(v);                                   // diagnostic
     {
@@ -676,6 +682,7 @@ static void fill_scan_args(kb_engine* e, ScanArgs& s) {
     s.pset = e->pset;
     s.rfpass = 0;
     s.rf = e->rf_dev;
+    s.eager = e->eager && e->nscan > 0 ? EGW : 0;
 }
 
 static void fill_step_args(kb_engine* e, StepArgs& a, const Recs& R, int use_spill) {
@@ -699,6 +706,7 @@ static void fill_step_args(kb_engine* e, StepArgs& a, const Recs& R, int use_spi
     a.ub_heavy = e->nubdesc > 2 * std::max<int64_t>(e->nscan, STEP_THREADS) ? 1 : 0;
     a.pset = e->pset;
     a.rf_final = 0;
+    a.eager = e->eager && e->nscan > 0 ? 1 : 0;
 }
 
 static const int kStepBatch = 64;
@@ -754,6 +762,7 @@ static void enqueue_ubinit(kb_engine* e, bool rf = false) {
     fill_scan_args(e, s);
     s.rfpass = rf && e->rf_stream;
     s.listwg = 0;
+    s.eager = 0;                      // (the main scan launch refolds)
     s.dbg |= 1;
     s.ubpass = 1;
     // (set records in LDS: the block-list kernel, which scans only the blocks of the last
@@ -859,6 +868,7 @@ static int refresh(kb_engine* e) {
     DevCtl c = *e->h_ctl;
     if (c.halted == H_NEED_EXACT) c.halted = H_RUN;
     c.prepped = 0; c.full_prep = 1; c.ndirty = 0; c.want_refresh = 0;
+    c.eg_n = 0;
     HIPCHK(hipMemcpyAsync(e->ctl, &c, sizeof c, hipMemcpyHostToDevice, e->st));
     HIPCHK(hipStreamSynchronize(e->st));
     e->refreshes++;

@@ -32,6 +32,7 @@ constexpr int SUMMARY_KEYS_MAX = 2048;
 constexpr int DEDUP_STEP = 2048;    // LDS key table of k_step / k_summary
 constexpr int DEDUP_SCAN = 256;     // LDS key table of one k_scan workgroup
 constexpr int TMAX = 2 * MAXR + 4;  // brokers touched by one applied change (bound)
+constexpr int EGW = 4;              // eager refold workgroups per scan launch (touched brokers)
 constexpr int RF_CHUNK = 2048;       // in-stream refresh: contributions per fold chunk (two buffers)
 constexpr int RF_LDS_BYTES = 2 * RF_CHUNK * 8;
 constexpr int BLK = 128;            // partitions of one wave in a scan tile = one block of
@@ -224,6 +225,11 @@ struct DevCtl {
     // rounding those updates added to U0, frz_n counts the steps since the base (0: none)
     double uerr, rm_bound;          // rm_bound: max |r| over bl_move (an upper bound when frozen)
     int32_t frz_n, frz_pad;
+    // eager refolds (ScanArgs.eager): the brokers whose contribution the last applied step
+    // changed, refolded exactly by extra workgroups of the next scan launch (their list edit
+    // done by k_step), so the next resolve finds every load exact
+    int32_t eg_n, eg_pad;
+    int32_t eg_b[8];
     // diagnostic phase stamps (builds with -DKB_STAMPS): accumulated
     // shader-clock ticks (clock64) per phase of k_step; [24]/[25] the wall-clock
     // (100 MHz) and shader-clock length of k_step; [26] one stamp's own cost

@@ -959,12 +959,19 @@ __device__ __forceinline__ void scan_round(const ScanArgs& a, const ScanParams& 
 
 __device__ __attribute__((noinline)) void refresh_in_scan(const RefreshArgs* rfp, int pend, int kind, int from, int to,
                                                           uint32_t part, double* buf);   // (k_refresh below)
+__device__ __attribute__((noinline)) void eager_refold(const RefreshArgs* rfp, int k, double* buf);
 
 template <int RC, bool LSETS, bool INCR>
 __global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
     extern __shared__ __align__(16) unsigned char smem[];
     __shared__ int s_li;
     DevCtl* ctl = a.ctl;
+    // eager refolds: the last workgroups of the grid refold the brokers the last step touched
+    // (their lists already edited by k_step), concurrently with the scan
+    if (a.eager && (int)blockIdx.x >= a.nscan + (a.listwg ? 1 : 0)) {
+        eager_refold(a.rf, (int)blockIdx.x - a.nscan - (a.listwg ? 1 : 0), (double*)smem);
+        return;
+    }
     // (rfpass: if the last k_step halted for exact loads, this launch is the refresh,
     // refresh_in_scan; the scanning workgroups decide with their control words below)
     auto rf_run = [&]() {
@@ -1290,6 +1297,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
     }
     const int halted = C.halted;
     const bool do_res = C.prepped && C.steps < C.budget;
+    if (tid == 0) C.eg_n = 0;                    // (the last launch ran this list's refolds)
     // the steps this Balance() may take (kb_engine_step's mask; SM_ALL = the whole table)
     const uint32_t sm = C.step_mask;
     const bool lead_on = a.allow_leader && (sm & SM_MOVE_LEADERS), non_on = (sm & SM_MOVE_NON_LEADERS) != 0;
@@ -2156,6 +2164,31 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
         }
         __syncthreads();
         if (D.status != 1) { write_back(); return; }
+        // eager refolds: edit the per-broker lists now (the next scan's extra workgroups refold
+        // the touched brokers from them); more touched brokers than EGW: the old way (pending
+        // edit in the scan's list workgroup, the brokers stay dirty until a refresh)
+        if (a.eager && !a.integral && s_nT <= EGW) {
+            __shared__ int s_eok;
+            if (C.pending_list) {
+                const int kind = C.pl_kind, from = C.pl_from, to = C.pl_to;
+                const uint32_t p = (uint32_t)C.pl_part;
+                bool ok = true;
+                if (kind == 1) { list_remove(a.L, from, p, &s_i); ok = list_insert(a.L, to, p, &s_i); }
+                else if (kind == 2) list_remove(a.L, from, p, &s_i);
+                else if (kind == 3) ok = list_insert(a.L, to, p, &s_i);
+                if (tid == 0) s_eok = ok ? 1 : 0;
+            } else if (tid == 0) s_eok = 1;
+            __syncthreads();
+            if (tid == 0) {
+                C.pending_list = 0;
+                if (!s_eok) { C.list_overflow = 1; C.eg_n = 0; }      // (the host relists, refresh)
+                else {
+                    C.eg_n = s_nT;
+                    for (int k = 0; k < s_nT; k++) C.eg_b[k] = s_T[k];
+                }
+            }
+            __syncthreads();
+        }
         KB_STAMP(ctl, 5);
     KB_STOP(5);
     }
@@ -2192,7 +2225,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
         // (replace / swap keep the real load sum: the weight changes brokers; a remove or an
         // add changes it, and then the sums are folded again)
         const bool frz = do_res && D.status == 1 && (D.kind == 1 || D.kind == 4) && !s_memb && C.frz_n > 0 &&
-                         C.frz_n < FRZ_MAX && !(KB_ABL & 32);
+                         C.frz_n < FRZ_MAX && !a.eager && !(KB_ABL & 32);
         __shared__ double s_fz[6];                      // frozen step: dU, |updates|, dV, dE, r lo / hi
         __shared__ double s_fq[2][NRW], s_fq2[7][NW];
         __shared__ int s_fcnt[NRW];
@@ -3186,6 +3219,21 @@ __device__ __attribute__((noinline)) void refresh_in_scan(const RefreshArgs* rfp
     }
 }
 
+// One touched broker of the last applied step (DevCtl.eg_b[k]) refolded exactly by an extra
+// workgroup of the next scan launch (ScanArgs.eager): k_step edited the lists already, the
+// lists and partition words are read-only during the launch, and the scan never reads the
+// loads, so the next k_step resolves on exact loads (no halt for a refresh when its decision
+// needs the exact folds).  A halted step's launch is the in-stream refresh's instead.
+__device__ __attribute__((noinline)) void eager_refold(const RefreshArgs* rfp, int k, double* buf) {
+    const RefreshArgs rf = *rfp;
+    DevCtl* ctl = rf.ctl;
+    if (ctl->halted != H_RUN || k >= ctl->eg_n || ctl->list_overflow) return;   // (uniform)
+    const int b = ctl->eg_b[k];
+    if (b < 0 || b >= rf.B || !(rf.bfl[b] & BF_DIRTY)) return;
+    refold_broker<SCAN_THREADS, RF_CHUNK>(rf, b, buf);
+    if (threadIdx.x == 0) atomicSub(&ctl->ndirty, 1);
+}
+
 // --------------------------------------------------- multi-GPU summaries
 
 // pack this rank's scan result + its distinct near-tie keys (within 4*eps of the
@@ -3313,7 +3361,7 @@ __global__ __launch_bounds__(1024) void k_summary(SumArgs a) {
 
 template <int RC>
 static void launch_scan_rc(const ScanArgs& a, bool lds_sets, size_t lds, hipStream_t st) {
-    const int grid = a.nscan + (a.listwg ? 1 : 0);
+    const int grid = a.nscan + (a.listwg ? 1 : 0) + a.eager;
     // (incremental mode: with the set records in LDS only; engine.cpp gates it)
     if (lds_sets && a.incr) hipLaunchKernelGGL((k_scan<RC, true, true>), dim3(grid), dim3(SCAN_THREADS), lds, st, a);
     else if (lds_sets) hipLaunchKernelGGL((k_scan<RC, true, false>), dim3(grid), dim3(SCAN_THREADS), lds, st, a);

@@ -61,6 +61,8 @@ struct ScanArgs {
     int nblk;
     const BlockDesc* bdesc;
     const uint32_t* pset;     // [Ppad] allowed-set index per partition (set records in memory only)
+    int eager;                // > 0: that many extra workgroups after the list workgroup refold the
+                              //    last applied step's touched brokers (DevCtl.eg_*)
 };
 
 struct StepArgs {
@@ -103,6 +105,8 @@ struct StepArgs {
     const uint32_t* pset;     // [Ppad] allowed-set index per partition, or null (the meta word's field)
     int rf_final;             // 1: a halt for exact loads was refolded by this pair's first scan
                               //    (rfpass): resume with a full prep
+    int eager;                // 1: edit the lists in the apply and leave the touched brokers to the
+                              //    next scan's eager refolds (ScanArgs.eager)
 };
 
 

@@ -231,3 +231,34 @@ def test_list_overflow_relists_match_host_refresh(monkeypatch):
     check_loads(eng, cl, ch)
     eng.close()
     ref.close()
+
+
+@pytest.mark.gpu
+def test_eager_refolds_match_lazy_refresh(monkeypatch):
+    """c5's shape (1M x 4096, non-integral loads): with eager refolds (the default at 2048
+    brokers and up: k_step edits the per-broker lists, extra workgroups of the next scan
+    refold the touched brokers exactly) the plan, every su / cu and the final loads equal the
+    lazy engine's (KB_EAGER=0: approximate loads refolded only when a decision halts for
+    them), with fewer halts for exact loads; and the loads equal getBrokerLoad of the plan."""
+    cl, cfg, _ = synth.config("c5", scale=0.1)
+    eng = E.Engine(cl, cfg)
+    ch, err = eng.plan(150)
+    assert err is None, err
+    st = eng.stats()
+    monkeypatch.setenv("KB_EAGER", "0")
+    ref = E.Engine(cl, cfg)
+    rch, rerr = ref.plan(150)
+    assert rerr is None, rerr
+    rst = ref.stats()
+    assert [(c["step"], c["pidx"], c["kind"], c["from_"], c["to"], c["slot"]) for c in ch] == \
+           [(c["step"], c["pidx"], c["kind"], c["from_"], c["to"], c["slot"]) for c in rch]
+    for a, b in zip(ch, rch):
+        scale = max(abs(b["su"]), abs(b["cu"]), 1e-300)
+        assert abs(a["su"] - b["su"]) <= 1e-9 * scale and abs(a["cu"] - b["cu"]) <= 1e-9 * scale
+        if a["exact"] and b["exact"]:
+            assert (a["su"], a["cu"]) == (b["su"], b["cu"])
+    assert eng.loads() == ref.loads()
+    assert st["exact_halts"] < max(1, rst["exact_halts"]), (st, rst)
+    check_loads(eng, cl, ch)
+    eng.close()
+    ref.close()
