@@ -57,7 +57,6 @@ struct kb_engine {
     int twaves = SCAN_THREADS / 64;
     int rcap = 0, rc_dev = 1, K = 3, KR = 6, units = 1, W64 = 1, NP2 = 64;
     int sb_lds = 0, step_lds_bytes = 0;     // k_step: resident allowed-set words, dynamic LDS
-    int bk_lds = 0;                         // k_step: records whose best keys fit its LDS
     int sem = KB_SEM_APPLIED, allow_leader = 0, rebalance = 0;
     int64_t minrep = 2;
     double min_unb = 0.01;
@@ -536,13 +535,7 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
         const int sbw = (int)e->nsets * e->W64;
         e->sb_lds = (sbw * 8 <= STEP_SB_MAX && st_lds + step_lds((int)e->B, e->NP2, sbw).total <= lim) ? 1 : 0;
         if (const char* v = getenv("KB_STEP_SB")) if (*v == '0') e->sb_lds = 0;                           // diagnostic
-        // the records' best keys in LDS too when they fit (staged with the tables: no second
-        // round trip for the resolve's single key and the prep's upper bound); rank
-        // summaries are at most a few per step
-        const int nbk = (int)std::max<int64_t>(e->nscan, 64);
-        e->bk_lds = st_lds + step_lds((int)e->B, e->NP2, e->sb_lds ? sbw : 0, nbk).total <= lim ? nbk : 0;
-        if (const char* v = getenv("KB_STEP_BK")) if (*v == '0') e->bk_lds = 0;                           // diagnostic
-        e->step_lds_bytes = step_lds((int)e->B, e->NP2, e->sb_lds ? sbw : 0, e->bk_lds).total;
+        e->step_lds_bytes = step_lds((int)e->B, e->NP2, e->sb_lds ? sbw : 0).total;
         if (st_lds + e->step_lds_bytes > lim) { e->last_err = "too many brokers for k_step's LDS"; *out = e; return KB_ERR_UNSUPPORTED; }
     }
     HIPCHK(hipStreamCreateWithFlags(&e->st, hipStreamNonBlocking));
@@ -690,7 +683,6 @@ static void fill_step_args(kb_engine* e, StepArgs& a, const Recs& R, int use_spi
     a.RC = e->rc_dev; a.KR = e->KR; a.K = e->K; a.units = e->units; a.W64 = e->W64; a.B = (int)e->B;
     a.nsets = (int)e->nsets; a.NP2 = e->NP2;
     a.sb_lds = e->sb_lds; a.lds_bytes = e->step_lds_bytes;
-    a.bk_lds = R.n <= e->bk_lds ? e->bk_lds : 0;
     a.setbits = e->setbits; a.setrec = e->setrec;
     a.order = e->order; a.posu = e->posu; a.blm = e->blm; a.posm = e->posm; a.r = e->r;
     a.load = e->load; a.lerr = e->lerr; a.eb = e->eb; a.bfl = e->bfl; a.cnt = e->cnt;

@@ -140,10 +140,9 @@ inline Recs summary_recs(unsigned char* base, int n, int keys) {
 }
 
 // dynamic LDS of k_step (byte offsets): loads [B], error bounds / sort keys [NP2],
-// universe order [NP2], allowed-set words of every set when resident [sbw], flags [B],
-// the records' best keys when staged [2 nbk] (Contender)
-struct StepLds { int e, ord, sb, fl, bk, total; };
-__host__ __device__ inline StepLds step_lds(int B, int NP2, int sbw, int nbk = 0) {
+// universe order [NP2], allowed-set words of every set when resident [sbw], flags [B]
+struct StepLds { int e, ord, sb, fl, total; };
+__host__ __device__ inline StepLds step_lds(int B, int NP2, int sbw) {
     auto al = [](int x) { return (x + 15) & ~15; };
     StepLds L;
     int o = al(B * 8);
@@ -151,7 +150,6 @@ __host__ __device__ inline StepLds step_lds(int B, int NP2, int sbw, int nbk = 0
     L.ord = o; o += al(NP2 * 4);
     L.sb = o;  o += al(sbw * 8);
     L.fl = o;  o += al(B);
-    L.bk = o;  o += 2 * nbk * 32;
     L.total = o;
     return L;
 }
@@ -226,8 +224,8 @@ struct DevCtl {
     double uerr, rm_bound;          // rm_bound: max |r| over bl_move (an upper bound when frozen)
     int32_t frz_n, frz_pad;
     // eager refolds (ScanArgs.eager): the brokers whose contribution the last applied step
-    // changed, refolded exactly by extra workgroups of the next scan launch (their list edit
-    // done by k_step), so the next resolve finds every load exact
+    // changed, refolded exactly (after their half of the pending list edit) by extra
+    // workgroups of the next scan launch, so the next resolve finds every load exact
     int32_t eg_n, eg_pad;
     int32_t eg_b[8];
     // diagnostic phase stamps (builds with -DKB_STAMPS): accumulated

@@ -982,7 +982,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
         // (the pending list edit of a step halted for exact loads waits for its refresh)
         const int h = ctl->halted;
         if (a.rfpass && h == H_NEED_EXACT) rf_run();
-        else if (!(a.dbg & 8) && h != H_NEED_EXACT) do_list_op(ctl, a.L, &s_li);
+        else if (!(a.dbg & 8) && h != H_NEED_EXACT && !(a.eager && ctl->eg_n > 0)) do_list_op(ctl, a.L, &s_li);
         return;
     }
     const unsigned long long t_in = wall_clock64();
@@ -1203,14 +1203,13 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
     __shared__ uint32_t s_key[DEDUP_STEP];
     __shared__ unsigned long long s_wb[DEDUP_STEP], s_it[DEDUP_STEP];
     extern __shared__ __align__(16) unsigned char dsm[];
-    const StepLds LY = step_lds(a.B, a.NP2, a.sb_lds ? a.nsets * a.W64 : 0, a.bk_lds);
+    const StepLds LY = step_lds(a.B, a.NP2, a.sb_lds ? a.nsets * a.W64 : 0);
     double* s_ld = (double*)dsm;                     // loads by broker id
     double* s_e = (double*)(dsm + LY.e);             // load error bounds; zero whenever every load is
                                                      // exact, so then also sort keys / exact bl loads
     int32_t* s_ord = (int32_t*)(dsm + LY.ord);       // universe order by (load, id)
     uint64_t* s_sb = (uint64_t*)(dsm + LY.sb);       // allowed-set words (sb_lds)
     uint8_t* s_fl = dsm + LY.fl;                     // BF_* flags
-    Contender* s_bk = (Contender*)(dsm + LY.bk);     // records' best keys [2 R.n] (a.bk_lds)
     __shared__ int s_T[TMAX], s_posT[TMAX];
     __shared__ double s_Lold[TMAX], s_ebold[TMAX];  // touched brokers' load / bound before the apply
     __shared__ int s_memb;                          // the apply changed bl_move's membership
@@ -1227,24 +1226,6 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
     // bytes, 16.5 vs 19.9 us per k_step at c3).  The record headers come to registers.
     const unsigned long long ts_b = ctl->ts_beg, ts_e = ctl->ts_end;   // (kernel timing, tk_on)
     const unsigned long long ts_pe = ctl->ts_prev_end;
-    // (the record headers and, when staged, the best keys first: their loads share the
-    // tables' round trip -- the LDS writes below wait on the in-order vmcnt anyway)
-    double hd0 = HUGE_VAL, hd1 = HUGE_VAL;
-    unsigned long long hc0 = 0, hc1 = 0;
-    uint32_t hflg = 0, hfm = 0, hnk0 = 0, hnk1 = 0;
-    if (tid < a.R.n) {
-        const RecHdr* h = a.R.h(tid);
-        hd0 = ldd(&h->dmin[0]); hd1 = ldd(&h->dmin[1]);
-        hc0 = ldobj(&h->cand[0]); hc1 = ldobj(&h->cand[1]);
-        hflg = ld32(&h->flags) & 1u; hfm = ld32(&h->fmask);
-        const uint32_t nkk = ld32(&h->nkk[0]);
-        hnk0 = nkk & 0xFFFFu; hnk1 = nkk >> 16;
-    }
-    if (a.bk_lds)
-        for (int i = tid; i < a.R.n; i += STEP_THREADS) {
-            const Contender k0 = ldobj(&a.R.h(i)->best[0]), k1 = ldobj(&a.R.h(i)->best[1]);
-            s_bk[2 * i] = k0; s_bk[2 * i + 1] = k1;
-        }
     if (tid < CTL_WORDS) ((uint32_t*)&C)[tid] = ((const uint32_t*)ctl)[tid];
     for (int b = tid; b < B; b += STEP_THREADS) {
         s_ld[b] = a.load[b];
@@ -1261,6 +1242,17 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
     }
     KB_STAMP(ctl, 23);
     KB_STAMP(ctl, 27);
+    double hd0 = HUGE_VAL, hd1 = HUGE_VAL;
+    unsigned long long hc0 = 0, hc1 = 0;
+    uint32_t hflg = 0, hfm = 0, hnk0 = 0, hnk1 = 0;
+    if (tid < a.R.n) {
+        const RecHdr* h = a.R.h(tid);
+        hd0 = ldd(&h->dmin[0]); hd1 = ldd(&h->dmin[1]);
+        hc0 = ldobj(&h->cand[0]); hc1 = ldobj(&h->cand[1]);
+        hflg = ld32(&h->flags) & 1u; hfm = ld32(&h->fmask);
+        const uint32_t nkk = ld32(&h->nkk[0]);
+        hnk0 = nkk & 0xFFFFu; hnk1 = nkk >> 16;
+    }
     KB_STAMP(ctl, 28);
     dedup_clear(T);
     if (tid < 2) { s_nd[tid] = 0; s_li[tid] = -1; s_kfail[tid] = 0; }
@@ -1297,7 +1289,12 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
     }
     const int halted = C.halted;
     const bool do_res = C.prepped && C.steps < C.budget;
-    if (tid == 0) C.eg_n = 0;                    // (the last launch ran this list's refolds)
+    if (tid == 0) {
+        // (the launch that just ran refolded the last step's touched brokers and did its
+        // pending list edit -- unless the step halted: then the in-stream refresh did it)
+        if (C.eg_n > 0 && halted == H_RUN && !C.list_overflow) C.pending_list = 0;
+        C.eg_n = 0;
+    }
     // the steps this Balance() may take (kb_engine_step's mask; SM_ALL = the whole table)
     const uint32_t sm = C.step_mask;
     const bool lead_on = a.allow_leader && (sm & SM_MOVE_LEADERS), non_on = (sm & SM_MOVE_NON_LEADERS) != 0;
@@ -1317,10 +1314,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
     // round trip so they are not held in registers through it
     Contender hb0, hb1;
     hb0.s = hb1.s = -1;
-    if (do_res && tid < a.R.n) {
-        if (a.bk_lds) { hb0 = s_bk[2 * tid]; hb1 = s_bk[2 * tid + 1]; }
-        else { hb0 = ldobj(&a.R.h(tid)->best[0]); hb1 = ldobj(&a.R.h(tid)->best[1]); }
-    }
+    if (do_res && tid < a.R.n) { hb0 = ldobj(&a.R.h(tid)->best[0]); hb1 = ldobj(&a.R.h(tid)->best[1]); }
     KB_STAMP(ctl, 12);
     KB_STOP(1);
     // ---- the scan records (or the gathered rank summaries): one per thread, reduced
@@ -2164,30 +2158,13 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
         }
         __syncthreads();
         if (D.status != 1) { write_back(); return; }
-        // eager refolds: edit the per-broker lists now (the next scan's extra workgroups refold
-        // the touched brokers from them); more touched brokers than EGW: the old way (pending
-        // edit in the scan's list workgroup, the brokers stay dirty until a refresh)
-        if (a.eager && !a.integral && s_nT <= EGW) {
-            __shared__ int s_eok;
-            if (C.pending_list) {
-                const int kind = C.pl_kind, from = C.pl_from, to = C.pl_to;
-                const uint32_t p = (uint32_t)C.pl_part;
-                bool ok = true;
-                if (kind == 1) { list_remove(a.L, from, p, &s_i); ok = list_insert(a.L, to, p, &s_i); }
-                else if (kind == 2) list_remove(a.L, from, p, &s_i);
-                else if (kind == 3) ok = list_insert(a.L, to, p, &s_i);
-                if (tid == 0) s_eok = ok ? 1 : 0;
-            } else if (tid == 0) s_eok = 1;
-            __syncthreads();
-            if (tid == 0) {
-                C.pending_list = 0;
-                if (!s_eok) { C.list_overflow = 1; C.eg_n = 0; }      // (the host relists, refresh)
-                else {
-                    C.eg_n = s_nT;
-                    for (int k = 0; k < s_nT; k++) C.eg_b[k] = s_T[k];
-                }
-            }
-            __syncthreads();
+        // eager refolds: the next scan's extra workgroups edit the touched brokers' lists
+        // (the pending edit, each its own broker's half) and refold them; more touched brokers
+        // than EGW: the old way (the edit in the scan's list workgroup, the brokers stay dirty
+        // until a refresh)
+        if (tid == 0 && a.eager && !a.integral) {
+            C.eg_n = s_nT <= EGW ? s_nT : 0;
+            for (int k = 0; k < C.eg_n; k++) C.eg_b[k] = s_T[k];
         }
         KB_STAMP(ctl, 5);
     KB_STOP(5);
@@ -2263,12 +2240,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
         const bool bkeys = do_res && tid < a.R.n;
         Contender bk0, bk1;
         bk0.s = bk1.s = -1;
-#if KB_ABL & 64
-        if (bkeys) { bk0 = hb0; bk1 = hb1; }            // (variant: the resolve's registers)
-#else
-        if (bkeys && a.bk_lds) { bk0 = s_bk[2 * tid]; bk1 = s_bk[2 * tid + 1]; }
-        else if (bkeys) { bk0 = ldobj(&a.R.h(tid)->best[0]); bk1 = ldobj(&a.R.h(tid)->best[1]); }
-#endif
+        if (bkeys) { bk0 = ldobj(&a.R.h(tid)->best[0]); bk1 = ldobj(&a.R.h(tid)->best[1]); }
         if (tid < nT) { s_fl[s_T[tid]] |= BF_TOUCHED; s_cntT[tid] = 0; }
         if (tid == 0) { s_unc = 0; s_nsub = 0; }
         if (wid < NRW) {
@@ -2633,8 +2605,17 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
                 int nj[G];
 #pragma unroll
                 for (int j = 0; j < G; j++) nj[j] = lane < W64 ? (int)__popcll(sb[j][lane] & s_blmb[lane]) : 0;
+                {
+                    // |set ∩ bl_move| of the G sets in one reduction: 16-bit fields (at most
+                    // MAXB = 4096 per set), G <= 4
+                    static_assert(G <= 4 && MAXB < 65536, "packed nelig sums");
+                    unsigned long long pk = 0;
 #pragma unroll
-                for (int j = 0; j < G; j++) nj[j] = wave_sum(nj[j]);
+                    for (int j = 0; j < G; j++) pk |= (unsigned long long)nj[j] << (16 * j);
+                    pk = wave_sum(pk);
+#pragma unroll
+                    for (int j = 0; j < G; j++) nj[j] = (int)((pk >> (16 * j)) & 0xFFFFu);
+                }
 #pragma unroll
                 for (int j = 0; j < G; j++) {
                     if (j >= ng) break;
@@ -3220,16 +3201,32 @@ __device__ __attribute__((noinline)) void refresh_in_scan(const RefreshArgs* rfp
 }
 
 // One touched broker of the last applied step (DevCtl.eg_b[k]) refolded exactly by an extra
-// workgroup of the next scan launch (ScanArgs.eager): k_step edited the lists already, the
-// lists and partition words are read-only during the launch, and the scan never reads the
-// loads, so the next k_step resolves on exact loads (no halt for a refresh when its decision
-// needs the exact folds).  A halted step's launch is the in-stream refresh's instead.
+// workgroup of the next scan launch (ScanArgs.eager), after its own half of the pending list
+// edit (each list belongs to one workgroup; the list workgroup skips the edit), while the
+// scan runs (it never reads the loads): the next k_step resolves on exact loads, with no halt
+// for a refresh when its decision needs the exact folds.  A halted step's launch is the
+// in-stream refresh's instead (it does the edit and refolds every dirty broker).
 __device__ __attribute__((noinline)) void eager_refold(const RefreshArgs* rfp, int k, double* buf) {
     const RefreshArgs rf = *rfp;
     DevCtl* ctl = rf.ctl;
     if (ctl->halted != H_RUN || k >= ctl->eg_n || ctl->list_overflow) return;   // (uniform)
     const int b = ctl->eg_b[k];
-    if (b < 0 || b >= rf.B || !(rf.bfl[b] & BF_DIRTY)) return;
+    if (b < 0 || b >= rf.B) return;
+    if (ctl->pending_list) {
+        // this broker's half of the last step's list edit (replace = remove from `from`,
+        // insert into `to`: different lists, different workgroups)
+        __shared__ int s_i;
+        const int kind = ctl->pl_kind;
+        const uint32_t p = (uint32_t)ctl->pl_part;
+        bool ok = true;
+        if (b == ctl->pl_from && (kind == 1 || kind == 2)) list_remove(rf.L, b, p, &s_i);
+        if (b == ctl->pl_to && (kind == 1 || kind == 3)) ok = list_insert(rf.L, b, p, &s_i);
+        if (!ok) {                                 // (the broker stays dirty: the host relists)
+            if (threadIdx.x == 0) ctl->list_overflow = 1;
+            return;
+        }
+    }
+    if (!(rf.bfl[b] & BF_DIRTY)) return;
     refold_broker<SCAN_THREADS, RF_CHUNK>(rf, b, buf);
     if (threadIdx.x == 0) atomicSub(&ctl->ndirty, 1);
 }

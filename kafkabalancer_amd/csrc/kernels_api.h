@@ -74,8 +74,7 @@ struct StepArgs {
     long long Ppad;
     int RC, KR, K, units, W64, B, nsets, NP2;
     int sb_lds;               // 1: every set's allowed-set words are staged in LDS
-    int lds_bytes;            // dynamic LDS (step_lds(B, NP2, sb_lds ? nsets * W64 : 0, bk_lds).total)
-    int bk_lds;               // > 0: the records' best keys are staged in LDS (room for bk_lds records)
+    int lds_bytes;            // dynamic LDS (step_lds(B, NP2, sb_lds ? nsets * W64 : 0).total)
     const uint64_t* setbits;
     uint4* setrec;
     int32_t* order;           // [B] universe sorted by (load, id)
@@ -105,8 +104,8 @@ struct StepArgs {
     const uint32_t* pset;     // [Ppad] allowed-set index per partition, or null (the meta word's field)
     int rf_final;             // 1: a halt for exact loads was refolded by this pair's first scan
                               //    (rfpass): resume with a full prep
-    int eager;                // 1: edit the lists in the apply and leave the touched brokers to the
-                              //    next scan's eager refolds (ScanArgs.eager)
+    int eager;                // 1: leave the touched brokers (and their list edit) to the next
+                              //    scan's eager refolds (ScanArgs.eager)
 };
 
 

@@ -16,5 +16,5 @@ for spec in "$@"; do
   python3 -c "
 import json
 d=[json.loads(l) for l in open('$O/$name.out') if l.startswith('{')][0]
-print('$name', round(d['ms_per_step']*1e3,2), {k: round(x,2) for k,x in d['kernels_us_per_step'].items()}, d['engine_events'])"
+print('$name', round(d['ms_per_step']*1e3,2), {k: round(x,2) for k,x in d['kernels_us_per_launch'].items()}, d['engine_events'])"
 done
