@@ -1289,18 +1289,21 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
     }
     const int halted = C.halted;
     const bool do_res = C.prepped && C.steps < C.budget;
-    if (tid == 0) {
-        // (the launch that just ran refolded the last step's touched brokers and did its
-        // pending list edit -- unless the step halted: then the in-stream refresh did it)
-        if (C.eg_n > 0 && halted == H_RUN && !C.list_overflow) C.pending_list = 0;
-        C.eg_n = 0;
+    // (eager refolds: the launch that just ran refolded the last step's touched brokers and
+    // did its pending list edit -- unless the step halted, then the in-stream refresh did it;
+    // every thread reads the control words before thread 0 rewrites them)
+    bool eg_done = false;
+    if (a.eager) {
+        eg_done = C.eg_n > 0 && halted == H_RUN && !C.list_overflow;
+        __syncthreads();
+        if (tid == 0) { if (eg_done) C.pending_list = 0; C.eg_n = 0; }
     }
     // the steps this Balance() may take (kb_engine_step's mask; SM_ALL = the whole table)
     const uint32_t sm = C.step_mask;
     const bool lead_on = a.allow_leader && (sm & SM_MOVE_LEADERS), non_on = (sm & SM_MOVE_NON_LEADERS) != 0;
     const double eps = C.eps, inv_avg = C.inv_avg, U0h = C.U0;
     const int nblm0 = C.nblm, ndirty0 = C.ndirty;
-    const bool pend = C.pending_list != 0;
+    const bool pend = !eg_done && C.pending_list != 0;   // (eg_done: thread 0 clears it)
     __shared__ long long s_moved;
     __shared__ int s_lkind, s_lpick;
     __shared__ uint32_t s_lpart;
@@ -2605,17 +2608,8 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
                 int nj[G];
 #pragma unroll
                 for (int j = 0; j < G; j++) nj[j] = lane < W64 ? (int)__popcll(sb[j][lane] & s_blmb[lane]) : 0;
-                {
-                    // |set ∩ bl_move| of the G sets in one reduction: 16-bit fields (at most
-                    // MAXB = 4096 per set), G <= 4
-                    static_assert(G <= 4 && MAXB < 65536, "packed nelig sums");
-                    unsigned long long pk = 0;
 #pragma unroll
-                    for (int j = 0; j < G; j++) pk |= (unsigned long long)nj[j] << (16 * j);
-                    pk = wave_sum(pk);
-#pragma unroll
-                    for (int j = 0; j < G; j++) nj[j] = (int)((pk >> (16 * j)) & 0xFFFFu);
-                }
+                for (int j = 0; j < G; j++) nj[j] = wave_sum(nj[j]);   // (independent chains: they overlap)
 #pragma unroll
                 for (int j = 0; j < G; j++) {
                     if (j >= ng) break;
