@@ -374,7 +374,8 @@ def main():
                           "k_step_alone_us": res, "iters": args.steps}))
         return
     if args.stamps:
-        os.environ["KB_ENGINE_LIB"] = os.path.join(ROOT, "kafkabalancer_amd", "lib", "libkbengine_stamps.so")
+        os.environ["KB_ENGINE_LIB"] = os.environ.get("KB_STAMPS_LIB") or \
+            os.path.join(ROOT, "kafkabalancer_amd", "lib", "libkbengine_stamps.so")
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

@@ -41,6 +41,10 @@ namespace kbe {
 
 // --------------------------------------------------------------- helpers
 
+#ifndef KB_EAGER_CODE
+#define KB_EAGER_CODE 1   // (diagnostic A/B: 0 compiles the eager-refold code out)
+#endif
+
 __device__ __forceinline__ unsigned long long d2u(double d) { return (unsigned long long)__double_as_longlong(d); }
 __device__ __forceinline__ double u2d(unsigned long long u) { return __longlong_as_double((long long)u); }
 
@@ -968,7 +972,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
     DevCtl* ctl = a.ctl;
     // eager refolds: the last workgroups of the grid refold the brokers the last step touched
     // (their lists already edited by k_step), concurrently with the scan
-    if (a.eager && (int)blockIdx.x >= a.nscan + (a.listwg ? 1 : 0)) {
+    if (KB_EAGER_CODE && a.eager && (int)blockIdx.x >= a.nscan + (a.listwg ? 1 : 0)) {
         eager_refold(a.rf, (int)blockIdx.x - a.nscan - (a.listwg ? 1 : 0), (double*)smem);
         return;
     }
@@ -982,7 +986,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
         // (the pending list edit of a step halted for exact loads waits for its refresh)
         const int h = ctl->halted;
         if (a.rfpass && h == H_NEED_EXACT) rf_run();
-        else if (!(a.dbg & 8) && h != H_NEED_EXACT && !(a.eager && ctl->eg_n > 0)) do_list_op(ctl, a.L, &s_li);
+        else if (!(a.dbg & 8) && h != H_NEED_EXACT && !(KB_EAGER_CODE && a.eager && ctl->eg_n > 0)) do_list_op(ctl, a.L, &s_li);
         return;
     }
     const unsigned long long t_in = wall_clock64();
@@ -1293,7 +1297,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
     // did its pending list edit -- unless the step halted, then the in-stream refresh did it;
     // every thread reads the control words before thread 0 rewrites them)
     bool eg_done = false;
-    if (a.eager) {
+    if (KB_EAGER_CODE && a.eager) {
         eg_done = C.eg_n > 0 && halted == H_RUN && !C.list_overflow;
         __syncthreads();
         if (tid == 0) { if (eg_done) C.pending_list = 0; C.eg_n = 0; }
@@ -2165,7 +2169,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
         // (the pending edit, each its own broker's half) and refold them; more touched brokers
         // than EGW: the old way (the edit in the scan's list workgroup, the brokers stay dirty
         // until a refresh)
-        if (tid == 0 && a.eager && !a.integral) {
+        if (KB_EAGER_CODE && tid == 0 && a.eager && !a.integral) {
             C.eg_n = s_nT <= EGW ? s_nT : 0;
             for (int k = 0; k < C.eg_n; k++) C.eg_b[k] = s_T[k];
         }

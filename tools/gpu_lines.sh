@@ -10,17 +10,18 @@ run() {   # name timeout args...
   grep -h '^{' $O/$n.out | tail -1 > $O/$n.json
   python3 -c "
 import json; d=json.load(open('$O/$n.json'))
-print('$n', {k: d.get(k) for k in ('value','ms_per_step','balance_per_call_us','plan_per_step_us')}, d.get('kernels_us_per_step', ''), d.get('cli', ''))"
+print('$n', {k: d.get(k) for k in ('value','ms_per_step','balance_per_call_us','steps_table_per_balance_us','plan_per_step_us')}, d.get('kernels_us_per_launch', ''), d.get('cli', ''))"
 }
 for l in ${LINES:-default c2 c4 c5 dropin prof}; do
   case $l in
     default) run default 400 ;;
-    c2) run c2 200 --workload c2 --steps 80 --no-cpu-baseline ;;
-    c4) run c4 300 --workload c4 --steps 1000 --no-cpu-baseline ;;
-    c5) run c5 500 --workload c5 --steps 200 --no-cpu-baseline ;;
+    c2) run c2 300 --workload c2 --steps 80 --cpu-seconds 10 ;;
+    c4) run c4 400 --workload c4 --steps 1000 --cpu-seconds 10 ;;
+    c5) run c5 600 --workload c5 --steps 200 --cpu-seconds 10 ;;
     dropin) run dropin 500 --workload c3 --drop-in --steps 200 ;;
-    prof) WLS="c3 c2" tools/prof_wl.sh > $O/prof.txt 2>&1 || { cat $O/prof.txt; exit 1; }
-          cat $O/prof.txt; cp gpurun_out/prof/c3/run_kernel_stats.csv $O/c3_kernel_stats.csv
-          cp gpurun_out/prof/c2/run_kernel_stats.csv $O/c2_kernel_stats.csv ;;
+    prof) WLS="c3 c5" tools/prof_wl.sh > $O/prof.txt 2>&1 || { cat $O/prof.txt; exit 1; }
+          cat $O/prof.txt
+          for w in c3 c5; do cp $(find gpurun_out/prof/$w -name 'run_kernel_stats.csv' | head -1) $O/${w}_kernel_stats.csv
+                             grep -h '^{' gpurun_out/prof/$w/bench.out | tail -1 > $O/${w}_bench_under_rocprof.json; done ;;
   esac
 done
