@@ -91,6 +91,8 @@ struct kb_engine {
     double* r = nullptr;
     int32_t* bset_off = nullptr;
     int32_t* bset_ids = nullptr;
+    unsigned char* gscr = nullptr;    // k_step's per-broker tables past MAXB brokers (StepArgs.gscr)
+    bool gb = false;                  // B > MAXB: broker tables in memory (k_scan GT, k_step GB)
     unsigned char* recs = nullptr;
     Contender* cont = nullptr;
     uint32_t cont_cap = 1u << 20;
@@ -201,32 +203,32 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
     if (c->partition_id) e->pids.assign(c->partition_id, c->partition_id + n);
 
     // dense broker universe = sorted unique ids (so dense order == BrokerID order).
-    // An open-addressing id table (at most MAXB distinct ids, else unsupported) instead of
+    // An open-addressing id table (at most MAXB_G distinct ids, else unsupported) instead of
     // sorting every replica id: one hash probe per replica (c3: 3M) and a sort of the
     // few distinct ids.
     int64_t nrep_total = n ? c->replica_off[n] - c->replica_off[0] : 0;
-    constexpr uint32_t HCAP = 1u << 14;                  // > 2 * MAXB: short probe chains
+    constexpr uint32_t HCAP = 1u << 16;                  // > 2 * MAXB_G: short probe chains
     std::vector<int64_t> hkey(HCAP);
     std::vector<int32_t> hval(HCAP, -1);
     std::vector<int64_t> all;
-    all.reserve(MAXB + 1);
+    all.reserve(MAXB_G + 1);
     auto hslot = [&](int64_t id) -> uint32_t {
         uint64_t x = (uint64_t)id * 0x9E3779B97F4A7C15ull;
-        uint32_t h = (uint32_t)(x >> 50);                // top 14 bits
+        uint32_t h = (uint32_t)(x >> 48);                // top 16 bits
         while (hval[h] >= 0 && hkey[h] != id) h = (h + 1) & (HCAP - 1);
         return h;
     };
     auto add_id = [&](int64_t id) {
         const uint32_t h = hslot(id);
-        if (hval[h] < 0 && (int64_t)all.size() <= MAXB) { hkey[h] = id; hval[h] = 0; all.push_back(id); }
+        if (hval[h] < 0 && (int64_t)all.size() <= MAXB_G) { hkey[h] = id; hval[h] = 0; all.push_back(id); }
     };
-    for (int64_t i = 0; i < nrep_total && (int64_t)all.size() <= MAXB; i++) add_id(c->replica_ids[c->replica_off[0] + i]);
+    for (int64_t i = 0; i < nrep_total && (int64_t)all.size() <= MAXB_G; i++) add_id(c->replica_ids[c->replica_off[0] + i]);
     if (c->n_sets > 0 && c->set_off)
-        for (int64_t i = c->set_off[0]; i < c->set_off[c->n_sets] && (int64_t)all.size() <= MAXB; i++) add_id(c->set_ids[i]);
+        for (int64_t i = c->set_off[0]; i < c->set_off[c->n_sets] && (int64_t)all.size() <= MAXB_G; i++) add_id(c->set_ids[i]);
     if (!cfg->brokers_nil)
-        for (int64_t i = 0; i < cfg->n_brokers && (int64_t)all.size() <= MAXB; i++) add_id(cfg->brokers[i]);
-    if ((int64_t)all.size() > MAXB) {
-        e->last_err = "engine supports at most 4096 distinct brokers";
+        for (int64_t i = 0; i < cfg->n_brokers && (int64_t)all.size() <= MAXB_G; i++) add_id(cfg->brokers[i]);
+    if ((int64_t)all.size() > MAXB_G) {
+        e->last_err = "engine supports at most 16384 distinct brokers";
         *out = e;
         return KB_ERR_UNSUPPORTED;
     }
@@ -498,15 +500,18 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
     const size_t rbytes = (size_t)e->B * 16;          // (r, f(r)) pairs
     const size_t setbytes = (size_t)e->nsets * e->units * 16;
     const size_t dedup = (size_t)DEDUP_SCAN * (4 + 8 + 8);
-    e->lds_sets = setbytes <= (size_t)LDS_SETS_MAX;
+    // past MAXB brokers the scan reads the broker tables (and the set records) from memory
+    // (L2-resident) and k_step keeps its per-broker tables in a memory scratch
+    e->gb = e->B > MAXB;
+    e->lds_sets = !e->gb && setbytes <= (size_t)LDS_SETS_MAX;
     const size_t pbytes = ((size_t)e->B * 2 + 15) & ~(size_t)15;
-    e->scan_lds = rbytes + 2 * pbytes + (e->lds_sets ? setbytes : 0) + dedup;
+    e->scan_lds = (e->gb ? 0 : rbytes + 2 * pbytes) + (e->lds_sets ? setbytes : 0) + dedup;
     // (room for the in-stream refresh's two fold buffers: ScanArgs.rfpass)
     e->rf_stream = !e->integral;
     if (const char* v = getenv("KB_RF_STREAM")) if (*v == '0') e->rf_stream = false;   // diagnostic
     if (e->rf_stream) e->scan_lds = std::max(e->scan_lds, (size_t)RF_LDS_BYTES);
     // one wave of resident workgroups; each loops over its tiles
-    int per_cu = scan_blocks_per_cu(e->rc_dev, e->lds_sets, e->scan_lds);
+    int per_cu = scan_blocks_per_cu(e->rc_dev, e->lds_sets, e->gb, e->scan_lds);
     if (per_cu < 1) per_cu = 1;
     // a tile is twaves blocks of BLK partitions, one per scoring wave: the full 16 when the
     // shard fills every resident workgroup slot with whole tiles, fewer on small shards
@@ -529,13 +534,13 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
     if (const char* v = getenv("KB_DEBUG_SCAN")) e->dbg_scan = atoi(v);                                   // diagnostic
     {
         // k_step's LDS: static tables + per-broker arrays (+ every set's words when they fit)
-        const int st_lds = step_static_lds();
+        const int st_lds = step_static_lds(e->gb);
         if (st_lds < 0) { e->last_err = "k_step attributes unavailable"; *out = e; return KB_ERR_HIP; }
         const int lim = 160 * 1024;
         const int sbw = (int)e->nsets * e->W64;
-        e->sb_lds = (sbw * 8 <= STEP_SB_MAX && st_lds + step_lds((int)e->B, e->NP2, sbw).total <= lim) ? 1 : 0;
+        e->sb_lds = (!e->gb && sbw * 8 <= STEP_SB_MAX && st_lds + step_lds((int)e->B, e->NP2, sbw).total <= lim) ? 1 : 0;
         if (const char* v = getenv("KB_STEP_SB")) if (*v == '0') e->sb_lds = 0;                           // diagnostic
-        e->step_lds_bytes = step_lds((int)e->B, e->NP2, e->sb_lds ? sbw : 0).total;
+        e->step_lds_bytes = e->gb ? 0 : step_lds((int)e->B, e->NP2, e->sb_lds ? sbw : 0).total;
         if (st_lds + e->step_lds_bytes > lim) { e->last_err = "too many brokers for k_step's LDS"; *out = e; return KB_ERR_UNSUPPORTED; }
     }
     HIPCHK(hipStreamCreateWithFlags(&e->st, hipStreamNonBlocking));
@@ -547,6 +552,7 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
     // (+16 B on the arrays k_step stages by LDS-DMA: it copies whole 16-B granules)
     HIPCHK(dalloc(&e->load, e->B + 2));
     HIPCHK(dalloc(&e->lerr, e->B));
+    if (e->gb) HIPCHK(dalloc(&e->gscr, (size_t)step_lds((int)e->B, e->NP2, 0).total));
     HIPCHK(dalloc(&e->eb, e->B + 2));
     HIPCHK(dalloc(&e->bfl, e->B + 16));
     HIPCHK(dalloc(&e->cnt, e->B));
@@ -676,6 +682,7 @@ static void fill_scan_args(kb_engine* e, ScanArgs& s) {
     s.rfpass = 0;
     s.rf = e->rf_dev;
     s.eager = e->eager && e->nscan > 0 ? EGW : 0;
+    s.gt = e->gb ? 1 : 0;
 }
 
 static void fill_step_args(kb_engine* e, StepArgs& a, const Recs& R, int use_spill) {
@@ -683,6 +690,7 @@ static void fill_step_args(kb_engine* e, StepArgs& a, const Recs& R, int use_spi
     a.RC = e->rc_dev; a.KR = e->KR; a.K = e->K; a.units = e->units; a.W64 = e->W64; a.B = (int)e->B;
     a.nsets = (int)e->nsets; a.NP2 = e->NP2;
     a.sb_lds = e->sb_lds; a.lds_bytes = e->step_lds_bytes;
+    a.gscr = e->gscr;
     a.setbits = e->setbits; a.setrec = e->setrec;
     a.order = e->order; a.posu = e->posu; a.blm = e->blm; a.posm = e->posm; a.r = e->r;
     a.load = e->load; a.lerr = e->lerr; a.eb = e->eb; a.bfl = e->bfl; a.cnt = e->cnt;
@@ -1453,7 +1461,7 @@ extern "C" void kb_engine_destroy(kb_engine* e) {
     if (!e) return;
     void* ptrs[] = {e->w, e->rep, e->meta, e->pset, e->nc, e->load, e->lerr, e->eb, e->bfl, e->cnt,
                     e->setbits, e->setrec, e->order, e->posu, e->blm, e->posm, e->r,
-                    e->bset_off, e->bset_ids, e->recs, e->cont, e->ctl, e->log, e->bdesc, e->ubdesc,
+                    e->bset_off, e->bset_ids, e->gscr, e->recs, e->cont, e->ctl, e->log, e->bdesc, e->ubdesc,
                     e->L.lstart, e->L.llen, e->L.lcap, e->L.lent, e->rf_dev};
     for (void* p : ptrs) if (p) hipFree(p);
     if (e->h_ctl) hipHostFree(e->h_ctl);

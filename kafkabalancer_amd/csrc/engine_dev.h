@@ -6,7 +6,9 @@
 
 namespace kbe {
 
-constexpr int MAXB = 4096;          // dense broker universe limit (sorted in LDS)
+constexpr int MAXB = 4096;          // brokers whose tables k_scan / k_step keep in LDS
+constexpr int MAXB_G = 16384;       // dense broker universe limit (past MAXB: tables in memory;
+                                    // 15-bit ids in the near-tie keys, 16-bit bl positions)
 constexpr int MAXR = 16;            // replica slots per partition
 #ifndef KB_SCAN_THREADS
 #define KB_SCAN_THREADS 1024

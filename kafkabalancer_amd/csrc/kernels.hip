@@ -231,6 +231,46 @@ __device__ __attribute__((noinline)) double exact_unbalance_wave(const double* L
     return U;
 }
 
+// The same fold over bl-ordered loads in memory (k_step with its broker tables in memory,
+// B > MAXB): the lanes load each 64-element chunk (the next one in flight while the
+// current one is chained) into the wave's LDS row, and the chain runs from there.
+__device__ __attribute__((noinline)) double exact_unbalance_wave_g(const double* Lm, int n, int ps, int pt, double Ls, double Lt, double* scr_) {
+    lds_f64* scr = (lds_f64*)scr_;
+    const int lane = threadIdx.x & 63;
+    auto ld = [&](int k) -> double {
+        const int i = k + lane;
+        return i < n ? (i == ps ? Ls : (i == pt ? Lt : Lm[i])) : 0.0;
+    };
+    double S = 0.0, nx = ld(0);
+    for (int k = 0; k < n; k += 64) {
+        const int m = n - k < 64 ? n - k : 64;
+        const double cur = nx;
+        nx = ld(k + 64);
+        scr[lane] = cur;
+        wave_lds_sync();
+        S = chain_lds(S, scr, m);
+        wave_lds_sync();
+    }
+    const double avg = S / (double)n;
+    double U = 0.0;
+    nx = ld(0);
+    for (int k = 0; k < n; k += 64) {
+        const int m = n - k < 64 ? n - k : 64;
+        const double cur = nx;
+        nx = ld(k + 64);
+        scr[lane] = term_x(cur, avg);
+        wave_lds_sync();
+        U = chain_lds(U, scr, m);
+        wave_lds_sync();
+    }
+    return U;
+}
+template <bool GB>
+__device__ __forceinline__ double exact_unb_w(const double* Lm, int n, int ps, int pt, double Ls, double Lt, double* scr) {
+    if constexpr (GB) return exact_unbalance_wave_g(Lm, n, ps, pt, Ls, Lt, scr);
+    else return exact_unbalance_wave(Lm, n, ps, pt, Ls, Lt, scr);
+}
+
 // ---------------------------------------------- near-tie de-duplication
 // LDS open-addressing table keyed by (kind, source, target); the weight bits are
 // claimed by the first insert; a different weight under the same key is a
@@ -438,9 +478,9 @@ __device__ __forceinline__ void set_record(const ScanArgs& a, const uint4* s_set
 // walk every allowed, non-replica target in bl order for one (partition, slot)
 // and emit the ones within 4*eps of the tile minimum g; stop once 8*eps is
 // exceeded (the approximate delta is monotone in the target load up to 2*eps).
-template <int RC>
-__device__ void walk_targets(const ScanArgs& a, const Dedup& T, const double2* s_rf, const int16_t* s_pos,
-                             const uint16_t* s_blm, const uint4 (&R)[sr_units(RC)], int kind, long long p,
+template <int RC, typename RF, typename PS, typename BL>
+__device__ void walk_targets(const ScanArgs& a, const Dedup& T, RF s_rf, PS s_pos,
+                             BL s_blm, const uint4 (&R)[sr_units(RC)], int kind, long long p,
                              int slot, int src, const uint32_t (&reps)[RC], int nrep, int set, double w, double ds,
                              double g, double eps, double inv_avg, int nblm) {
     constexpr int KR = sr_kr(RC);
@@ -487,7 +527,7 @@ __device__ __forceinline__ int first_target(const ScanArgs& a, const uint4* s_se
     uint4 R[U];
     set_record<RC, LSETS>(a, s_set, set, R);
     *nelig = (int)rec_u16(R, 0);
-    // slots past nrep compare against an id no record holds (ids < MAXB, NONE16 = padding);
+    // slots past nrep compare against an id no record holds (ids < MAXB_G, NONE16 = padding);
     // padding is never a replica, so it is picked only when no valid target precedes it
     uint32_t rq[RC];
 #pragma unroll
@@ -537,9 +577,23 @@ struct TabRaw {
     uint4 set;
 };
 
+// Broker tables read from memory (GT: more brokers than the LDS tables hold, B > MAXB):
+// the same indexing as the LDS tables, (r, f(r)) computed from r[] on each read; the
+// tables stay L2-resident (B * 16 bytes)
+struct RfMem {
+    const double* r;
+    __device__ __forceinline__ double2 operator[](int b) const { const double x = r[b]; return make_double2(x, fsq(x)); }
+};
+struct I32Mem {
+    const int32_t* p;
+    __device__ __forceinline__ int operator[](int i) const { return p[i]; }
+};
+template <bool GT> struct ScanTabs { double2* rf; int16_t* pos; uint16_t* blm; };
+template <> struct ScanTabs<true> { RfMem rf; I32Mem pos; I32Mem blm; };
+
 // One scan round of a workgroup over its tiles (its first tile and the tables already
 // loaded into A / T): stage the tables, score, write the workgroup record.
-template <int RC, bool LSETS, bool INCR>
+template <int RC, bool LSETS, bool INCR, bool GT>
 __device__ __forceinline__ void scan_round(const ScanArgs& a, const ScanParams& q, unsigned char* smem,
                                            PartRaw<RC>& A, const TabRaw& TR,
                                            unsigned long long t_in,
@@ -549,11 +603,19 @@ __device__ __forceinline__ void scan_round(const ScanArgs& a, const ScanParams& 
     constexpr int NW = SCAN_THREADS / 64;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
 
-    double2* s_rf = (double2*)smem;                 // (r, f(r)) per broker
-    const size_t rbytes = (size_t)a.B * 16;
-    int16_t* s_pos = (int16_t*)(smem + rbytes);
-    const size_t pbytes = ((size_t)a.B * 2 + 15) & ~(size_t)15;
-    uint16_t* s_blm = (uint16_t*)(smem + rbytes + pbytes);
+    const size_t rbytes = GT ? 0 : (size_t)a.B * 16;
+    const size_t pbytes = GT ? 0 : ((size_t)a.B * 2 + 15) & ~(size_t)15;
+    ScanTabs<GT> TB;
+    if constexpr (GT) {
+        TB.rf = RfMem{a.r}; TB.pos = I32Mem{a.posm}; TB.blm = I32Mem{a.blm};
+    } else {
+        TB.rf = (double2*)smem;                     // (r, f(r)) per broker
+        TB.pos = (int16_t*)(smem + rbytes);
+        TB.blm = (uint16_t*)(smem + rbytes + pbytes);
+    }
+    const auto s_rf = TB.rf;
+    const auto s_pos = TB.pos;
+    const auto s_blm = TB.blm;
     uint4* s_set = (uint4*)(smem + rbytes + 2 * pbytes);
     const size_t setbytes = LSETS ? (size_t)a.nsets * U * 16 : 0;
     uint32_t* s_key = (uint32_t*)(smem + rbytes + 2 * pbytes + setbytes);
@@ -568,11 +630,12 @@ __device__ __forceinline__ void scan_round(const ScanArgs& a, const ScanParams& 
 
     int tile = wg;
     // the lookup tables (loaded by the caller with the control block when they are small)
-    if (TR.pre) {
+    if constexpr (GT) {
+    } else if (TR.pre) {
         if (tid < a.B) {
-            s_rf[tid] = make_double2(TR.r, fsq(TR.r));
-            s_pos[tid] = (int16_t)TR.pos;
-            s_blm[tid] = (uint16_t)TR.blm;
+            TB.rf[tid] = make_double2(TR.r, fsq(TR.r));
+            TB.pos[tid] = (int16_t)TR.pos;
+            TB.blm[tid] = (uint16_t)TR.blm;
         }
     } else {
         // (more brokers: every load first -- at most MAXB / SCAN_THREADS per thread --
@@ -591,9 +654,9 @@ __device__ __forceinline__ void scan_round(const ScanArgs& a, const ScanParams& 
         for (int k = 0; k < TQ; k++) {
             const int i = k * SCAN_THREADS + tid;
             if (i < a.B) {
-                s_rf[i] = make_double2(rr[k], fsq(rr[k]));
-                s_pos[i] = (int16_t)pp[k];
-                s_blm[i] = (uint16_t)bb[k];
+                TB.rf[i] = make_double2(rr[k], fsq(rr[k]));
+                TB.pos[i] = (int16_t)pp[k];
+                TB.blm[i] = (uint16_t)bb[k];
             }
         }
     }
@@ -965,7 +1028,7 @@ __device__ __attribute__((noinline)) void refresh_in_scan(const RefreshArgs* rfp
                                                           uint32_t part, double* buf);   // (k_refresh below)
 __device__ __attribute__((noinline)) void eager_refold(const RefreshArgs* rfp, int k, double* buf);
 
-template <int RC, bool LSETS, bool INCR>
+template <int RC, bool LSETS, bool INCR, bool GT = false>
 __global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
     extern __shared__ __align__(16) unsigned char smem[];
     __shared__ int s_li;
@@ -1024,7 +1087,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
     const double c_wskip = cc->wskip;
     TabRaw TR;
     const int nu = LSETS ? a.nsets * sr_units(RC) : 0;
-    TR.pre = a.B <= SCAN_THREADS && nu <= SCAN_THREADS;
+    TR.pre = !GT && a.B <= SCAN_THREADS && nu <= SCAN_THREADS;
     if (TR.pre) {
         const int i = min((int)threadIdx.x, a.B - 1);
         TR.r = ldd(a.r + i);
@@ -1061,7 +1124,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
         c0 = d0.blk * BLK;
         load_parts<RC, LSETS>(a, c0 + (long long)(threadIdx.x & 63) * PER_LANE, A);
     }
-    scan_round<RC, LSETS, INCR>(a, q, smem, A, TR, t_in, (int)blockIdx.x, c0);
+    scan_round<RC, LSETS, INCR, GT>(a, q, smem, A, TR, t_in, (int)blockIdx.x, c0);
 }
 
 // --------------------------------------------------------------- k_step
@@ -1159,9 +1222,10 @@ constexpr int CTL_WORDS = (int)(offsetof(DevCtl, stamps) / 4);
 // The serial half of one Balance() step (k_step): stage the control block, the
 // broker tables and the allowed-set words in LDS, resolve the scan records (when
 // prepped), apply the change and prep the next step.
-template <bool BIG>
+template <bool BIG, bool GB>
 __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
     DevCtl* ctl = a.ctl;
+    constexpr int MB = GB ? MAXB_G : MAXB;          // (GB: the per-broker tables in memory, a.gscr)
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     constexpr int NW = STEP_THREADS / 64;
     const unsigned long long t_in = wall_clock64();
@@ -1206,7 +1270,9 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
     __shared__ __align__(16) double s_fold[NW * 64];   // per-wave rows of the exact folds
     __shared__ uint32_t s_key[DEDUP_STEP];
     __shared__ unsigned long long s_wb[DEDUP_STEP], s_it[DEDUP_STEP];
-    extern __shared__ __align__(16) unsigned char dsm[];
+    extern __shared__ __align__(16) unsigned char dsm_lds[];
+    unsigned char* dsm;
+    if constexpr (GB) dsm = a.gscr; else dsm = dsm_lds;
     const StepLds LY = step_lds(a.B, a.NP2, a.sb_lds ? a.nsets * a.W64 : 0);
     double* s_ld = (double*)dsm;                     // loads by broker id
     double* s_e = (double*)(dsm + LY.e);             // load error bounds; zero whenever every load is
@@ -1218,7 +1284,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
     __shared__ double s_Lold[TMAX], s_ebold[TMAX];  // touched brokers' load / bound before the apply
     __shared__ int s_memb;                          // the apply changed bl_move's membership
     __shared__ int s_cntT[TMAX];
-    __shared__ uint64_t s_blmb[MAXB / 64], s_presb[MAXB / 64];
+    __shared__ uint64_t s_blmb[MB / 64], s_presb[MB / 64];
     __shared__ uint32_t s_smark[MAX_SETS / 32];
     __shared__ int s_nd[2], s_li[2], s_kfail[2];
     Dedup T{s_key, s_wb, s_it, DEDUP_STEP, s_nd, s_li};
@@ -1312,7 +1378,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
     __shared__ int s_lkind, s_lpick;
     __shared__ uint32_t s_lpart;
     __shared__ int s_lrep[MAXR + 1];
-    __shared__ unsigned long long s_lsb[64];
+    __shared__ unsigned long long s_lsb[MB / 64];
     if (tid == 0) { s_nT = 0; s_done = 0; s_exact_need = 0; s_retry = 0; s_moved = -1; s_lkind = 0; s_memb = 0; }
     if (tid < NF) s_first[tid] = NONE32;
     if (tid < 2) { s_kc[tid] = 0; s_sok[tid] = -1; }   // (s_sok: -1 = no record offered its best key)
@@ -1606,8 +1672,12 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
                 const int nrep = (int)meta_nrep(m), set = (int)(BIG && a.pset ? a.pset[p] : meta_set(m));
                 if (wid == 0) {
                     if (lane < nrep) s_lrep[lane] = (int)a.rep[(long long)lane * a.Ppad + p];
-                    const unsigned long long sbw = lane < a.W64 ? (unsigned long long)a.setbits[(size_t)set * a.W64 + lane] : 0ull;
-                    s_lsb[lane] = sbw;
+#pragma unroll
+                    for (int q = 0; q < MB / 4096; q++) {
+                        const int wi = q * 64 + lane;
+                        const unsigned long long sbw = wi < a.W64 ? (unsigned long long)a.setbits[(size_t)set * a.W64 + wi] : 0ull;
+                        s_lsb[wi] = sbw;
+                    }
                     if (lane == 0) s_lpick = -1;
                     const unsigned long long lt = (1ull << lane) - 1ull;
                     bool done = false;
@@ -1653,7 +1723,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
                 __syncthreads();
             };
             auto su_wave = [&]() {               // (wave 0, after stage_exact)
-                const double su = exact_unbalance_wave(s_Lm, nblm0, -1, -1, 0.0, 0.0, s_fold);
+                const double su = exact_unb_w<GB>(s_Lm, nblm0, -1, -1, 0.0, 0.0, s_fold);
                 if (lane == 0) { s_sux = su; atomicAdd(&C.total_folds, 1ull); }
             };
             auto exact_su = [&]() {
@@ -1803,7 +1873,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
                     if (wid == 0) su_wave();
                     if (!fail && ndist == 1) {
                         if (wid == 1) {
-                            const double u = exact_unbalance_wave(s_Lm, nblm0, (int)ld32(a.posm + cw.s), (int)ld32(a.posm + cw.t),
+                            const double u = exact_unb_w<GB>(s_Lm, nblm0, (int)ld32(a.posm + cw.s), (int)ld32(a.posm + cw.t),
                                                                   s_ld[cw.s] - cw.w, s_ld[cw.t] + cw.w, s_fold + 64);
                             if (lane == 0) { s_dv[0] = u; atomicAdd(&C.total_folds, 1ull); }
                         }
@@ -1827,7 +1897,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
                             if (wid > 0)
                                 for (int i = wid - 1; i < ncl; i += NW - 1) {
                                     const Contender c = dedup_entry(T, (int)s_cl[i]);
-                                    const double u = exact_unbalance_wave(s_Lm, nblm0, (int)s_cps[i], (int)s_cpt[i],
+                                    const double u = exact_unb_w<GB>(s_Lm, nblm0, (int)s_cps[i], (int)s_cpt[i],
                                                                           s_ld[c.s] - c.w, s_ld[c.t] + c.w, s_fold + 64 * wid);
                                     if (lane == 0) nf++;
                                     better(u, c);
@@ -1838,7 +1908,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
                                 for (int h = wid - 1; h < DEDUP_STEP; h += NW - 1) {
                                     if (!(s_key[h] != NONE32 && (int)(s_key[h] >> 30) == kind)) continue;
                                     const Contender c = dedup_entry(T, h);
-                                    const double u = exact_unbalance_wave(s_Lm, nblm0, (int)ld32(a.posm + c.s), (int)ld32(a.posm + c.t),
+                                    const double u = exact_unb_w<GB>(s_Lm, nblm0, (int)ld32(a.posm + c.s), (int)ld32(a.posm + c.t),
                                                                           s_ld[c.s] - c.w, s_ld[c.t] + c.w, s_fold + 64 * wid);
                                     if (lane == 0) nf++;
                                     better(u, c);
@@ -2186,7 +2256,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
 #endif
     const int nT = s_nT;
     bool marked = false;                              // (unused: the fused path returns itself)
-    if (!full && a.sb_lds) {
+    if (!GB && !full && a.sb_lds) {
         // ---- fused incremental prep, wave-specialised.  A wave reduction of a double
         // costs ~340 clocks when all 16 waves run one (four per SIMD, issue-bound) and
         // ~100 when one wave per SIMD does (tools/lat_probe.hip), while a workgroup
@@ -2681,9 +2751,9 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
         }
         __syncthreads();
         // per untouched element: new position = old - (touched before it) + (touched keys below it)
-        int nb[(MAXB + STEP_THREADS - 1) / STEP_THREADS], np[(MAXB + STEP_THREADS - 1) / STEP_THREADS];
+        int nb[(MB + STEP_THREADS - 1) / STEP_THREADS], np[(MB + STEP_THREADS - 1) / STEP_THREADS];
 #pragma unroll
-        for (int q = 0; q < (MAXB + STEP_THREADS - 1) / STEP_THREADS; q++) {
+        for (int q = 0; q < (MB + STEP_THREADS - 1) / STEP_THREADS; q++) {
             nb[q] = -1;
             if (q * STEP_THREADS >= B) continue;         // uniform
             const int i = q * STEP_THREADS + tid;
@@ -2707,7 +2777,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
         }
         __syncthreads();
 #pragma unroll
-        for (int q = 0; q < (MAXB + STEP_THREADS - 1) / STEP_THREADS; q++)
+        for (int q = 0; q < (MB + STEP_THREADS - 1) / STEP_THREADS; q++)
             if (nb[q] >= 0) s_ord[np[q]] = nb[q];
         if (tid < nT) {
             const int t = s_T[tid];
@@ -2724,14 +2794,15 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
     __syncthreads();
     KB_STAMP(ctl, 6);
     // bl_move = brokers present in the load map or listed in -broker-ids (steps.go:150-157)
-    for (int w = tid; w < MAXB / 64; w += STEP_THREADS) { s_blmb[w] = 0; s_presb[w] = 0; }
+    for (int w = tid; w < MB / 64; w += STEP_THREADS) { s_blmb[w] = 0; s_presb[w] = 0; }
     if (tid == 0) s_unc = 0;
     __syncthreads();
     {
-        int flag[4], c = 0;
-        const int base = tid * 4;
+        constexpr int FQ = MB / STEP_THREADS;           // universe positions per thread
+        int flag[FQ], c = 0;
+        const int base = tid * FQ;
 #pragma unroll
-        for (int q = 0; q < 4; q++) {
+        for (int q = 0; q < FQ; q++) {
             const int i = base + q;
             flag[q] = 0;
             if (i < B) {
@@ -2762,7 +2833,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
         const int woff = wave_sum(lane < wid ? wc : 0), total = wave_sum(wc);
         int pos = woff + incl - c;
 #pragma unroll
-        for (int q = 0; q < 4; q++) {
+        for (int q = 0; q < FQ; q++) {
             const int i = base + q;
             if (i < B) {
                 const int b = s_ord[i];
@@ -2940,7 +3011,11 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
         int* s_mlist = (int*)s_it;                         // [CH]
         __shared__ int s_mn, s_cursor;
         const int W64 = a.W64, KR = a.KR;
-        const int CH = a.sb_lds ? 2 * DEDUP_STEP : DEDUP_STEP / W64;   // >= 32
+        // (past MAXB brokers the words are read from memory where they lie: a staged chunk
+        // of DEDUP_STEP / W64 < 32 sets could not take a whole mark word, the compaction
+        // below needs room for 32)
+        const bool stage = !GB && !a.sb_lds;
+        const int CH = stage ? DEDUP_STEP / W64 : 2 * DEDUP_STEP;   // >= 32
         const int nwords = (a.nsets + 31) / 32;
         const unsigned long long lt = (1ull << lane) - 1ull;
         // each wave builds its records in LDS, then writes them as whole 16-B units
@@ -2990,7 +3065,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
             KB_STAMP(ctl, 19);
             if (bigm && tid == 0) s_cursor = c0 + bn;      // (every thread has read the old cursor)
             const int mn = s_mn;
-            if (!a.sb_lds) {
+            if (stage) {
                 for (int q = tid; q < mn * W64; q += STEP_THREADS) {
                     const int i = q / W64, wd = q - i * W64;
                     s_stage[q] = a.setbits[(size_t)s_mlist[i] * W64 + wd];
@@ -3006,7 +3081,8 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
                 for (int j = 0; j < G; j++) {
                     const int jj = j < ng ? j : 0;
                     const int set = s_mlist[g + jj];
-                    sb[j] = a.sb_lds ? s_sb + (size_t)set * W64 : s_stage + (size_t)(g + jj) * W64;
+                    sb[j] = a.sb_lds ? s_sb + (size_t)set * W64
+                                     : (GB ? a.setbits + (size_t)set * W64 : s_stage + (size_t)(g + jj) * W64);
                     rec16[j] = &s_rs[wid][j][0];
                     found[j] = j < ng ? 0 : KR;
                 }
@@ -3057,7 +3133,12 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
                     if (j >= ng) break;
                     for (int rk = found[j] + lane; rk < KR; rk += 64) rec16[j][2 + rk] = NONE16;
                     if (lane == 0) rec16[j][1] = (uint16_t)(found[j] < KR ? found[j] : KR);
-                    int n = lane < W64 ? (int)__popcll(sb[j][lane] & s_blmb[lane]) : 0;
+                    int n = 0;
+#pragma unroll
+                    for (int q = 0; q < MB / 4096; q++) {
+                        const int wi = q * 64 + lane;
+                        n += wi < W64 ? (int)__popcll(sb[j][wi] & s_blmb[wi]) : 0;
+                    }
                     n = wave_sum(n);
                     if (lane == 0) rec16[j][0] = (uint16_t)n;
                 }
@@ -3080,10 +3161,10 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
 
 // (BIG: more broker lists than the meta word's set field / the LDS mark bitmap hold --
 // a separate instantiation, so the common kernel's register allocation is untouched)
-template <bool BIG>
+template <bool BIG, bool GB = false>
 __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
     __shared__ DevCtl C;
-    step_body<BIG>(a, C);
+    step_body<BIG, GB>(a, C);
 }
 
 // ------------------------------------------------------------- k_listop
@@ -3357,8 +3438,10 @@ __global__ __launch_bounds__(1024) void k_summary(SumArgs a) {
 template <int RC>
 static void launch_scan_rc(const ScanArgs& a, bool lds_sets, size_t lds, hipStream_t st) {
     const int grid = a.nscan + (a.listwg ? 1 : 0) + a.eager;
-    // (incremental mode: with the set records in LDS only; engine.cpp gates it)
-    if (lds_sets && a.incr) hipLaunchKernelGGL((k_scan<RC, true, true>), dim3(grid), dim3(SCAN_THREADS), lds, st, a);
+    // (incremental mode: with the set records in LDS only; engine.cpp gates it.  Broker
+    // tables in memory (a.gt, B > MAXB): set records in memory too)
+    if (a.gt) hipLaunchKernelGGL((k_scan<RC, false, false, true>), dim3(grid), dim3(SCAN_THREADS), lds, st, a);
+    else if (lds_sets && a.incr) hipLaunchKernelGGL((k_scan<RC, true, true>), dim3(grid), dim3(SCAN_THREADS), lds, st, a);
     else if (lds_sets) hipLaunchKernelGGL((k_scan<RC, true, false>), dim3(grid), dim3(SCAN_THREADS), lds, st, a);
     else hipLaunchKernelGGL((k_scan<RC, false, false>), dim3(grid), dim3(SCAN_THREADS), lds, st, a);
 }
@@ -3376,10 +3459,11 @@ void launch_scan(const ScanArgs& a, int rc, bool lds_sets, size_t lds, hipStream
     }
 }
 template <int RC>
-static int scan_occ_rc(bool lds_sets, size_t lds) {
+static int scan_occ_rc(bool lds_sets, bool gt, size_t lds) {
     int n = 0;
     int m = 0;
-    if (lds_sets) {
+    if (gt) hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_scan<RC, false, false, true>, SCAN_THREADS, lds);
+    else if (lds_sets) {
         hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_scan<RC, true, false>, SCAN_THREADS, lds);
         hipOccupancyMaxActiveBlocksPerMultiprocessor(&m, k_scan<RC, true, true>, SCAN_THREADS, lds);
         n = n < m ? n : m;
@@ -3387,16 +3471,16 @@ static int scan_occ_rc(bool lds_sets, size_t lds) {
     return n;
 }
 
-int scan_blocks_per_cu(int rc, bool lds_sets, size_t lds) {
+int scan_blocks_per_cu(int rc, bool lds_sets, bool gt, size_t lds) {
     switch (rc) {
-        case 1: return scan_occ_rc<1>(lds_sets, lds);
-        case 2: return scan_occ_rc<2>(lds_sets, lds);
-        case 3: return scan_occ_rc<3>(lds_sets, lds);
-        case 4: return scan_occ_rc<4>(lds_sets, lds);
-        case 6: return scan_occ_rc<6>(lds_sets, lds);
-        case 8: return scan_occ_rc<8>(lds_sets, lds);
-        case 12: return scan_occ_rc<12>(lds_sets, lds);
-        default: return scan_occ_rc<16>(lds_sets, lds);
+        case 1: return scan_occ_rc<1>(lds_sets, gt, lds);
+        case 2: return scan_occ_rc<2>(lds_sets, gt, lds);
+        case 3: return scan_occ_rc<3>(lds_sets, gt, lds);
+        case 4: return scan_occ_rc<4>(lds_sets, gt, lds);
+        case 6: return scan_occ_rc<6>(lds_sets, gt, lds);
+        case 8: return scan_occ_rc<8>(lds_sets, gt, lds);
+        case 12: return scan_occ_rc<12>(lds_sets, gt, lds);
+        default: return scan_occ_rc<16>(lds_sets, gt, lds);
     }
 }
 
@@ -3455,15 +3539,20 @@ void launch_touch(double* r, int B, int32_t* blm, int32_t* posm, uint4* setrec, 
     hipLaunchKernelGGL(k_touch, dim3(1), dim3(1024), 0, st, r, B, blm, posm, setrec, nrec);
 }
 
-int step_static_lds() {
+int step_static_lds(bool gb) {
     hipFuncAttributes fa, fb;
-    if (hipFuncGetAttributes(&fa, (const void*)k_step<false>) != hipSuccess) return -1;
-    if (hipFuncGetAttributes(&fb, (const void*)k_step<true>) != hipSuccess) return -1;
+    if (hipFuncGetAttributes(&fa, gb ? (const void*)k_step<false, true> : (const void*)k_step<false>) != hipSuccess) return -1;
+    if (hipFuncGetAttributes(&fb, gb ? (const void*)k_step<true, true> : (const void*)k_step<true>) != hipSuccess) return -1;
     return (int)(fa.sharedSizeBytes > fb.sharedSizeBytes ? fa.sharedSizeBytes : fb.sharedSizeBytes);
 }
 
 void launch_step(const StepArgs& a, hipStream_t st) {
-    if (a.pset && a.nsets > (int)MAX_SETS)
+    if (a.gscr) {
+        if (a.pset && a.nsets > (int)MAX_SETS)
+            hipLaunchKernelGGL((k_step<true, true>), dim3(1), dim3(STEP_THREADS), a.lds_bytes, st, a);
+        else
+            hipLaunchKernelGGL((k_step<false, true>), dim3(1), dim3(STEP_THREADS), a.lds_bytes, st, a);
+    } else if (a.pset && a.nsets > (int)MAX_SETS)
         hipLaunchKernelGGL(k_step<true>, dim3(1), dim3(STEP_THREADS), a.lds_bytes, st, a);
     else
         hipLaunchKernelGGL(k_step<false>, dim3(1), dim3(STEP_THREADS), a.lds_bytes, st, a);

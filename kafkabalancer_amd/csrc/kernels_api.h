@@ -63,6 +63,7 @@ struct ScanArgs {
     const uint32_t* pset;     // [Ppad] allowed-set index per partition (set records in memory only)
     int eager;                // > 0: that many extra workgroups after the list workgroup refold the
                               //    last applied step's touched brokers (DevCtl.eg_*)
+    int gt;                   // 1: the broker tables are read from memory (B > MAXB; k_scan<.., GT>)
 };
 
 struct StepArgs {
@@ -106,6 +107,8 @@ struct StepArgs {
                               //    (rfpass): resume with a full prep
     int eager;                // 1: leave the touched brokers (and their list edit) to the next
                               //    scan's eager refolds (ScanArgs.eager)
+    unsigned char* gscr;      // non-null (B > MAXB): k_step's per-broker tables live in this
+                              //    memory scratch (step_lds(B, NP2, 0) layout) instead of LDS
 };
 
 
@@ -120,9 +123,9 @@ struct SumArgs {
 };
 
 void launch_scan(const ScanArgs& a, int rc, bool lds_sets, size_t lds_bytes, hipStream_t st);
-int scan_blocks_per_cu(int rc, bool lds_sets, size_t lds_bytes);
+int scan_blocks_per_cu(int rc, bool lds_sets, bool gt, size_t lds_bytes);
 void launch_step(const StepArgs& a, hipStream_t st);
-int step_static_lds();
+int step_static_lds(bool gb);
 // diagnostic: one workgroup rewrites the given tables in place (n = 0: nothing)
 void launch_ubinit(DevCtl* ctl, const Recs& R, int allow_leader, hipStream_t st);
 void launch_touch(double* r, int B, int32_t* blm, int32_t* posm, uint4* setrec, int nrec, hipStream_t st);

@@ -2,7 +2,11 @@
 
 SURVEY.md 8d: broker ids 1..B, topic "t%05d" with 100 partitions each, weights
 absent (-> 1.0) or Zipf-like w = r^-1.1 with r uniform in [1, 1e6], allowed
-sets drawn per partition.  Deterministic for a seed (numpy PCG64).
+sets drawn per partition.  Deterministic for a seed.  SURVEY 8d named splitmix64;
+the generator is numpy's PCG64 instead (vectorised draws for 10M partitions): no
+reference-run numbers exist for these inputs, so the stream only has to be fixed and
+reproducible -- the golden fixtures regenerate from it bit-identically
+(tests/test_golden_scale.py).
 Returns (ClusterSoA, cfg dict, description).
 """
 import numpy as np
@@ -28,10 +32,6 @@ def _distinct(rng, n_choices, count, rf):
 def _zipf_weights(rng, n):
     r = rng.uniform(1.0, 1e6, size=n)
     return r ** -1.1
-
-
-def _topics(n):
-    return None  # topic names are generated lazily by topic_names() when needed
 
 
 def topic_names(n):

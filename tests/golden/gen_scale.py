@@ -81,12 +81,24 @@ CASES = {
                   dict(O.default_cfg(), min_unbalance=0.0), 40),
     # BASELINE.json configs[4] at full size: 10M partitions x 4096 brokers, the first steps
     "c5_full": (dict(config="c5", scale=1.0), None, 12),
+    # past the 4096 brokers the kernels keep in LDS (broker tables in memory): auto lists
+    # with Zipf weights (eager refolds, exact folds), allowed sets with -allow-leader, the
+    # integral mode at the engine's 16384-broker limit, and the uniform exact-tie case
+    # (b8000_sets without -allow-leader: with it, the leader 2-cycle of SURVEY 3.4 repeats)
+    "b6000_zipf": (dict(P=30000, B=6000, rf=3, weights="zipf", seed=0x5EED6000),
+                   dict(O.default_cfg(), min_unbalance=0.0), 40),
+    "b8000_sets": (dict(P=30000, B=8000, rf=3, weights="zipf", nsets=200, set_size=64, seed=0x5EED8000),
+                   dict(O.default_cfg(), min_unbalance=0.0), 60),
+    "b16384_int": (dict(P=60000, B=16384, rf=3, weights="int", seed=0x5EED4000),
+                   dict(O.default_cfg(), min_unbalance=0.0), 30),
+    "b12000_uniform": (dict(P=40000, B=12000, rf=3, weights="uniform", seed=0x5EEDC000),
+                       dict(O.default_cfg(), min_unbalance=0.0), 12),
 }
 
 # cases generated with the oracle's windowed exact move() (or_set_window: the literal
 # loop's result, tests/test_oracle.py::test_windowed_oracle_*; the literal loop would take
 # hours to days per step at these sizes)
-WINDOWED = {"c3nl_full", "b4096_50k", "c5_full"}
+WINDOWED = {"c3nl_full", "b4096_50k", "c5_full", "b6000_zipf", "b8000_sets", "b16384_int", "b12000_uniform"}
 
 
 def build(params):

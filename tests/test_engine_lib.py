@@ -43,3 +43,16 @@ def test_product_does_not_reference_oracle():
                 with open(os.path.join(dp, fn), errors="ignore") as f:
                     txt = f.read()
                 assert "oracle" not in txt.lower().replace("oracle_free", ""), os.path.join(dp, fn)
+
+
+def test_broker_universe_limit():
+    """Up to MAXB_G = 16384 distinct broker ids (past 4096 the kernels read the broker tables
+    from memory); one more is an explicit KB_ERR_UNSUPPORTED, checked before any device call."""
+    import pytest
+    from kafkabalancer_amd import synth
+    cl = synth.make_cluster(10, 40, 3, "int", seed=1)
+    cfg = {"allow_leader": False, "rebalance_leaders": False, "min_replicas": 2, "min_unbalance": 0.0,
+           "brokers": list(range(1, 16386))}
+    with pytest.raises(E.EngineError) as ei:
+        E.Engine(cl, cfg)
+    assert ei.value.code == -3 and "16384 distinct brokers" in str(ei.value)   # KB_ERR_UNSUPPORTED

@@ -217,6 +217,21 @@ def test_many_brokers_sorting():
     check_plan(pl, cfg, 2)
 
 
+def test_broker_tables_in_memory_literal_oracle():
+    """Past the 4096 brokers the kernels keep in LDS the broker tables live in memory
+    (k_scan's GT and k_step's GB instantiations): 5000 listed brokers, tiny P for the
+    literal oracle loop (threaded; the scale_b6000 / b8000 / b12000 / b16384 fixtures of
+    test_golden_scale.py cover the larger cases)."""
+    cl = synth.make_cluster(60, 5000, 3, "int", seed=7, with_names=True, broker_hi=5000)
+    cfg = default_cfg(min_unbalance=0.0, brokers=list(range(1, 5001)))
+    pl = synth.to_plist(cl)
+    O.set_threads(min(16, os.cpu_count() or 1))
+    try:
+        check_plan(pl, cfg, 3)
+    finally:
+        O.set_threads(1)
+
+
 # ------------------------------------------ full-size properties (c3 size)
 
 def test_full_size_properties():
