@@ -146,6 +146,7 @@ typedef struct {
                                        (kb_engine_set_incremental, ABI 6) */
     int64_t relists;                /* per-broker partition lists laid out again after one ran
                                        out of slack (kb_config.list_slack, ABI 8) */
+    int64_t fused_pairs;            /* 1: a plan's scan + step run as one launch (k_pair, ABI 8) */
 } kb_stats;
 
 typedef struct kb_engine kb_engine;

@@ -92,6 +92,9 @@ struct kb_engine {
     int32_t* bset_off = nullptr;
     int32_t* bset_ids = nullptr;
     unsigned char* gscr = nullptr;    // k_step's per-broker tables past MAXB brokers (StepArgs.gscr)
+    uint32_t* pair_cnt = nullptr;     // k_pair's arrival count (ScanArgs.done / StepArgs.wait_cnt)
+    bool fuse = false;                // pairs run as one k_pair launch (scan grid + step workgroup)
+    size_t pair_lds = 0;              // k_pair's dynamic LDS: max(scan, step)
     bool gb = false;                  // B > MAXB: broker tables in memory (k_scan GT, k_step GB)
     unsigned char* recs = nullptr;
     Contender* cont = nullptr;
@@ -543,6 +546,22 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
         e->step_lds_bytes = e->gb ? 0 : step_lds((int)e->B, e->NP2, e->sb_lds ? sbw : 0).total;
         if (st_lds + e->step_lds_bytes > lim) { e->last_err = "too many brokers for k_step's LDS"; *out = e; return KB_ERR_UNSUPPORTED; }
     }
+    {
+        // fused pairs (k_pair): the scan's grid plus one resident step workgroup, which then
+        // takes a scan workgroup's slot; the scan keeps its kernel for the bound passes, the
+        // incremental mode and the multi-GPU summaries
+        const bool full_shard = e->shard_begin == 0 && e->shard_end == n;
+        e->fuse = !e->gb && pair_supported(e->rc_dev) && e->nsets <= (int64_t)MAX_SETS &&
+                  full_shard && e->nscan > 1;
+        if (const char* v = getenv("KB_FUSE")) e->fuse = e->fuse && *v != '0';                      // A/B
+        if (e->fuse) {
+            e->pair_lds = std::max(e->scan_lds, (size_t)e->step_lds_bytes);
+            int pst = 0;
+            const int pcu = pair_blocks_per_cu(e->rc_dev, e->lds_sets, e->pair_lds, &pst);
+            if (pcu < 1 || pst + e->pair_lds > 160 * 1024) e->fuse = false;
+            else e->nscan = std::min<int64_t>(e->ntiles, std::max<int64_t>(1, (int64_t)pcu * ncu - (e->eager ? EGW + 1 : 0) - 1));
+        }
+    }
     HIPCHK(hipStreamCreateWithFlags(&e->st, hipStreamNonBlocking));
     e->own_st = true;
     HIPCHK(dalloc(&e->w, e->Ppad));
@@ -553,6 +572,8 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
     HIPCHK(dalloc(&e->load, e->B + 2));
     HIPCHK(dalloc(&e->lerr, e->B));
     if (e->gb) HIPCHK(dalloc(&e->gscr, (size_t)step_lds((int)e->B, e->NP2, 0).total));
+    HIPCHK(dalloc(&e->pair_cnt, PAIR_SHARDS * PAIR_STRIDE));
+    HIPCHK(hipMemset(e->pair_cnt, 0, PAIR_SHARDS * PAIR_STRIDE * 4));
     HIPCHK(dalloc(&e->eb, e->B + 2));
     HIPCHK(dalloc(&e->bfl, e->B + 16));
     HIPCHK(dalloc(&e->cnt, e->B));
@@ -683,6 +704,7 @@ static void fill_scan_args(kb_engine* e, ScanArgs& s) {
     s.rf = e->rf_dev;
     s.eager = e->eager && e->nscan > 0 ? EGW : 0;
     s.gt = e->gb ? 1 : 0;
+    s.done = e->pair_cnt;
 }
 
 static void fill_step_args(kb_engine* e, StepArgs& a, const Recs& R, int use_spill) {
@@ -691,6 +713,7 @@ static void fill_step_args(kb_engine* e, StepArgs& a, const Recs& R, int use_spi
     a.nsets = (int)e->nsets; a.NP2 = e->NP2;
     a.sb_lds = e->sb_lds; a.lds_bytes = e->step_lds_bytes;
     a.gscr = e->gscr;
+    a.wait_cnt = e->pair_cnt; a.wait_n = 0;
     a.setbits = e->setbits; a.setrec = e->setrec;
     a.order = e->order; a.posu = e->posu; a.blm = e->blm; a.posm = e->posm; a.r = e->r;
     a.load = e->load; a.lerr = e->lerr; a.eb = e->eb; a.bfl = e->bfl; a.cnt = e->cnt;
@@ -785,6 +808,19 @@ static void enqueue_step(kb_engine* e, bool rf = false) {
 // (rf: this pair may follow a step halted for exact loads: the pair's first scan launch
 // refolds the loads and its k_step resumes; rf_scan: the main scan is that first launch)
 static void enqueue_pair(kb_engine* e, bool rf = false, bool rf_scan = false) {
+    if (e->fuse && !e->incr) {
+        // one launch: the scan's grid and the step workgroup (k_pair)
+        mark(e, TK_SCAN);
+        ScanArgs s;
+        fill_scan_args(e, s);
+        s.rfpass = rf && rf_scan && e->rf_stream;
+        StepArgs a;
+        fill_step_args(e, a, scan_recs(e->recs, (int)e->nscan), 1);
+        a.rf_final = rf && e->rf_stream;
+        a.wait_n = s.nscan + (s.listwg ? 1 : 0) + s.eager;
+        launch_pair(s, a, e->rc_dev, e->lds_sets, e->pair_lds, e->st);
+        return;
+    }
     mark(e, TK_SCAN);
     enqueue_scan(e, rf && rf_scan);
     mark(e, TK_STEP);
@@ -941,6 +977,10 @@ static int convert(kb_engine* e, const ChangeDev& d, kb_change* o) {
                           "remove) and ValidateReplicas is not in the step mask; the engine's loads assume "
                           "distinct replicas";
             rc = KB_ERR_UNSUPPORTED;
+            break;
+        case E_PAIR_TIMEOUT:
+            e->last_err = "engine: the fused scan + step launch timed out waiting for the scan workgroups";
+            rc = KB_ERR_HIP;
             break;
         default: e->last_err = step + ": error"; break;
     }
@@ -1255,6 +1295,7 @@ extern "C" int kb_engine_stats(kb_engine* e, kb_stats* o) {
     o->spill_grows = e->spill_grows;
     o->blocks_scanned = (int64_t)c.total_blocks;
     o->relists = e->relists;
+    o->fused_pairs = e->fuse && !e->incr ? 1 : 0;
     return KB_OK;
 }
 
@@ -1461,7 +1502,7 @@ extern "C" void kb_engine_destroy(kb_engine* e) {
     if (!e) return;
     void* ptrs[] = {e->w, e->rep, e->meta, e->pset, e->nc, e->load, e->lerr, e->eb, e->bfl, e->cnt,
                     e->setbits, e->setrec, e->order, e->posu, e->blm, e->posm, e->r,
-                    e->bset_off, e->bset_ids, e->gscr, e->recs, e->cont, e->ctl, e->log, e->bdesc, e->ubdesc,
+                    e->bset_off, e->bset_ids, e->gscr, e->pair_cnt, e->recs, e->cont, e->ctl, e->log, e->bdesc, e->ubdesc,
                     e->L.lstart, e->L.llen, e->L.lcap, e->L.lent, e->rf_dev};
     for (void* p : ptrs) if (p) hipFree(p);
     if (e->h_ctl) hipHostFree(e->h_ctl);

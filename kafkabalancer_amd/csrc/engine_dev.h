@@ -35,6 +35,8 @@ constexpr int DEDUP_STEP = 2048;    // LDS key table of k_step / k_summary
 constexpr int DEDUP_SCAN = 256;     // LDS key table of one k_scan workgroup
 constexpr int TMAX = 2 * MAXR + 4;  // brokers touched by one applied change (bound)
 constexpr int EGW = 4;              // eager refold workgroups per scan launch (touched brokers)
+constexpr int PAIR_SHARDS = 8;      // k_pair's arrival count: one word per XCD group of blocks,
+constexpr int PAIR_STRIDE = 32;     // each on a 128-B line of its own
 constexpr int RF_CHUNK = 2048;       // in-stream refresh: contributions per fold chunk (two buffers)
 constexpr int RF_LDS_BYTES = 2 * RF_CHUNK * 8;
 constexpr int BLK = 128;            // partitions of one wave in a scan tile = one block of
@@ -288,7 +290,8 @@ struct DevCtl {
 enum {
     E_NONE = 0, E_DUP = 1, E_REMOVE = 2, E_ADD = 3, E_DIS = 4, E_PANIC = 5,
     E_CONT_OVERFLOW = 6, E_LIST_OVERFLOW = 7,
-    E_DUP_UNSUP = 8     // kb_engine_step without ValidateReplicas on a state holding duplicates (Go sem)
+    E_DUP_UNSUP = 8,    // kb_engine_step without ValidateReplicas on a state holding duplicates (Go sem)
+    E_PAIR_TIMEOUT = 9  // k_pair's step workgroup waited 2 s for the scan's workgroups (never expected)
 };
 
 }  // namespace kbe

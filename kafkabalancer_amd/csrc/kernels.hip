@@ -58,6 +58,22 @@ template <typename T>
 __device__ __forceinline__ T ldobj(const T* p) { return *p; }
 template <typename T>
 __device__ __forceinline__ void stobj(T* p, const T& v) { *p = v; }
+// write-through (sc1) stores of what a scan workgroup hands to k_step (records, spilled
+// keys): the line leaves the XCD's L2 at once, so k_pair's step workgroup, acquiring after
+// the workgroup's drained arrival, reads it with no L2 write-back on the producer's side
+// (MI355X_MICROARCH.md, inter-workgroup visibility; the same cost as plain stores here)
+template <typename T>
+__device__ __forceinline__ void stobj_wt(T* p, const T& v) {
+    static_assert(sizeof(T) % 8 == 0, "8-byte granules");
+    const unsigned long long* src = (const unsigned long long*)&v;
+    unsigned long long* dst = (unsigned long long*)p;
+#pragma unroll
+    for (int i = 0; i < (int)(sizeof(T) / 8); i++)
+        __hip_atomic_store(dst + i, src[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st32_wt(uint32_t* p, uint32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 // reference term (utils.go:136-143): r = L/avg - 1; r>0 ? r*r : r*r/2 (exact ops)
 __device__ __forceinline__ double term_x(double L, double avg) {
@@ -451,8 +467,8 @@ __device__ __forceinline__ uint32_t set_of(const PartRaw<RC>& P, int j) {
 
 __device__ __forceinline__ void emit_global(const ScanArgs& a, const Contender& c) {
     uint32_t i = atomicAdd(a.ncont, 1u);
-    if (i < a.cont_cap) stobj(&a.cont[i], c);
-    else st32(a.cont_ovf, 1u);
+    if (i < a.cont_cap) stobj_wt(&a.cont[i], c);
+    else st32_wt(a.cont_ovf, 1u);
 }
 
 __device__ __forceinline__ void emit(const ScanArgs& a, const Dedup& T, int kind, int s, int t, double w,
@@ -973,7 +989,7 @@ __device__ __forceinline__ void scan_round(const ScanArgs& a, const ScanParams& 
             atomicMin(&s_benc[c.kind], myenc);
             atomicAdd(&s_nkk[c.kind], 1u);
             const uint32_t k = atomicAdd(&s_nk, 1u);
-            if (k < (uint32_t)TILE_KEYS) stobj(&keys[k], c);
+            if (k < (uint32_t)TILE_KEYS) stobj_wt(&keys[k], c);
             else emit_global(a, c);
         }
     }
@@ -1010,11 +1026,11 @@ __device__ __forceinline__ void scan_round(const ScanArgs& a, const ScanParams& 
             if (s_bslot[k] != NONE32) r.best[k] = dedup_entry(T, (int)s_bslot[k]);
             else { r.best[k].s = r.best[k].t = -1; r.best[k].w = 0.0; r.best[k].iter = NONE64; r.best[k].kind = k; r.best[k].pad = 0; }
         }
-        stobj(hdr, r);
+        stobj_wt(hdr, r);
         if (fm) {
             uint32_t* fo = a.R.f(wg);
 #pragma unroll
-            for (int f = 0; f < NF; f++) st32(fo + f, fst[f]);
+            for (int f = 0; f < NF; f++) st32_wt(fo + f, fst[f]);
         }
         if (tk_on) {                           // the scan's interval (kernel timing)
             atomicMin(&ctl->ts_beg, t_in);
@@ -1028,8 +1044,8 @@ __device__ __attribute__((noinline)) void refresh_in_scan(const RefreshArgs* rfp
                                                           uint32_t part, double* buf);   // (k_refresh below)
 __device__ __attribute__((noinline)) void eager_refold(const RefreshArgs* rfp, int k, double* buf);
 
-template <int RC, bool LSETS, bool INCR, bool GT = false>
-__global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
+template <int RC, bool LSETS, bool INCR, bool GT>
+__device__ __forceinline__ void scan_kernel_body(const ScanArgs& a) {
     extern __shared__ __align__(16) unsigned char smem[];
     __shared__ int s_li;
     DevCtl* ctl = a.ctl;
@@ -1127,6 +1143,11 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
     scan_round<RC, LSETS, INCR, GT>(a, q, smem, A, TR, t_in, (int)blockIdx.x, c0);
 }
 
+template <int RC, bool LSETS, bool INCR, bool GT = false>
+__global__ __launch_bounds__(SCAN_THREADS) void k_scan(ScanArgs a) {
+    scan_kernel_body<RC, LSETS, INCR, GT>(a);
+}
+
 // --------------------------------------------------------------- k_step
 
 struct Decision {
@@ -1222,13 +1243,13 @@ constexpr int CTL_WORDS = (int)(offsetof(DevCtl, stamps) / 4);
 // The serial half of one Balance() step (k_step): stage the control block, the
 // broker tables and the allowed-set words in LDS, resolve the scan records (when
 // prepped), apply the change and prep the next step.
-template <bool BIG, bool GB>
+template <bool BIG, bool GB, bool FUSED = false>
 __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
     DevCtl* ctl = a.ctl;
     constexpr int MB = GB ? MAXB_G : MAXB;          // (GB: the per-broker tables in memory, a.gscr)
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     constexpr int NW = STEP_THREADS / 64;
-    const unsigned long long t_in = wall_clock64();
+    unsigned long long t_in = wall_clock64();       // (FUSED: reset when the scan is in)
     KB_STAMP_BEGIN();
     __shared__ unsigned long long s_span_from;      // (kernel timing: the scan's end, or 0)
     auto write_back = [&]() {
@@ -1294,21 +1315,88 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
     // words (plain loads then LDS writes: at B <= 1024 one load of each array per thread,
     // all issued before the first LDS write; measured faster than LDS-DMA of the same
     // bytes, 16.5 vs 19.9 us per k_step at c3).  The record headers come to registers.
-    const unsigned long long ts_b = ctl->ts_beg, ts_e = ctl->ts_end;   // (kernel timing, tk_on)
-    const unsigned long long ts_pe = ctl->ts_prev_end;
+    auto stage_tables = [&]() {
+        for (int b = tid; b < B; b += STEP_THREADS) {
+            s_ld[b] = a.load[b];
+            s_e[b] = a.eb[b];
+            s_fl[b] = a.bfl[b];
+            s_ord[b] = a.order[b];
+        }
+    };
+    unsigned long long ts_b, ts_e, ts_pe;
+    if constexpr (FUSED) {
+        // k_pair's step workgroup (a resident workgroup of the scan's grid): the broker tables
+        // and the allowed-set words are staged while the scan runs -- nothing changes them
+        // then but the eager refolds of the last step's touched brokers (re-read below) and an
+        // in-stream refresh (a step halted for exact loads: everything is staged again) --
+        // then it waits for every other workgroup of the grid (scan, list, eager) to finish
+        stage_tables();
+        if (a.sb_lds) {
+            const int nq = a.nsets * a.W64;
+            for (int q = 2 * tid; q < nq; q += 2 * STEP_THREADS) {
+                if (q + 1 < nq) *(uint4*)(s_sb + q) = *(const uint4*)(a.setbits + q);
+                else s_sb[q] = a.setbits[q];
+            }
+        }
+        __shared__ int s_prehalt;
+        int egb = -1;
+        if (tid < EGW) {
+            const int n = ctl->eg_n;
+            egb = tid < n ? ctl->eg_b[tid] : -1;
+        }
+        __shared__ int s_wait_to;
+        if (wid == 0) {
+            if (lane == 0) s_prehalt = ctl->halted;
+            // the arrival count is sharded over PAIR_SHARDS words (a workgroup adds to the
+            // shard of blockIdx % 8, the blocks that share an XCD: 32 arrivals per word instead
+            // of 255 serialised on one); lanes 0..7 poll one shard each.  (A bounded wait: 2 s
+            // of the 100 MHz clock, orders of magnitude past any scan -- on expiry the plan
+            // stops with an error instead of spinning on)
+            const unsigned long long t0 = wall_clock64();
+            int to = 0;
+            for (;;) {
+                const uint32_t v = lane < PAIR_SHARDS
+                    ? __hip_atomic_load(a.wait_cnt + lane * PAIR_STRIDE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+                if (wave_sum(v) >= (uint32_t)a.wait_n) break;
+                __builtin_amdgcn_s_sleep(1);
+                if (wall_clock64() - t0 > 200000000ull) { to = 1; break; }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // (the other XCDs' writes)
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (!to && lane < PAIR_SHARDS)
+                __hip_atomic_store(a.wait_cnt + lane * PAIR_STRIDE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (lane == 0) s_wait_to = to;
+        }
+        __syncthreads();
+        if (s_wait_to) {
+            if (tid == 0) {
+                ChangeDev ch;
+                ch.status = -1; ch.step = -1; ch.kind = 0; ch.slot = -1; ch.part = -1; ch.from = ch.to = -1;
+                ch.su = ch.cu = 0.0; ch.exact = 0; ch.err_code = E_PAIR_TIMEOUT; ch.err_broker = -1; ch.pad = 0;
+                const int lp = ctl->logpos;
+                if (lp < ctl->logcap) a.log[lp] = ch;
+                ctl->logpos = lp + 1;
+                ctl->halted = H_DONE;
+            }
+            return;
+        }
+        t_in = wall_clock64();
+        ts_b = ctl->ts_beg; ts_e = ctl->ts_end; ts_pe = ctl->ts_prev_end;
+        if (tid < CTL_WORDS) ((uint32_t*)&C)[tid] = ((const uint32_t*)ctl)[tid];
+        if (s_prehalt == H_NEED_EXACT) stage_tables();
+        else if (egb >= 0 && egb < B) { s_ld[egb] = a.load[egb]; s_e[egb] = a.eb[egb]; s_fl[egb] = a.bfl[egb]; }
+    } else {
+    ts_b = ctl->ts_beg; ts_e = ctl->ts_end;         // (kernel timing, tk_on)
+    ts_pe = ctl->ts_prev_end;
     if (tid < CTL_WORDS) ((uint32_t*)&C)[tid] = ((const uint32_t*)ctl)[tid];
-    for (int b = tid; b < B; b += STEP_THREADS) {
-        s_ld[b] = a.load[b];
-        s_e[b] = a.eb[b];
-        s_fl[b] = a.bfl[b];
-        s_ord[b] = a.order[b];
-    }
+    stage_tables();
     if (a.sb_lds) {
         const int nq = a.nsets * a.W64;                   // 16-B loads (the rows are contiguous)
         for (int q = 2 * tid; q < nq; q += 2 * STEP_THREADS) {
             if (q + 1 < nq) *(uint4*)(s_sb + q) = *(const uint4*)(a.setbits + q);
             else s_sb[q] = a.setbits[q];
         }
+    }
     }
     KB_STAMP(ctl, 23);
     KB_STAMP(ctl, 27);
@@ -3167,6 +3255,40 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
     step_body<BIG, GB>(a, C);
 }
 
+// One Balance() step in one launch: the scan's grid (scan, list and eager workgroups) plus
+// one resident step workgroup, the last of the grid.  Every other workgroup publishes its
+// writes (agent-scope release) and counts itself in; the step workgroup stages the broker
+// tables while the scan runs, waits for the count, and resolves, applies and preps as
+// k_step does.  Dispatch is in grid order within an XCD, so every workgroup the step
+// workgroup waits for was dispatched before it or on another XCD: no wait can starve.
+// (Replaces the k_step launch of a pair: its dispatch gap behind the scan and the staging
+// round trip leave the step's critical path.)
+template <int RC, bool LSETS>
+__global__ __launch_bounds__(SCAN_THREADS) void k_pair(ScanArgs a, StepArgs sa) {
+    static_assert(SCAN_THREADS == STEP_THREADS, "one workgroup shape for both roles");
+    if ((int)blockIdx.x == (int)gridDim.x - 1) {
+        __shared__ DevCtl C;
+        step_body<false, false, true>(sa, C);
+        return;
+    }
+    // (a scanning workgroup's hand-off is write-through stores; the list and eager workgroups
+    // and an in-stream refresh write plain and publish with an agent-scope release)
+    const bool wt = (int)blockIdx.x < a.nscan && !(a.rfpass && a.ctl->halted == H_NEED_EXACT);
+    scan_kernel_body<RC, LSETS, false, false>(a);
+    // publish (MI355X_MICROARCH.md, inter-workgroup visibility): every wave drains its stores,
+    // then one lane (after an L2 write-back where the stores were plain) counts the
+    // workgroup in
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        if (!wt) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __hip_atomic_fetch_add(a.done + (blockIdx.x % PAIR_SHARDS) * PAIR_STRIDE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
 // ------------------------------------------------------------- k_listop
 
 __global__ __launch_bounds__(1024) void k_listop(DevCtl* ctl, Lists L) {
@@ -3557,6 +3679,38 @@ void launch_step(const StepArgs& a, hipStream_t st) {
     else
         hipLaunchKernelGGL(k_step<false>, dim3(1), dim3(STEP_THREADS), a.lds_bytes, st, a);
 }
+// the fused pair (k_pair) for the device slot counts of the common replication factors
+bool pair_supported(int rc) { return rc == 3 || rc == 4; }
+
+template <int RC>
+static int pair_attr(bool lds_sets, size_t lds, int* static_lds) {
+    hipFuncAttributes fa;
+    const void* f = lds_sets ? (const void*)k_pair<RC, true> : (const void*)k_pair<RC, false>;
+    if (hipFuncGetAttributes(&fa, f) != hipSuccess) return -1;
+    *static_lds = (int)fa.sharedSizeBytes;
+    int n = 0;
+    if (lds_sets) hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_pair<RC, true>, SCAN_THREADS, lds);
+    else hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_pair<RC, false>, SCAN_THREADS, lds);
+    return n;
+}
+
+int pair_blocks_per_cu(int rc, bool lds_sets, size_t lds, int* static_lds) {
+    if (rc == 3) return pair_attr<3>(lds_sets, lds, static_lds);
+    if (rc == 4) return pair_attr<4>(lds_sets, lds, static_lds);
+    return -1;
+}
+
+void launch_pair(const ScanArgs& a, const StepArgs& sa, int rc, bool lds_sets, size_t lds, hipStream_t st) {
+    const int grid = a.nscan + (a.listwg ? 1 : 0) + a.eager + 1;
+    if (rc == 3) {
+        if (lds_sets) hipLaunchKernelGGL((k_pair<3, true>), dim3(grid), dim3(SCAN_THREADS), lds, st, a, sa);
+        else hipLaunchKernelGGL((k_pair<3, false>), dim3(grid), dim3(SCAN_THREADS), lds, st, a, sa);
+    } else {
+        if (lds_sets) hipLaunchKernelGGL((k_pair<4, true>), dim3(grid), dim3(SCAN_THREADS), lds, st, a, sa);
+        else hipLaunchKernelGGL((k_pair<4, false>), dim3(grid), dim3(SCAN_THREADS), lds, st, a, sa);
+    }
+}
+
 void launch_listop(DevCtl* ctl, const Lists& L, hipStream_t st) {
     hipLaunchKernelGGL(k_listop, dim3(1), dim3(1024), 0, st, ctl, L);
 }

@@ -64,6 +64,7 @@ struct ScanArgs {
     int eager;                // > 0: that many extra workgroups after the list workgroup refold the
                               //    last applied step's touched brokers (DevCtl.eg_*)
     int gt;                   // 1: the broker tables are read from memory (B > MAXB; k_scan<.., GT>)
+    uint32_t* done;           // k_pair: every non-step workgroup counts itself in here when done
 };
 
 struct StepArgs {
@@ -109,6 +110,8 @@ struct StepArgs {
                               //    scan's eager refolds (ScanArgs.eager)
     unsigned char* gscr;      // non-null (B > MAXB): k_step's per-broker tables live in this
                               //    memory scratch (step_lds(B, NP2, 0) layout) instead of LDS
+    uint32_t* wait_cnt;       // k_pair's step workgroup: waits until *wait_cnt == wait_n (the
+    int wait_n;               //    grid's other workgroups), then resets it
 };
 
 
@@ -125,6 +128,9 @@ struct SumArgs {
 void launch_scan(const ScanArgs& a, int rc, bool lds_sets, size_t lds_bytes, hipStream_t st);
 int scan_blocks_per_cu(int rc, bool lds_sets, bool gt, size_t lds_bytes);
 void launch_step(const StepArgs& a, hipStream_t st);
+bool pair_supported(int rc);
+int pair_blocks_per_cu(int rc, bool lds_sets, size_t lds_bytes, int* static_lds);
+void launch_pair(const ScanArgs& a, const StepArgs& sa, int rc, bool lds_sets, size_t lds_bytes, hipStream_t st);
 int step_static_lds(bool gb);
 // diagnostic: one workgroup rewrites the given tables in place (n = 0: nothing)
 void launch_ubinit(DevCtl* ctl, const Recs& R, int allow_leader, hipStream_t st);

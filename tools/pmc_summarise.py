@@ -14,12 +14,13 @@ git_head = sys.argv[4] if len(sys.argv) > 4 else None      # the tree the passes
 
 
 def kernel_key(name):
-    """k_scan = the full-scan instantiations (k_scan<RC, LSETS, false>); k_scan_bound = the
-    block-list instantiation (k_scan<RC, LSETS, true>: the conditional bound passes and the
-    incremental mode); k_step; k_ubinit."""
+    """k_scan = the full-scan instantiations (k_scan<RC, LSETS, false, GT>); k_scan_bound = the
+    block-list instantiation (k_scan<RC, LSETS, true, GT>: the conditional bound passes and the
+    incremental mode); k_pair (the fused scan + step launch); k_step; k_ubinit."""
     if "k_scan" in name:
-        return "k_scan_bound" if name.replace(" ", "").split(">")[0].endswith(",true") else "k_scan"
-    for k in ("k_step", "k_ubinit", "k_refresh", "k_summary"):
+        params = name.replace(" ", "").split("<", 1)[-1].split(">")[0].split(",")
+        return "k_scan_bound" if len(params) > 2 and params[2] == "true" else "k_scan"
+    for k in ("k_pair", "k_step", "k_ubinit", "k_refresh", "k_summary"):
         if k in name:
             return k
     return None
