@@ -559,7 +559,10 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
             int pst = 0;
             const int pcu = pair_blocks_per_cu(e->rc_dev, e->lds_sets, e->pair_lds, &pst);
             if (pcu < 1 || pst + e->pair_lds > 160 * 1024) e->fuse = false;
-            else e->nscan = std::min<int64_t>(e->ntiles, std::max<int64_t>(1, (int64_t)pcu * ncu - (e->eager ? EGW + 1 : 0) - 1));
+            // (every workgroup of the grid resident at once: the scan's, the list workgroup, the
+            // eager ones and the step workgroup)
+            else e->nscan = std::min<int64_t>(e->ntiles, std::max<int64_t>(1, (int64_t)pcu * ncu -
+                                              (e->eager ? EGW + 1 : (e->integral ? 0 : 1)) - 1));
         }
     }
     HIPCHK(hipStreamCreateWithFlags(&e->st, hipStreamNonBlocking));
