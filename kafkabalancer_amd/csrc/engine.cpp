@@ -94,6 +94,7 @@ struct kb_engine {
     unsigned char* gscr = nullptr;    // k_step's per-broker tables past MAXB brokers (StepArgs.gscr)
     uint32_t* pair_cnt = nullptr;     // k_pair's arrival count (ScanArgs.done / StepArgs.wait_cnt)
     bool fuse = false;                // pairs run as one k_pair launch (scan grid + step workgroup)
+    int fuse_pre = 1;                 // k_pair stages the tables before its wait (KB_FUSE_PRE=0: after)
     size_t pair_lds = 0;              // k_pair's dynamic LDS: max(scan, step)
     bool gb = false;                  // B > MAXB: broker tables in memory (k_scan GT, k_step GB)
     unsigned char* recs = nullptr;
@@ -554,6 +555,7 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
         e->fuse = !e->gb && pair_supported(e->rc_dev) && e->nsets <= (int64_t)MAX_SETS &&
                   full_shard && e->nscan > 1;
         if (const char* v = getenv("KB_FUSE")) e->fuse = e->fuse && *v != '0';                      // A/B
+        if (const char* v = getenv("KB_FUSE_PRE")) e->fuse_pre = *v != '0';                          // diagnostic
         if (e->fuse) {
             e->pair_lds = std::max(e->scan_lds, (size_t)e->step_lds_bytes);
             int pst = 0;
@@ -716,7 +718,7 @@ static void fill_step_args(kb_engine* e, StepArgs& a, const Recs& R, int use_spi
     a.nsets = (int)e->nsets; a.NP2 = e->NP2;
     a.sb_lds = e->sb_lds; a.lds_bytes = e->step_lds_bytes;
     a.gscr = e->gscr;
-    a.wait_cnt = e->pair_cnt; a.wait_n = 0;
+    a.wait_cnt = e->pair_cnt; a.wait_n = 0; a.fuse_pre = 1;
     a.setbits = e->setbits; a.setrec = e->setrec;
     a.order = e->order; a.posu = e->posu; a.blm = e->blm; a.posm = e->posm; a.r = e->r;
     a.load = e->load; a.lerr = e->lerr; a.eb = e->eb; a.bfl = e->bfl; a.cnt = e->cnt;
@@ -821,6 +823,7 @@ static void enqueue_pair(kb_engine* e, bool rf = false, bool rf_scan = false) {
         fill_step_args(e, a, scan_recs(e->recs, (int)e->nscan), 1);
         a.rf_final = rf && e->rf_stream;
         a.wait_n = s.nscan + (s.listwg ? 1 : 0) + s.eager;
+        a.fuse_pre = e->fuse_pre;
         launch_pair(s, a, e->rc_dev, e->lds_sets, e->pair_lds, e->st);
         return;
     }

@@ -1041,7 +1041,7 @@ __device__ __forceinline__ void scan_round(const ScanArgs& a, const ScanParams& 
 }
 
 __device__ __attribute__((noinline)) void refresh_in_scan(const RefreshArgs* rfp, int pend, int kind, int from, int to,
-                                                          uint32_t part, double* buf);   // (k_refresh below)
+                                                          uint32_t part, double* buf, int ng);   // (k_refresh below)
 __device__ __attribute__((noinline)) void eager_refold(const RefreshArgs* rfp, int k, double* buf);
 
 template <int RC, bool LSETS, bool INCR, bool GT>
@@ -1058,8 +1058,10 @@ __device__ __forceinline__ void scan_kernel_body(const ScanArgs& a) {
     // (rfpass: if the last k_step halted for exact loads, this launch is the refresh,
     // refresh_in_scan; the scanning workgroups decide with their control words below)
     auto rf_run = [&]() {
+        // (the workgroups that share the refolds: the scan's and the list workgroup -- not the
+        // eager workgroups, which return at once on a halted step, nor k_pair's step workgroup)
         refresh_in_scan(a.rf, ctl->pending_list, ctl->pl_kind, ctl->pl_from, ctl->pl_to, (uint32_t)ctl->pl_part,
-                        (double*)smem);
+                        (double*)smem, a.nscan + (a.listwg ? 1 : 0));
     };
     if (a.listwg && (int)blockIdx.x == a.nscan) {
         // (the pending list edit of a step halted for exact loads waits for its refresh)
@@ -1330,7 +1332,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
         // then but the eager refolds of the last step's touched brokers (re-read below) and an
         // in-stream refresh (a step halted for exact loads: everything is staged again) --
         // then it waits for every other workgroup of the grid (scan, list, eager) to finish
-        stage_tables();
+        if (a.fuse_pre) stage_tables();
         if (a.sb_lds) {
             const int nq = a.nsets * a.W64;
             for (int q = 2 * tid; q < nq; q += 2 * STEP_THREADS) {
@@ -1383,7 +1385,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
         t_in = wall_clock64();
         ts_b = ctl->ts_beg; ts_e = ctl->ts_end; ts_pe = ctl->ts_prev_end;
         if (tid < CTL_WORDS) ((uint32_t*)&C)[tid] = ((const uint32_t*)ctl)[tid];
-        if (s_prehalt == H_NEED_EXACT) stage_tables();
+        if (s_prehalt == H_NEED_EXACT || !a.fuse_pre) stage_tables();
         else if (egb >= 0 && egb < B) { s_ld[egb] = a.load[egb]; s_e[egb] = a.eb[egb]; s_fl[egb] = a.bfl[egb]; }
     } else {
     ts_b = ctl->ts_beg; ts_e = ctl->ts_end;         // (kernel timing, tk_on)
@@ -3371,13 +3373,13 @@ __global__ __launch_bounds__(REFRESH_THREADS) void k_refresh(RefreshArgs a) {
 // arguments come from device memory, not the kernel-argument struct: a by-value copy
 // passed to this call would give every scan wave a stack frame.)
 __device__ __attribute__((noinline)) void refresh_in_scan(const RefreshArgs* rfp, int pend, int kind, int from, int to,
-                                                          uint32_t part, double* buf) {
+                                                          uint32_t part, double* buf, int ng) {
     const RefreshArgs rf = *rfp;
     // (a list that overflowed earlier: the host relists and refreshes; k_step leaves the
     // halt to it, StepArgs.rf_final)
     if (rf.ctl->list_overflow) return;
     __shared__ int s_i;
-    const int g = blockIdx.x, ng = gridDim.x;
+    const int g = blockIdx.x;
     const bool ef = pend && kind != 3 && from >= 0, et = pend && kind != 2 && to >= 0;
     bool ok = true;                       // (workgroup-uniform: list_insert reads llen / lcap)
     if (g == 0 && pend) {

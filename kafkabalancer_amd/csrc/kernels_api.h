@@ -112,6 +112,7 @@ struct StepArgs {
                               //    memory scratch (step_lds(B, NP2, 0) layout) instead of LDS
     uint32_t* wait_cnt;       // k_pair's step workgroup: waits until *wait_cnt == wait_n (the
     int wait_n;               //    grid's other workgroups), then resets it
+    int fuse_pre;             // k_pair: stage the broker tables before the wait (diagnostic 0: after)
 };
 
 
