@@ -552,8 +552,11 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
         // takes a scan workgroup's slot; the scan keeps its kernel for the bound passes, the
         // incremental mode and the multi-GPU summaries
         const bool full_shard = e->shard_begin == 0 && e->shard_end == n;
+        // (small shards -- scan tiles of fewer than 16 scoring waves, c2's 10k partitions --
+        // keep two launches: there the hand-off measured slower than the launch boundary,
+        // 0.0427 vs 0.0389 ms/step at c2, profiles/r04_c)
         e->fuse = !e->gb && pair_supported(e->rc_dev) && e->nsets <= (int64_t)MAX_SETS &&
-                  full_shard && e->nscan > 1;
+                  full_shard && e->nscan > 1 && e->twaves == SCAN_THREADS / 64;
         if (const char* v = getenv("KB_FUSE")) e->fuse = e->fuse && *v != '0';                      // A/B
         if (const char* v = getenv("KB_FUSE_PRE")) e->fuse_pre = *v != '0';                          // diagnostic
         if (e->fuse) {
