@@ -449,8 +449,16 @@ def main():
     fused = bool(st1.get("fused_pairs")) and not incr
     kname = "k_pair" if fused else "k_scan"
     scan_phase_us = scan_us
-    if fused and kdc.get("step", (0, 0))[1]:
-        scan_us = scan_us + kdc["step"][0]
+    pair_timing = None
+    if fused:
+        if kdc.get("step", (0, 0))[1] and kdc.get("scan", (0, 0))[1]:
+            scan_us = kdc["scan"][0] + kdc["step"][0]
+            pair_timing = "spans"
+        elif kdc.get("pair", (0, 0))[1]:
+            # (no back-to-back spans -- c5's bound passes sit between the launches: the launch
+            # from its first workgroup's start to the step workgroup's end, dispatch excluded)
+            scan_us = kdc["pair"][0]
+            pair_timing = "first workgroup start .. step end"
         achieved = bytes_scan / (scan_us * 1e-6) / 1e9
     traffic, traffic_git = (None, None) if incr else pmc_traffic(args.workload, kname)
     roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -462,9 +470,11 @@ def main():
                                      "descriptor); the full scan reads %d" % st1["scan_bytes"]
                                      if incr else ""),
             "avg_launch_us": scan_us,
-            "timing": ("device clock (100 MHz), in-plan launches back to back: the previous launch's end "
-                       "to the step workgroup's end (dispatch included, the interval rocprofv3 "
-                       "--kernel-trace reports), %d launches" % scan_n) if fused else
+            "timing": (("device clock (100 MHz), in-plan launches back to back: the previous launch's end "
+                        "to the step workgroup's end (dispatch included, the interval rocprofv3 "
+                        "--kernel-trace reports), %d launches" % scan_n) if pair_timing == "spans" else
+                       ("device clock (100 MHz): k_pair's first workgroup start to its step workgroup's "
+                        "end (dispatch excluded: no back-to-back launches), %d launches" % kdc["pair"][1])) if fused else
                       ("device clock (100 MHz), in-plan launches back to back: the previous k_step's end "
                        "to the last scan workgroup's end (dispatch included, the interval rocprofv3 "
                        "--kernel-trace reports), %d launches" % scan_n),

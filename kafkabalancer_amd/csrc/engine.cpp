@@ -1338,10 +1338,10 @@ extern "C" int kb_engine_timings(kb_engine* e, double* ms, int64_t* launches, in
     HIPCHK(hipStreamSynchronize(e->st));
     HIPCHK(hipMemcpy(&c, e->ctl, sizeof c, hipMemcpyDeviceToHost));
     const double tick_ms = 1e-5;
-    double kms[TK_N + 2];
-    int64_t kn[TK_N + 2];
+    double kms[TK_N + 3];
+    int64_t kn[TK_N + 3];
     for (int k = 0; k < TK_N; k++) { kms[k] = e->kms[k]; kn[k] = e->klaunch[k]; }
-    kms[TK_N] = kms[TK_N + 1] = 0; kn[TK_N] = kn[TK_N + 1] = 0;
+    kms[TK_N] = kms[TK_N + 1] = kms[TK_N + 2] = 0; kn[TK_N] = kn[TK_N + 1] = kn[TK_N + 2] = 0;
     if (e->time_kernels == 1) {
         // spans (dispatch included, rocprofv3's interval) and the inner device-clock
         // intervals (first workgroup start .. last end)
@@ -1349,12 +1349,13 @@ extern "C" int kb_engine_timings(kb_engine* e, double* ms, int64_t* launches, in
         kms[TK_SCAN] = (double)c.tk_span[0] * tick_ms; kn[TK_SCAN] = (int64_t)c.tk_span_n[0];
         kms[TK_N] = (double)c.tk_sum[1] * tick_ms; kn[TK_N] = (int64_t)c.tk_n[1];
         kms[TK_N + 1] = (double)c.tk_sum[0] * tick_ms; kn[TK_N + 1] = (int64_t)c.tk_n[0];
+        kms[TK_N + 2] = (double)c.tk_pair * tick_ms; kn[TK_N + 2] = (int64_t)c.tk_pair_n;
     }
-    for (int k = 0; k < TK_N + 2 && k < n; k++) {
+    for (int k = 0; k < TK_N + 3 && k < n; k++) {
         if (ms) ms[k] = kms[k];
         if (launches) launches[k] = kn[k];
     }
-    return TK_N + 2;
+    return TK_N + 3;
 }
 
 extern "C" int kb_engine_set_timing(kb_engine* e, int32_t on) {
@@ -1369,6 +1370,7 @@ extern "C" int kb_engine_set_timing(kb_engine* e, int32_t on) {
     c.tk_on = e->time_kernels == 1;                 // (mode 2: events only, production kernels)
     c.tk_sum[0] = c.tk_sum[1] = c.tk_n[0] = c.tk_n[1] = 0;
     c.tk_span[0] = c.tk_span[1] = c.tk_span_n[0] = c.tk_span_n[1] = 0;
+    c.tk_pair = c.tk_pair_n = 0;
     c.ts_beg = NONE64;
     c.ts_end = 0;
     c.ts_prev_end = 0;

@@ -201,6 +201,9 @@ struct DevCtl {
     // workgroup end, k_step: scan end .. k_step end}; only launches queued back to back
     // (first workgroup within 10 us of the previous end) are counted
     unsigned long long tk_span[2], tk_span_n[2];
+    // k_pair: its first workgroup's start .. the step workgroup's end (the fused launch less
+    // its dispatch), summed with its count
+    unsigned long long tk_pair, tk_pair_n;
     int32_t tk_on;
     uint32_t step_mask;             // steps the next Balance() may take (bit = kb_step; SM_ALL)
     // incremental mode (kb_engine_set_incremental): incr_ok = the next scan

@@ -1234,6 +1234,10 @@ __device__ double incr_wskip(double rlo, double rhi, double thr, double avg, dou
     return ws * iav <= best ? ws : 0.0;
 }
 
+#ifndef KB_SET_G
+#define KB_SET_G 4   // records a wave rebuilds at once in the fused prep (A/B)
+#endif
+
 #ifndef KB_CLIST
 #define KB_CLIST 1   // exact folds over a compact contender list (0: the table walk only; A/B)
 #endif
@@ -1254,6 +1258,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
     unsigned long long t_in = wall_clock64();       // (FUSED: reset when the scan is in)
     KB_STAMP_BEGIN();
     __shared__ unsigned long long s_span_from;      // (kernel timing: the scan's end, or 0)
+    __shared__ unsigned long long s_pair_from;      // (k_pair: its first workgroup's start, or 0)
     auto write_back = [&]() {
         KB_STAMP_FLUSH(ctl);
         __syncthreads();
@@ -1265,6 +1270,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
             C.tk_sum[1] += t_out - t_in;
             C.tk_n[1]++;
             if (s_span_from) { C.tk_span[1] += t_out - s_span_from; C.tk_span_n[1]++; }
+            if (s_pair_from && t_out > s_pair_from) { C.tk_pair += t_out - s_pair_from; C.tk_pair_n++; }
         }
         __syncthreads();
         if (tid < CTL_WORDS) ((uint32_t*)ctl)[tid] = ((const uint32_t*)&C)[tid];
@@ -1431,18 +1437,18 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
             __syncthreads();
         }
     }
-    if (tid == 0) s_span_from = 0;
+    if (tid == 0) { s_span_from = 0; s_pair_from = 0; }
     if (tid == 0 && C.tk_on) {
         // kernel timing: the interval of the scan that ran before this launch (if any), and
-        // the spans when the scan followed the last k_step and this launch the scan back to
-        // back (no host gap: the first workgroup within 10 us of the previous end)
+        // the spans: the scan's when it followed the last k_step back to back, this launch's
+        // when it followed the scan (no host gap: within 10 us of the previous end); each
+        // counted on its own (c5's bound passes sit between a step and the next scan)
         const unsigned long long b = ts_b, e = ts_e;
+        if (FUSED && b != NONE64) s_pair_from = b;
         if (b != NONE64 && e > b) {
             C.tk_sum[0] += e - b; C.tk_n[0]++;
-            if (ts_pe && b > ts_pe && b - ts_pe < 1000 && t_in > e && t_in - e < 1000) {
-                C.tk_span[0] += e - ts_pe; C.tk_span_n[0]++;
-                s_span_from = e;
-            }
+            if (ts_pe && b > ts_pe && b - ts_pe < 1000) { C.tk_span[0] += e - ts_pe; C.tk_span_n[0]++; }
+            if (t_in > e && t_in - e < 1000) s_span_from = e;
         }
         ctl->ts_beg = NONE64;
         ctl->ts_end = 0;
@@ -2730,7 +2736,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
         // ---- P5.  set records of the marked sets (steps.go:192-201 targets): each wave
         // rebuilds G records at a time so their LDS chains overlap
         for (;;) {
-            constexpr int G = 4;
+            constexpr int G = KB_SET_G;
             const int W64 = a.W64, KR = a.KR;
             const int mn = (KB_ABL & 8) ? 0 : s_mn;
             constexpr int MAXU = sr_units(MAXR);
