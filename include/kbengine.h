@@ -201,7 +201,8 @@ int kb_engine_stats(kb_engine *e, kb_stats *out);
  * 4 k_step and 5 k_scan first-workgroup-start .. last-end (mode 1 only)}.  In mode 1,
  * k = 0 / 1 are device-clock spans from the end of the kernel before (dispatch included:
  * the interval rocprofv3 --kernel-trace reports), over back-to-back launches; 6 (mode 1, fused
- * pairs) k_pair from its first workgroup's start to the step workgroup's end.  Returns 7. */
+ * pairs) k_pair from its first workgroup's start to the step workgroup's end; 7 / 8 (mode 1)
+ * an eager refold workgroup's start .. end / start .. its list edit done.  Returns 9. */
 int kb_engine_timings(kb_engine *e, double *ms, int64_t *launches, int n);
 
 /* Kernel timing for the following plans (resets the sums): 0 off; 1 k_scan / k_step from

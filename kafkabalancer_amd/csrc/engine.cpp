@@ -101,7 +101,7 @@ struct kb_engine {
     Contender* cont = nullptr;
     uint32_t cont_cap = 1u << 20;
     int64_t spill_grows = 0;           // spill buffer growths (grow_spill)
-    Lists L{nullptr, nullptr, nullptr, nullptr};
+    Lists L{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
     DevCtl* ctl = nullptr;
     ChangeDev* log = nullptr;
     int logcap = 0;
@@ -654,6 +654,25 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
             HIPCHK(hipMemcpy(e->L.lcap, hlc.data(), hlc.size() * 4, hipMemcpyHostToDevice));
         }
         HIPCHK(hipMemcpy(e->L.lent, hle.data(), hle.size() * 4, hipMemcpyHostToDevice));
+        {
+            // fold checkpoints of the initial loads: every 64th partial sum of each list's
+            // in-order fold (the loads above are the same folds)
+            std::vector<double> hck(hle.size(), 0.0);
+            for (int64_t b = 0; b < e->B; b++) {
+                double acc = 0.0;
+                for (uint32_t k = 0; k < hll[b]; k++) {
+                    const int64_t i = hle[hls[b] + k];
+                    int slot = 0;
+                    while (slot < len[i] && dn(i, slot) != (int)b) slot++;
+                    acc += slot == 0 ? wt[i] * (double)(len[i] + ncon[i]) : wt[i];
+                    if ((k + 1) % 64 == 0) hck[hls[b] + k] = acc;
+                }
+            }
+            HIPCHK(dalloc(&e->L.ck, hck.size()));
+            HIPCHK(hipMemcpy(e->L.ck, hck.data(), hck.size() * 8, hipMemcpyHostToDevice));
+            HIPCHK(dalloc(&e->L.dpos, std::max<int64_t>(e->B, 1)));
+            HIPCHK(hipMemset(e->L.dpos, 0xFF, std::max<int64_t>(e->B, 1) * 4));
+        }
         if (const int rc = upload_rf(e); rc != KB_OK) { *out = e; return rc; }
     }
     DevCtl z;
@@ -713,6 +732,7 @@ static void fill_scan_args(kb_engine* e, ScanArgs& s) {
     s.eager = e->eager && e->nscan > 0 ? EGW : 0;
     s.gt = e->gb ? 1 : 0;
     s.done = e->pair_cnt;
+    s.dyn_lds = (int)e->scan_lds;
 }
 
 static void fill_step_args(kb_engine* e, StepArgs& a, const Recs& R, int use_spill) {
@@ -826,6 +846,7 @@ static void enqueue_pair(kb_engine* e, bool rf = false, bool rf_scan = false) {
         fill_step_args(e, a, scan_recs(e->recs, (int)e->nscan), 1);
         a.rf_final = rf && e->rf_stream;
         a.wait_n = s.nscan + (s.listwg ? 1 : 0) + s.eager;
+        s.dyn_lds = (int)e->pair_lds;
         a.fuse_pre = e->fuse_pre;
         launch_pair(s, a, e->rc_dev, e->lds_sets, e->pair_lds, e->st);
         return;
@@ -868,6 +889,12 @@ static int relist(kb_engine* e) {
     HIPCHK(dalloc(&nent, hle.size()));
     hipFree(e->L.lent);
     e->L.lent = nent;
+    // (the checkpoints follow the new layout; every broker is refolded from its start)
+    double* nck = nullptr;
+    HIPCHK(dalloc(&nck, hle.size()));
+    hipFree(e->L.ck);
+    e->L.ck = nck;
+    HIPCHK(hipMemset(e->L.dpos, 0, std::max<int64_t>(e->B, 1) * 4));
     HIPCHK(hipMemcpy(e->L.lent, hle.data(), hle.size() * 4, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(e->L.lstart, hls.data(), hls.size() * 4, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(e->L.llen, hll.data(), hll.size() * 4, hipMemcpyHostToDevice));
@@ -1338,10 +1365,10 @@ extern "C" int kb_engine_timings(kb_engine* e, double* ms, int64_t* launches, in
     HIPCHK(hipStreamSynchronize(e->st));
     HIPCHK(hipMemcpy(&c, e->ctl, sizeof c, hipMemcpyDeviceToHost));
     const double tick_ms = 1e-5;
-    double kms[TK_N + 3];
-    int64_t kn[TK_N + 3];
+    double kms[TK_N + 5];
+    int64_t kn[TK_N + 5];
     for (int k = 0; k < TK_N; k++) { kms[k] = e->kms[k]; kn[k] = e->klaunch[k]; }
-    kms[TK_N] = kms[TK_N + 1] = kms[TK_N + 2] = 0; kn[TK_N] = kn[TK_N + 1] = kn[TK_N + 2] = 0;
+    for (int k = TK_N; k < TK_N + 5; k++) { kms[k] = 0; kn[k] = 0; }
     if (e->time_kernels == 1) {
         // spans (dispatch included, rocprofv3's interval) and the inner device-clock
         // intervals (first workgroup start .. last end)
@@ -1350,12 +1377,14 @@ extern "C" int kb_engine_timings(kb_engine* e, double* ms, int64_t* launches, in
         kms[TK_N] = (double)c.tk_sum[1] * tick_ms; kn[TK_N] = (int64_t)c.tk_n[1];
         kms[TK_N + 1] = (double)c.tk_sum[0] * tick_ms; kn[TK_N + 1] = (int64_t)c.tk_n[0];
         kms[TK_N + 2] = (double)c.tk_pair * tick_ms; kn[TK_N + 2] = (int64_t)c.tk_pair_n;
+        kms[TK_N + 3] = (double)c.tk_eg * tick_ms; kn[TK_N + 3] = (int64_t)c.tk_eg_n;
+        kms[TK_N + 4] = (double)c.tk_eg_edit * tick_ms; kn[TK_N + 4] = (int64_t)c.tk_eg_n;
     }
-    for (int k = 0; k < TK_N + 3 && k < n; k++) {
+    for (int k = 0; k < TK_N + 5 && k < n; k++) {
         if (ms) ms[k] = kms[k];
         if (launches) launches[k] = kn[k];
     }
-    return TK_N + 3;
+    return TK_N + 5;
 }
 
 extern "C" int kb_engine_set_timing(kb_engine* e, int32_t on) {
@@ -1371,6 +1400,7 @@ extern "C" int kb_engine_set_timing(kb_engine* e, int32_t on) {
     c.tk_sum[0] = c.tk_sum[1] = c.tk_n[0] = c.tk_n[1] = 0;
     c.tk_span[0] = c.tk_span[1] = c.tk_span_n[0] = c.tk_span_n[1] = 0;
     c.tk_pair = c.tk_pair_n = 0;
+    c.tk_eg = c.tk_eg_edit = c.tk_eg_n = 0;
     c.ts_beg = NONE64;
     c.ts_end = 0;
     c.ts_prev_end = 0;
@@ -1514,7 +1544,7 @@ extern "C" void kb_engine_destroy(kb_engine* e) {
     void* ptrs[] = {e->w, e->rep, e->meta, e->pset, e->nc, e->load, e->lerr, e->eb, e->bfl, e->cnt,
                     e->setbits, e->setrec, e->order, e->posu, e->blm, e->posm, e->r,
                     e->bset_off, e->bset_ids, e->gscr, e->pair_cnt, e->recs, e->cont, e->ctl, e->log, e->bdesc, e->ubdesc,
-                    e->L.lstart, e->L.llen, e->L.lcap, e->L.lent, e->rf_dev};
+                    e->L.lstart, e->L.llen, e->L.lcap, e->L.lent, e->L.ck, e->L.dpos, e->rf_dev};
     for (void* p : ptrs) if (p) hipFree(p);
     if (e->h_ctl) hipHostFree(e->h_ctl);
     if (e->h_log) hipHostFree(e->h_log);

@@ -204,6 +204,8 @@ struct DevCtl {
     // k_pair: its first workgroup's start .. the step workgroup's end (the fused launch less
     // its dispatch), summed with its count
     unsigned long long tk_pair, tk_pair_n;
+    // eager refold workgroups (tk_on): summed start .. end and start .. list edit done, count
+    unsigned long long tk_eg, tk_eg_edit, tk_eg_n;
     int32_t tk_on;
     uint32_t step_mask;             // steps the next Balance() may take (bit = kb_step; SM_ALL)
     // incremental mode (kb_engine_set_incremental): incr_ok = the next scan

@@ -349,59 +349,179 @@ __device__ __forceinline__ double cont_delta(const double* r, const Contender& c
 // ------------------------------------------------ per-broker list upkeep
 // (partition lists sorted by index, for the exact refold of k_refresh)
 
-// remove partition q from broker b's list (block-wide, all threads call)
-__device__ void list_remove(Lists L, int b, uint32_t q, int* s_i) {
-    const uint32_t st = L.lstart[b], n = L.llen[b];
+// The list edits move up to LIST_K * blockDim entries per pass: every load of the pass is
+// issued before one barrier, then every store.  A list of at most LIST_K * blockDim
+// entries (c5: ~7300) is edited in one round trip -- the entries the search loaded are the
+// ones stored shifted; one barrier pair per blockDim entries made an edit ~15 us of
+// dependent round trips on the eager refolds' critical path.  Each edit lowers the
+// broker's first changed position (Lists.dpos, the fold checkpoints).
+constexpr int LIST_K = 8;
+
+struct ListExt { uint32_t st, n, dp; };      // a list's start, length, first changed position
+
+__device__ __forceinline__ ListExt list_ext(const Lists& L, int b) {
+    ListExt x;
+    x.st = L.lstart[b]; x.n = L.llen[b]; x.dp = L.dpos[b];
+    return x;
+}
+
+// remove partition q from broker b's list (block-wide, all threads call); x follows
+__device__ void list_remove_x(Lists L, int b, uint32_t q, ListExt& x, int* s_i) {
+    const uint32_t st = x.st, n = x.n;
     const uint32_t nt = blockDim.x;
     if (threadIdx.x == 0) *s_i = -1;
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i < n; i += nt)
-        if (L.lent[st + i] == q) *s_i = (int)i;
+    if (n <= LIST_K * nt) {
+        uint32_t v[LIST_K];
+#pragma unroll
+        for (int k = 0; k < LIST_K; k++) {
+            const uint32_t i = k * nt + threadIdx.x;
+            v[k] = i < n ? L.lent[st + i] : NONE32;
+        }
+#pragma unroll
+        for (int k = 0; k < LIST_K; k++)
+            if (v[k] == q) *s_i = (int)(k * nt + threadIdx.x);
+        __syncthreads();
+        const int at = *s_i;
+        if (at < 0) return;
+#pragma unroll
+        for (int k = 0; k < LIST_K; k++) {
+            const uint32_t i = k * nt + threadIdx.x;
+            if (i > (uint32_t)at && i < n) L.lent[st + i - 1] = v[k];
+        }
+        if (threadIdx.x == 0) {
+            L.llen[b] = n - 1;
+            if ((uint32_t)at < x.dp) L.dpos[b] = (uint32_t)at;
+        }
+        __syncthreads();
+        x.n = n - 1;
+        x.dp = (uint32_t)at < x.dp ? (uint32_t)at : x.dp;
+        return;
+    }
+    for (uint32_t i0 = 0; i0 < n; i0 += LIST_K * nt) {
+        uint32_t v[LIST_K];
+#pragma unroll
+        for (int k = 0; k < LIST_K; k++) {
+            const uint32_t i = i0 + k * nt + threadIdx.x;
+            v[k] = i < n ? L.lent[st + i] : NONE32;
+        }
+#pragma unroll
+        for (int k = 0; k < LIST_K; k++)
+            if (v[k] == q) *s_i = (int)(i0 + k * nt + threadIdx.x);
+    }
     __syncthreads();
     const int at = *s_i;
     if (at < 0) return;
-    for (uint32_t c = (uint32_t)at; c + 1 < n; c += nt) {
-        uint32_t j = c + threadIdx.x;
-        uint32_t v = 0;
-        bool act = j + 1 < n;
-        if (act) v = L.lent[st + j + 1];
+    for (uint32_t c = (uint32_t)at; c + 1 < n; c += LIST_K * nt) {
+        uint32_t v[LIST_K];
+#pragma unroll
+        for (int k = 0; k < LIST_K; k++) {
+            const uint32_t j = c + k * nt + threadIdx.x;
+            v[k] = j + 1 < n ? L.lent[st + j + 1] : 0u;
+        }
         __syncthreads();
-        if (act) L.lent[st + j] = v;
+#pragma unroll
+        for (int k = 0; k < LIST_K; k++) {
+            const uint32_t j = c + k * nt + threadIdx.x;
+            if (j + 1 < n) L.lent[st + j] = v[k];
+        }
         __syncthreads();
     }
-    if (threadIdx.x == 0) L.llen[b] = n - 1;
+    if (threadIdx.x == 0) {
+        L.llen[b] = n - 1;
+        if ((uint32_t)at < x.dp) L.dpos[b] = (uint32_t)at;
+    }
     __syncthreads();
+    x.n = n - 1;
+    x.dp = (uint32_t)at < x.dp ? (uint32_t)at : x.dp;
 }
 
-// insert partition q into broker b's sorted list
-__device__ bool list_insert(Lists L, int b, uint32_t q, int* s_i) {
-    const uint32_t st = L.lstart[b], n = L.llen[b];
+// insert partition q into broker b's sorted list; false: no room (the list keeps q out)
+__device__ bool list_insert_x(Lists L, int b, uint32_t q, ListExt& x, int* s_i) {
+    const uint32_t st = x.st, n = x.n;
     const uint32_t nt = blockDim.x;
     if (n >= L.lcap[b]) return false;
     if (threadIdx.x == 0) *s_i = 0;
     __syncthreads();
+    if (n <= LIST_K * nt) {
+        uint32_t v[LIST_K];
+#pragma unroll
+        for (int k = 0; k < LIST_K; k++) {
+            const uint32_t i = k * nt + threadIdx.x;
+            v[k] = i < n ? L.lent[st + i] : NONE32;
+        }
+        int c = 0;
+#pragma unroll
+        for (int k = 0; k < LIST_K; k++) c += v[k] < q ? 1 : 0;
+        c = wave_sum(c);
+        if ((threadIdx.x & 63) == 0 && c) atomicAdd(s_i, c);
+        __syncthreads();
+        const uint32_t at = (uint32_t)*s_i;
+#pragma unroll
+        for (int k = 0; k < LIST_K; k++) {
+            const uint32_t i = k * nt + threadIdx.x;
+            if (i >= at && i < n) L.lent[st + i + 1] = v[k];
+        }
+        if (threadIdx.x == 0) {
+            L.lent[st + at] = q; L.llen[b] = n + 1;
+            if (at < x.dp) L.dpos[b] = at;
+        }
+        __syncthreads();
+        x.n = n + 1;
+        x.dp = at < x.dp ? at : x.dp;
+        return true;
+    }
     int c = 0;
-    for (uint32_t i = threadIdx.x; i < n; i += nt) c += L.lent[st + i] < q ? 1 : 0;
+    for (uint32_t i0 = 0; i0 < n; i0 += LIST_K * nt) {
+        uint32_t v[LIST_K];
+#pragma unroll
+        for (int k = 0; k < LIST_K; k++) {
+            const uint32_t i = i0 + k * nt + threadIdx.x;
+            v[k] = i < n ? L.lent[st + i] : NONE32;
+        }
+#pragma unroll
+        for (int k = 0; k < LIST_K; k++) c += v[k] < q ? 1 : 0;
+    }
     c = wave_sum(c);
     if ((threadIdx.x & 63) == 0 && c) atomicAdd(s_i, c);
     __syncthreads();
     const uint32_t at = (uint32_t)*s_i;
     long long hi = (long long)n;
     while (hi > (long long)at) {
-        long long lo = hi - (long long)nt;
+        long long lo = hi - (long long)LIST_K * nt;
         if (lo < (long long)at) lo = at;
-        long long j = lo + threadIdx.x;
-        bool act = j < hi;
-        uint32_t v = 0;
-        if (act) v = L.lent[st + j];
+        uint32_t v[LIST_K];
+#pragma unroll
+        for (int k = 0; k < LIST_K; k++) {
+            const long long j = lo + k * (long long)nt + threadIdx.x;
+            v[k] = j < hi ? L.lent[st + j] : 0u;
+        }
         __syncthreads();
-        if (act) L.lent[st + j + 1] = v;
+#pragma unroll
+        for (int k = 0; k < LIST_K; k++) {
+            const long long j = lo + k * (long long)nt + threadIdx.x;
+            if (j < hi) L.lent[st + j + 1] = v[k];
+        }
         __syncthreads();
         hi = lo;
     }
-    if (threadIdx.x == 0) { L.lent[st + at] = q; L.llen[b] = n + 1; }
+    if (threadIdx.x == 0) {
+        L.lent[st + at] = q; L.llen[b] = n + 1;
+        if (at < x.dp) L.dpos[b] = at;
+    }
     __syncthreads();
+    x.n = n + 1;
+    x.dp = at < x.dp ? at : x.dp;
     return true;
+}
+
+__device__ void list_remove(Lists L, int b, uint32_t q, int* s_i) {
+    ListExt x = list_ext(L, b);
+    list_remove_x(L, b, q, x, s_i);
+}
+__device__ bool list_insert(Lists L, int b, uint32_t q, int* s_i) {
+    ListExt x = list_ext(L, b);
+    return list_insert_x(L, b, q, x, s_i);
 }
 
 // the list change of the last applied move (kind 1 replace, 2 remove, 3 add)
@@ -1032,7 +1152,8 @@ __device__ __forceinline__ void scan_round(const ScanArgs& a, const ScanParams& 
 #pragma unroll
             for (int f = 0; f < NF; f++) st32_wt(fo + f, fst[f]);
         }
-        if (tk_on) {                           // the scan's interval (kernel timing)
+        if (tk_on && !a.ubpass) {              // the scan's interval (kernel timing; a bound
+                                               // pass before it is timed by events, mode 2)
             atomicMin(&ctl->ts_beg, t_in);
             atomicMax(&ctl->ts_end, wall_clock64());
         }
@@ -1042,7 +1163,7 @@ __device__ __forceinline__ void scan_round(const ScanArgs& a, const ScanParams& 
 
 __device__ __attribute__((noinline)) void refresh_in_scan(const RefreshArgs* rfp, int pend, int kind, int from, int to,
                                                           uint32_t part, double* buf, int ng);   // (k_refresh below)
-__device__ __attribute__((noinline)) void eager_refold(const RefreshArgs* rfp, int k, double* buf);
+__device__ __attribute__((noinline)) void eager_refold(const RefreshArgs* rfp, int k, double* buf, int cap);
 
 template <int RC, bool LSETS, bool INCR, bool GT>
 __device__ __forceinline__ void scan_kernel_body(const ScanArgs& a) {
@@ -1052,7 +1173,7 @@ __device__ __forceinline__ void scan_kernel_body(const ScanArgs& a) {
     // eager refolds: the last workgroups of the grid refold the brokers the last step touched
     // (their lists already edited by k_step), concurrently with the scan
     if (KB_EAGER_CODE && a.eager && (int)blockIdx.x >= a.nscan + (a.listwg ? 1 : 0)) {
-        eager_refold(a.rf, (int)blockIdx.x - a.nscan - (a.listwg ? 1 : 0), (double*)smem);
+        eager_refold(a.rf, (int)blockIdx.x - a.nscan - (a.listwg ? 1 : 0), (double*)smem, a.dyn_lds / 8);
         return;
     }
     // (rfpass: if the last k_step halted for exact loads, this launch is the refresh,
@@ -2283,6 +2404,15 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
                         a.load[b] = Ln; s_ld[b] = Ln;
                         a.eb[b] = eb; s_e[b] = eb;
                         a.bfl[b] = fl; s_fl[b] = fl;
+                        if (!a.integral) {
+                            // fold checkpoints: a broker whose list is edited gets its first
+                            // changed position from the edit (list_remove / list_insert); one
+                            // whose contribution changed in place (the leader's weight after a
+                            // remove / add, a swap's two brokers) is refolded from the start
+                            const bool ledit = (kind == 1 && (b == D.from || b == to)) ||
+                                               (kind == 2 && b == D.from) || (kind == 3 && b == to);
+                            if (!ledit) a.L.dpos[b] = 0u;
+                        }
                         mchg = ((fl0 ^ fl) & BF_PRESENT) && !(fl & BF_INCFG);
                     }
                 }
@@ -3317,11 +3447,19 @@ constexpr int REFRESH_CHUNK = 1024;
 // gather chunk j + 1 from the partition list -- every list load of a thread first, then
 // the partition words they index, then the LDS writes (two round trips per chunk, not
 // two per element).  buf: 2 * CH doubles of LDS.
+// (x: the list's extent when the caller has it -- the eager refold, right after its edit)
 template <int NT, int CH>
-__device__ __forceinline__ double refold_broker(const RefreshArgs& a, int b, double* buf) {
+__device__ __forceinline__ double refold_broker(const RefreshArgs& a, int b, double* buf, const ListExt* xk = nullptr) {
     constexpr int GT = NT - 64, PER = (CH + GT - 1) / GT;
-    const uint32_t st = a.L.lstart[b], n = a.L.llen[b];
-    const int tid = threadIdx.x, wid = tid >> 6;
+    static_assert(CH % 64 == 0, "whole checkpoint blocks per chunk");
+    const ListExt x = xk ? *xk : list_ext(a.L, b);
+    const uint32_t st = x.st, n = x.n;
+    const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
+    // restart at the last checkpoint below the first changed position: the fold of the
+    // unchanged prefix is that checkpoint's value, bit for bit (the same chain)
+    const uint32_t dp = x.dp;
+    const uint32_t base = (dp < n ? dp : n) & ~63u;
+    const double acc0 = base ? a.L.ck[st + base - 1] : 0.0;
     auto gather = [&](uint32_t c0, double* dst) {
         const int t = tid - 64;
         uint32_t q[PER];
@@ -3344,13 +3482,21 @@ __device__ __forceinline__ double refold_broker(const RefreshArgs& a, int b, dou
             if (q[k] != NONE32)   // slot 0 carries the leader weight W * (len(R) + NumConsumers)
                 dst[t + k * GT] = r0[k] == (uint16_t)b ? w[k] * (double)((int)meta_nrep(mq[k]) + ncq[k]) : w[k];
     };
-    double acc = 0.0;
-    if (wid > 0 && n) gather(0, buf);
+    double acc = acc0;
+    if (wid > 0 && base < n) gather(base, buf);
     __syncthreads();
-    for (uint32_t c0 = 0, j = 0; c0 < n; c0 += CH, j++) {
+    for (uint32_t c0 = base, j = 0; c0 < n; c0 += CH, j++) {
         const uint32_t m = n - c0 < (uint32_t)CH ? n - c0 : (uint32_t)CH;
         if (wid > 0 && c0 + CH < n) gather(c0 + CH, buf + ((j + 1) & 1) * CH);
-        if (wid == 0) acc = chain_lds(acc, (const lds_f64*)(buf + (j & 1) * CH), (int)m);
+        if (wid == 0) {
+            // the chain in 64-element blocks, a checkpoint after each whole one
+            const lds_f64* x = (const lds_f64*)(buf + (j & 1) * CH);
+            for (uint32_t u = 0; u < m; u += 64) {
+                const int mm = m - u < 64u ? (int)(m - u) : 64;
+                acc = chain_lds(acc, x + u, mm);
+                if (mm == 64 && lane == 0) a.L.ck[st + c0 + u + 63] = acc;
+            }
+        }
         __syncthreads();
     }
     if (tid == 0) {
@@ -3358,6 +3504,7 @@ __device__ __forceinline__ double refold_broker(const RefreshArgs& a, int b, dou
         a.lerr[b] = gamma_n((int)n) * acc;
         a.eb[b] = 0.0;
         a.bfl[b] = a.bfl[b] & ~BF_DIRTY;
+        a.L.dpos[b] = NONE32;
     }
     return acc;
 }
@@ -3415,29 +3562,141 @@ __device__ __attribute__((noinline)) void refresh_in_scan(const RefreshArgs* rfp
 // scan runs (it never reads the loads): the next k_step resolves on exact loads, with no halt
 // for a refresh when its decision needs the exact folds.  A halted step's launch is the
 // in-stream refresh's instead (it does the edit and refolds every dirty broker).
-__device__ __attribute__((noinline)) void eager_refold(const RefreshArgs* rfp, int k, double* buf) {
+// The edit and the refold in one pass over the list (a list of at most LIST_K * blockDim
+// entries whose suffix fits the workgroup's LDS): the entries the edit loads are the ones
+// whose partition words the refold gathers, at their new positions, so the refold costs one
+// memory round trip -- the partition words -- then the chain from the last checkpoint below
+// the first changed position.  (Under the scan's full-rate stream a round trip costs ~10 us:
+// the chunked refold's two per chunk made an eager workgroup ~50 us at c5, longer than the
+// scan it runs beside.)  Returns false (nothing done) when the list does not qualify.
+__device__ bool eager_edit_refold(const RefreshArgs& rf, int b, int op, uint32_t q, ListExt& x, double* buf, int cap) {
+    const uint32_t st = x.st, n = x.n, nt = blockDim.x;
+    const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
+    if (n + 1 > LIST_K * nt || (int)n + 1 > cap) return false;
+    if (op == 2 && n >= rf.L.lcap[b]) return false;          // (the general path reports it)
+    __shared__ int s_at;
+    __shared__ double s_acc0;
+    if (tid == 0) s_at = op == 1 ? -1 : 0;
+    __syncthreads();
+    uint32_t v[LIST_K];
+#pragma unroll
+    for (int k = 0; k < LIST_K; k++) {
+        const uint32_t i = k * nt + tid;
+        v[k] = i < n ? rf.L.lent[st + i] : NONE32;
+    }
+    if (op == 1) {
+#pragma unroll
+        for (int k = 0; k < LIST_K; k++)
+            if (v[k] == q) s_at = (int)(k * nt + tid);
+    } else if (op == 2) {
+        int c = 0;
+#pragma unroll
+        for (int k = 0; k < LIST_K; k++) c += v[k] < q ? 1 : 0;
+        c = wave_sum(c);
+        if (lane == 0 && c) atomicAdd(&s_at, c);
+    }
+    __syncthreads();
+    int at = s_at;
+    if (op == 1 && at < 0) op = 0;                           // (not listed: nothing to remove)
+    if (op == 0) at = (int)n;
+    const uint32_t nn = op == 1 ? n - 1 : (op == 2 ? n + 1 : n);
+    const uint32_t dp = (uint32_t)at < x.dp ? (uint32_t)at : x.dp;
+    const uint32_t base = (dp < nn ? dp : nn) & ~63u;
+    // the edit's stores, and the contributions of the new positions >= base
+#pragma unroll
+    for (int k = 0; k < LIST_K; k++) {
+        const uint32_t i = k * nt + tid;
+        if (i >= n) continue;
+        uint32_t np = i;
+        if (op == 1) { if (i == (uint32_t)at) continue; if (i > (uint32_t)at) { np = i - 1; rf.L.lent[st + np] = v[k]; } }
+        if (op == 2 && i >= (uint32_t)at) { np = i + 1; rf.L.lent[st + np] = v[k]; }
+        if (np >= base) {
+            const uint32_t pp = v[k];
+            const double w = rf.w[pp];
+            const uint32_t m = rf.meta[pp];
+            const int32_t ncp = rf.nc[pp];
+            const uint16_t r0 = rf.rep[pp];
+            buf[np - base] = r0 == (uint16_t)b ? w * (double)((int)meta_nrep(m) + ncp) : w;
+        }
+    }
+    if (tid == 0) {
+        if (op == 2) {
+            rf.L.lent[st + at] = q;
+            if ((uint32_t)at >= base) {
+                const double w = rf.w[q];
+                const uint32_t m = rf.meta[q];
+                const int32_t ncp = rf.nc[q];
+                const uint16_t r0 = rf.rep[q];
+                buf[at - base] = r0 == (uint16_t)b ? w * (double)((int)meta_nrep(m) + ncp) : w;
+            }
+        }
+        rf.L.llen[b] = nn;
+        s_acc0 = base ? rf.L.ck[st + base - 1] : 0.0;
+    }
+    __syncthreads();
+    if (wid == 0) {
+        double acc = s_acc0;
+        const lds_f64* xb = (const lds_f64*)buf;
+        for (uint32_t u = 0; u < nn - base; u += 64) {
+            const int mm = nn - base - u < 64u ? (int)(nn - base - u) : 64;
+            acc = chain_lds(acc, xb + u, mm);
+            if (mm == 64 && lane == 0) rf.L.ck[st + base + u + 63] = acc;
+        }
+        if (lane == 0) {
+            rf.load[b] = acc;
+            rf.lerr[b] = gamma_n((int)nn) * acc;
+            rf.eb[b] = 0.0;
+            rf.bfl[b] = rf.bfl[b] & ~BF_DIRTY;
+            rf.L.dpos[b] = NONE32;
+        }
+    }
+    __syncthreads();
+    x.n = nn;
+    x.dp = NONE32;
+    return true;
+}
+
+__device__ __attribute__((noinline)) void eager_refold(const RefreshArgs* rfp, int k, double* buf, int cap) {
     const RefreshArgs rf = *rfp;
     DevCtl* ctl = rf.ctl;
     if (ctl->halted != H_RUN || k >= ctl->eg_n || ctl->list_overflow) return;   // (uniform)
     const int b = ctl->eg_b[k];
     if (b < 0 || b >= rf.B) return;
+    const bool tk = ctl->tk_on != 0;
+    const unsigned long long t0 = tk ? wall_clock64() : 0ull;
+    ListExt x = list_ext(rf.L, b);                // (one round trip with the flags below)
+    const bool dirty = (rf.bfl[b] & BF_DIRTY) != 0;
+    // this broker's half of the last step's list edit (replace = remove from `from`, insert
+    // into `to`: different lists, different workgroups)
+    int op = 0;
+    uint32_t p = 0;
     if (ctl->pending_list) {
-        // this broker's half of the last step's list edit (replace = remove from `from`,
-        // insert into `to`: different lists, different workgroups)
-        __shared__ int s_i;
         const int kind = ctl->pl_kind;
-        const uint32_t p = (uint32_t)ctl->pl_part;
+        p = (uint32_t)ctl->pl_part;
+        if (b == ctl->pl_from && (kind == 1 || kind == 2)) op = 1;
+        else if (b == ctl->pl_to && (kind == 1 || kind == 3)) op = 2;
+    }
+    const bool one = dirty && eager_edit_refold(rf, b, op, p, x, buf, cap);
+    const unsigned long long t1 = tk ? wall_clock64() : 0ull;
+    if (!one) {
+        __shared__ int s_i;
         bool ok = true;
-        if (b == ctl->pl_from && (kind == 1 || kind == 2)) list_remove(rf.L, b, p, &s_i);
-        if (b == ctl->pl_to && (kind == 1 || kind == 3)) ok = list_insert(rf.L, b, p, &s_i);
+        if (op == 1) list_remove_x(rf.L, b, p, x, &s_i);
+        if (op == 2) ok = list_insert_x(rf.L, b, p, x, &s_i);
         if (!ok) {                                 // (the broker stays dirty: the host relists)
             if (threadIdx.x == 0) ctl->list_overflow = 1;
             return;
         }
+        if (dirty) refold_broker<SCAN_THREADS, RF_CHUNK>(rf, b, buf, &x);
     }
-    if (!(rf.bfl[b] & BF_DIRTY)) return;
-    refold_broker<SCAN_THREADS, RF_CHUNK>(rf, b, buf);
-    if (threadIdx.x == 0) atomicSub(&ctl->ndirty, 1);
+    if (threadIdx.x == 0) {
+        if (dirty) atomicSub(&ctl->ndirty, 1);
+        if (tk) {                                  // (kernel timing: the eager workgroups' spans)
+            atomicAdd(&ctl->tk_eg, wall_clock64() - t0);
+            atomicAdd(&ctl->tk_eg_edit, t1 - t0);
+            atomicAdd(&ctl->tk_eg_n, 1ull);
+        }
+    }
 }
 
 // --------------------------------------------------- multi-GPU summaries

@@ -13,6 +13,12 @@ struct Lists {
     uint32_t* llen;
     uint32_t* lcap;
     uint32_t* lent;
+    // fold checkpoints: ck[lstart + 64 i - 1] = the in-order fold of a list's first 64 i
+    // contributions (i >= 1, the partial sums of getBrokerLoad's own chain), valid below
+    // dpos[b], the first list position whose entry or contribution changed since the broker's
+    // last refold (NONE32: all valid) -- a refold restarts at the checkpoint below dpos
+    double* ck;
+    uint32_t* dpos;
 };
 
 struct RefreshArgs {
@@ -65,6 +71,7 @@ struct ScanArgs {
                               //    last applied step's touched brokers (DevCtl.eg_*)
     int gt;                   // 1: the broker tables are read from memory (B > MAXB; k_scan<.., GT>)
     uint32_t* done;           // k_pair: every non-step workgroup counts itself in here when done
+    int dyn_lds;              // the launch's dynamic LDS bytes (the eager refolds' buffer)
 };
 
 struct StepArgs {

@@ -355,14 +355,14 @@ class Engine:
         lib().kb_engine_stats(self.h, C.byref(s))
         return {f: getattr(s, f) for f, _ in s._fields_}
 
-    KERNELS = ("step", "scan", "refresh", "bound", "step_inner", "scan_inner", "pair")
+    KERNELS = ("step", "scan", "refresh", "bound", "step_inner", "scan_inner", "pair", "eager", "eager_edit")
 
     def timings(self):
         """{kernel: (total_ms, launches)} of the plans since set_timing; mode 1: step / scan are
         rocprof-comparable device-clock spans, step_inner / scan_inner first-start..last-end."""
-        ms = np.zeros(7)
-        n = np.zeros(7, np.int64)
-        lib().kb_engine_timings(self.h, ms.ctypes.data_as(PD), n.ctypes.data_as(P64), 7)
+        ms = np.zeros(9)
+        n = np.zeros(9, np.int64)
+        lib().kb_engine_timings(self.h, ms.ctypes.data_as(PD), n.ctypes.data_as(P64), 9)
         return {k: (float(ms[i]), int(n[i])) for i, k in enumerate(self.KERNELS)}
 
     def set_timing(self, on):
