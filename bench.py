@@ -7,13 +7,16 @@ Balance() call (balancer.go:49-65) executed device-resident by kb_engine_plan;
 `value` counts the candidates the reference would score (SURVEY.md 8d metric 1)
 over the timed steps, per wall second.
 
-Roofline: the streaming kernel is k_scan; `achieved` = its algorithmic
-bytes per launch / its average in-plan launch duration, measured live on the engine's
-stream with the device clock: each launch's span from the end of the kernel before it to
-its own last workgroup's end (dispatch included: the interval rocprofv3 --kernel-trace
-reports, so the committed profiles/*/c3_kernel_stats.csv recomputes it; HIP events
-around each launch add ~2-3 us of their own and are reported as a side figure).  The
-inner duration (first scan workgroup start to last end) and the whole-step fraction
+Roofline: the dominant kernel is the launch that streams the partitions --
+k_pair (the scan's grid and the step workgroup in one launch per step) where the engine
+fuses the pair, else k_scan; `achieved` = the scan's algorithmic bytes per launch / that
+launch's average in-plan duration, measured live on the engine's stream with the device
+clock: each launch's span from the end of the launch before it to its own end (dispatch
+included: the interval rocprofv3 --kernel-trace reports, so the committed
+profiles/*/c3_kernel_stats.csv recomputes it; k_pair's span = the scan span + the step
+span; HIP events around each launch add ~2-3 us of their own and are reported as a side
+figure).  The scan phase alone (`scan_phase_frac`), the inner duration (first scan
+workgroup start to last end) and the whole-step fraction
 `frac_step` (SURVEY 8(d) bytes per step / ms_per_step / 8 TB/s) are reported beside it.  `traffic` is the rocprofv3 PMC figure for the same workload
 (profiles/pmc_traffic.json, keyed by workload, stamped with the git head it ran on).
 
