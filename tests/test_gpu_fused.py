@@ -1,0 +1,66 @@
+"""The fused pair (k_pair: the scan's grid plus one resident step workgroup per launch)
+against the two-launch pair (k_scan + k_step, KB_FUSE=0): the same plans, the same device
+state after them (every broker load bit for bit), on the headline shape, on c5's broker
+width with eager refolds and fold checkpoints, and the small-shard gate (c2 keeps two
+launches).  The parity of both against the oracle is the rest of the -m gpu suite."""
+import os
+
+import pytest
+
+from kafkabalancer_amd import engine as E
+from kafkabalancer_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+
+def run(cl, cfg, steps, fuse):
+    old = os.environ.get("KB_FUSE")
+    os.environ["KB_FUSE"] = "1" if fuse else "0"
+    try:
+        eng = E.Engine(cl, cfg)
+    finally:
+        if old is None:
+            del os.environ["KB_FUSE"]
+        else:
+            os.environ["KB_FUSE"] = old
+    changes, err = eng.plan(steps)
+    st = eng.stats()
+    loads = eng.loads()
+    eng.close()
+    return changes, err, st, loads
+
+
+def keyed(changes):
+    return [(c["step"], c["pidx"], c["kind"], c["from_"], c["to"], c["slot"], c["su"], c["cu"]) for c in changes]
+
+
+# (full size: the pair is fused only when the scan tiles are full -- 16 scoring waves)
+@pytest.mark.parametrize("name,scale,steps", [("c3", 1.0, 200), ("c4", 1.0, 400)])
+def test_fused_matches_two_launches(name, scale, steps):
+    cl, cfg, _ = synth.config(name, scale=scale)
+    a = run(cl, cfg, steps, True)
+    b = run(cl, cfg, steps, False)
+    assert a[2]["fused_pairs"] == 1 and b[2]["fused_pairs"] == 0
+    assert (a[1] is None) == (b[1] is None)
+    assert keyed(a[0]) == keyed(b[0])
+    assert a[3] == b[3]
+
+
+def test_fused_eager_checkpoints_match_two_launches():
+    """c5's broker width (1M partitions x 4096 brokers, Zipf): eager refolds with fold
+    checkpoints inside the fused launch, against the two-launch pair."""
+    cl = synth.make_cluster(1_000_000, 4096, 3, "zipf", seed=0x5EED5005)
+    cfg = {"allow_leader": False, "rebalance_leaders": False, "min_replicas": 2, "min_unbalance": 0.0,
+           "brokers": None}
+    a = run(cl, cfg, 80, True)
+    b = run(cl, cfg, 80, False)
+    assert a[2]["fused_pairs"] == 1
+    assert keyed(a[0]) == keyed(b[0])
+    assert a[3] == b[3]
+
+
+def test_small_shard_keeps_two_launches():
+    cl, cfg, _ = synth.config("c2")
+    eng = E.Engine(cl, cfg)
+    assert eng.stats()["fused_pairs"] == 0
+    eng.close()
