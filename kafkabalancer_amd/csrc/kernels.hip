@@ -206,6 +206,38 @@ __device__ __forceinline__ double chain_lds(double acc, const lds_f64* x, int m)
     for (; k < m; k++) acc += x[k];
     return acc;
 }
+// The same in-order chain over m elements with the next 16 elements' LDS reads issued
+// before the current 16 are added (two register sets, alternating; the reads are
+// unconditional -- x must have 32 readable elements past m -- so the compiler waits for the
+// older eight reads only), and the running sum stored after every 64th element (the list
+// folds' checkpoints: ck[i] for the element i closing a 64-block, i relative to x; lane 0).
+__device__ __forceinline__ double chain_lds_ck(double acc, const lds_f64* x, int m, double* ck, int lane) {
+    const lds_f64x2* x2 = (const lds_f64x2*)x;
+    f64x2 a[8], b[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) a[j] = x2[j];
+    int k = 0;
+    for (; k + 32 <= m; k += 32) {
+#pragma unroll
+        for (int j = 0; j < 8; j++) b[j] = x2[((k + 16) >> 1) + j];
+#pragma unroll
+        for (int j = 0; j < 8; j++) { acc += a[j].x; acc += a[j].y; }
+        if (((k + 16) & 63) == 0 && lane == 0) ck[k + 15] = acc;
+#pragma unroll
+        for (int j = 0; j < 8; j++) a[j] = x2[((k + 32) >> 1) + j];
+#pragma unroll
+        for (int j = 0; j < 8; j++) { acc += b[j].x; acc += b[j].y; }
+        if (((k + 32) & 63) == 0 && lane == 0) ck[k + 31] = acc;
+    }
+    if (k + 16 <= m) {
+#pragma unroll
+        for (int j = 0; j < 8; j++) { acc += a[j].x; acc += a[j].y; }
+        if (((k + 16) & 63) == 0 && lane == 0) ck[k + 15] = acc;
+        k += 16;
+    }
+    for (; k < m; k++) acc += x[k];
+    return acc;
+}
 // a wave's own LDS writes are seen by its later reads (LDS executes a wave's
 // operations in order); this keeps the compiler from moving them across
 __device__ __forceinline__ void wave_lds_sync() {
@@ -3572,7 +3604,7 @@ __device__ __attribute__((noinline)) void refresh_in_scan(const RefreshArgs* rfp
 __device__ bool eager_edit_refold(const RefreshArgs& rf, int b, int op, uint32_t q, ListExt& x, double* buf, int cap) {
     const uint32_t st = x.st, n = x.n, nt = blockDim.x;
     const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
-    if (n + 1 > LIST_K * nt || (int)n + 1 > cap) return false;
+    if (n + 1 > LIST_K * nt || (int)n + 1 + 32 > cap) return false;   // (+32: the chain's read-ahead)
     if (op == 2 && n >= rf.L.lcap[b]) return false;          // (the general path reports it)
     __shared__ int s_at;
     __shared__ double s_acc0;
@@ -3635,13 +3667,7 @@ __device__ bool eager_edit_refold(const RefreshArgs& rf, int b, int op, uint32_t
     }
     __syncthreads();
     if (wid == 0) {
-        double acc = s_acc0;
-        const lds_f64* xb = (const lds_f64*)buf;
-        for (uint32_t u = 0; u < nn - base; u += 64) {
-            const int mm = nn - base - u < 64u ? (int)(nn - base - u) : 64;
-            acc = chain_lds(acc, xb + u, mm);
-            if (mm == 64 && lane == 0) rf.L.ck[st + base + u + 63] = acc;
-        }
+        const double acc = chain_lds_ck(s_acc0, (const lds_f64*)buf, (int)(nn - base), rf.L.ck + st + base, lane);
         if (lane == 0) {
             rf.load[b] = acc;
             rf.lerr[b] = gamma_n((int)nn) * acc;
