@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define KB_ABI_VERSION 8
+#define KB_ABI_VERSION 9
 
 /* step indices == position in the reference's steps table (balancer.go:34-44) */
 enum kb_step {
@@ -210,6 +210,12 @@ int kb_engine_timings(kb_engine *e, double *ms, int64_t *launches, int n);
  * from HIP events; 2 HIP events around every launch (each event adds its own ~2-3 us to
  * the interval around a launch). */
 int kb_engine_set_timing(kb_engine *e, int32_t on);
+
+/* Diagnostic (ABI 9): host phases of the kb_engine_plan calls since kb_engine_set_timing, in
+ * microseconds: us[0] control-block reset, [1] enqueue of the batches, [2] waiting for them
+ * (the batch-end control-block / log transfer included), [3] log conversion, [4] the
+ * number of calls.  Returns 5. */
+int kb_engine_host_timings(kb_engine *e, double *us, int n);
 
 /* Incremental rescoring mode (single GPU, off by default): after a
  * move() step (MoveLeaders / MoveNonLeaders, steps.go:145-232) the next scan reads only

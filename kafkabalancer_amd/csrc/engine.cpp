@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 #include <algorithm>
 #include <cfloat>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -142,10 +143,37 @@ struct kb_engine {
     bool recs_fresh = false;           // the scan records describe the current state (a masked
                                        //   step changed nothing): the next masked step reuses them
     bool reuse_now = false;            //   (the run about to start takes them)
+    // control-block / step-log transfers (run_steps, reset_ctl): 0 = hipMemcpyAsync, 1 = k_xfer
+    // (one-workgroup kernel to / from the pinned mirror, then a stream synchronisation),
+    // 2 = k_xfer whose system-scope flag the host polls (KB_XFER, diagnostic A/B)
+    int xfer = 2;
+    DevCtl* h_ctl_d = nullptr;         // device addresses of the mapped pinned mirror
+    ChangeDev* h_log_d = nullptr;
+    uint32_t* h_flag = nullptr;        // k_xfer's sequence word (pinned, fine-grained)
+    uint32_t* h_flag_d = nullptr;
+    uint32_t xseq = 0;
+    // host phases of the plan calls (us): reset_ctl, enqueue, wait for the batch, the rest of
+    // kb_engine_plan (log conversion); [4] calls (kb_engine_host_timings, diagnostic)
+    double host_us[5] = {0, 0, 0, 0, 0};
+    // a k_pair step workgroup timed out waiting for its grid (never expected): the engine
+    // refuses further work (its arrival count was reset, but a plan may have been cut short)
+    bool dead = false;
+    unsigned long long pair_wait_ticks = 200000000ull;   // k_pair's wait bound: 2 s of the 100 MHz clock
     std::string last_err;
 };
 
 // ------------------------------------------------------------ helpers
+
+static double now_us() {
+    return 1e-3 * (double)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                      std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// after a k_pair timeout (run_steps) every step entry point refuses with this
+static int dead_result(kb_engine* e) {
+    e->last_err = "engine unusable: an earlier fused scan + step launch timed out waiting for its grid";
+    return KB_ERR_HIP;
+}
 
 static std::string part_string(kb_engine* e, int64_t p, const std::vector<int64_t>& reps) {
     std::string t = p < (int64_t)e->topics.size() ? e->topics[p] : std::string();
@@ -559,6 +587,7 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
                   full_shard && e->nscan > 1 && e->twaves == SCAN_THREADS / 64;
         if (const char* v = getenv("KB_FUSE")) e->fuse = e->fuse && *v != '0';                      // A/B
         if (const char* v = getenv("KB_FUSE_PRE")) e->fuse_pre = *v != '0';                          // diagnostic
+        if (const char* v = getenv("KB_PAIR_WAIT_TICKS")) e->pair_wait_ticks = strtoull(v, nullptr, 10);   // tests
         if (e->fuse) {
             e->pair_lds = std::max(e->scan_lds, (size_t)e->step_lds_bytes);
             int pst = 0;
@@ -618,7 +647,14 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
     if (!hbd.empty()) HIPCHK(hipMemcpy(e->bdesc, hbd.data(), hbd.size() * sizeof(BlockDesc), hipMemcpyHostToDevice));
     e->logcap = 1024;
     HIPCHK(dalloc(&e->log, e->logcap));
-    HIPCHK(hipHostMalloc((void**)&e->h_ctl, sizeof(DevCtl), hipHostMallocDefault));
+    // the pinned mirror of the control block (fine-grained and mapped: k_xfer writes and
+    // reads it directly) and k_xfer's sequence word
+    HIPCHK(hipHostMalloc((void**)&e->h_ctl, sizeof(DevCtl), hipHostMallocCoherent | hipHostMallocMapped));
+    HIPCHK(hipHostGetDevicePointer((void**)&e->h_ctl_d, e->h_ctl, 0));
+    HIPCHK(hipHostMalloc((void**)&e->h_flag, 64, hipHostMallocCoherent | hipHostMallocMapped));
+    HIPCHK(hipHostGetDevicePointer((void**)&e->h_flag_d, e->h_flag, 0));
+    *e->h_flag = 0;
+    if (const char* v = getenv("KB_XFER")) e->xfer = std::min(2, std::max(0, atoi(v)));      // A/B
     HIPCHK(hipMemcpy(e->w, hw.data(), hw.size() * 8, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(e->meta, hm.data(), hm.size() * 4, hipMemcpyHostToDevice));
     if (!e->lds_sets) {
@@ -741,7 +777,7 @@ static void fill_step_args(kb_engine* e, StepArgs& a, const Recs& R, int use_spi
     a.nsets = (int)e->nsets; a.NP2 = e->NP2;
     a.sb_lds = e->sb_lds; a.lds_bytes = e->step_lds_bytes;
     a.gscr = e->gscr;
-    a.wait_cnt = e->pair_cnt; a.wait_n = 0; a.fuse_pre = 1;
+    a.wait_cnt = e->pair_cnt; a.wait_n = 0; a.fuse_pre = 1; a.wait_ticks = e->pair_wait_ticks;
     a.setbits = e->setbits; a.setrec = e->setrec;
     a.order = e->order; a.posu = e->posu; a.blm = e->blm; a.posm = e->posm; a.r = e->r;
     a.load = e->load; a.lerr = e->lerr; a.eb = e->eb; a.bfl = e->bfl; a.cnt = e->cnt;
@@ -968,7 +1004,14 @@ static int reset_ctl(kb_engine* e, int64_t budget_steps) {
     const long long bud = (long long)c.steps + budget_steps;
     c.budget = bud > 0x7FFFFFFF ? 0x7FFFFFFF : (int32_t)bud;
     *e->h_ctl = c;
-    HIPCHK(hipMemcpyAsync(e->ctl, e->h_ctl, sizeof c, hipMemcpyHostToDevice, e->st));
+    if (e->xfer) {
+        // (k_xfer reads the mirror when it runs: nothing writes it before the batch's end)
+        XferArgs x{};
+        x.src[0] = (const uint32_t*)e->h_ctl_d; x.dst[0] = (uint32_t*)e->ctl; x.n[0] = (int)(sizeof(DevCtl) / 4);
+        launch_xfer(x, e->st);
+    } else {
+        HIPCHK(hipMemcpyAsync(e->ctl, e->h_ctl, sizeof c, hipMemcpyHostToDevice, e->st));
+    }
     return KB_OK;
 }
 
@@ -1090,13 +1133,17 @@ static int run_steps(kb_engine* e, int64_t max_steps) {
         if (e->h_log) hipHostFree(e->h_log);
         e->h_log = nullptr;
         e->h_logcap = 0;
-        HIPCHK(hipHostMalloc((void**)&e->h_log, (size_t)e->logcap * sizeof(ChangeDev), hipHostMallocDefault));
+        HIPCHK(hipHostMalloc((void**)&e->h_log, (size_t)e->logcap * sizeof(ChangeDev),
+                             hipHostMallocCoherent | hipHostMallocMapped));
+        HIPCHK(hipHostGetDevicePointer((void**)&e->h_log_d, e->h_log, 0));
         e->h_logcap = e->logcap;
     }
     // (kb_engine_step: the scan records of a masked step that changed nothing describe the
     // state still; the first pair reuses them)
     bool reuse = e->reuse_now && e->h_ctl->prepped;
+    const double t_r0 = now_us();
     if (const int rc = reset_ctl(e, max_steps); rc != KB_OK) { e->reuse_now = false; return rc; }
+    e->host_us[0] += now_us() - t_r0;
     e->reuse_now = false;
     reuse = reuse && e->h_ctl->prepped && e->h_ctl->halted == H_RUN;
     const int steps0 = e->h_ctl->steps;
@@ -1109,6 +1156,7 @@ static int run_steps(kb_engine* e, int64_t max_steps) {
         const int64_t pairs = std::min<int64_t>(e->batch, max_steps - done + (prepped ? 0 : 1));
         const int lp0 = e->h_ctl->logpos;
         const int st0 = e->h_ctl->steps;
+        const double t_b0 = now_us();
         roctxRangePush("kb:batch (scan + step pairs)");
         for (int64_t s = 0; s < pairs; s++) {
             // pair 0 ran the full prep; once a step had to re-scan (no surviving best
@@ -1129,13 +1177,51 @@ static int run_steps(kb_engine* e, int64_t max_steps) {
         HIPCHK(hipEventRecord(e->ev1, e->st));
         // the control block and this batch's log entries (at most one per pair) come
         // back with one synchronisation
-        HIPCHK(hipMemcpyAsync(e->h_ctl, e->ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, e->st));
         const int64_t ln = std::min<int64_t>(pairs, (int64_t)e->logcap - lp0);
-        if (ln > 0)
-            HIPCHK(hipMemcpyAsync(e->h_log + lp0, e->log + lp0, (size_t)ln * sizeof(ChangeDev),
-                                  hipMemcpyDeviceToHost, e->st));
-        HIPCHK(hipStreamSynchronize(e->st));
+        const double t_enq = now_us();
+        if (e->xfer) {
+            XferArgs x{};
+            x.src[0] = (const uint32_t*)e->ctl; x.dst[0] = (uint32_t*)e->h_ctl_d; x.n[0] = (int)(sizeof(DevCtl) / 4);
+            if (ln > 0) {
+                x.src[1] = (const uint32_t*)(e->log + lp0); x.dst[1] = (uint32_t*)(e->h_log_d + lp0);
+                x.n[1] = (int)(ln * (int64_t)(sizeof(ChangeDev) / 4));
+            }
+            if (e->xfer == 2) { x.flag = e->h_flag_d; x.seq = ++e->xseq; }
+            launch_xfer(x, e->st);
+            HIPCHK(hipGetLastError());
+            if (e->xfer == 2) {
+                // poll the sequence word k_xfer stores after its copies (system-scope release);
+                // past 2 ms of polling (long batches, or a failed launch) wait on the stream
+                const double t0 = now_us();
+                bool seen = false;
+                for (int it = 0;; it++) {
+                    if (__atomic_load_n(e->h_flag, __ATOMIC_ACQUIRE) == x.seq) { seen = true; break; }
+                    if ((it & 255) == 255 && now_us() - t0 > 2000.0) break;
+                }
+                if (!seen) HIPCHK(hipStreamSynchronize(e->st));
+            } else {
+                HIPCHK(hipStreamSynchronize(e->st));
+            }
+        } else {
+            HIPCHK(hipMemcpyAsync(e->h_ctl, e->ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, e->st));
+            if (ln > 0)
+                HIPCHK(hipMemcpyAsync(e->h_log + lp0, e->log + lp0, (size_t)ln * sizeof(ChangeDev),
+                                      hipMemcpyDeviceToHost, e->st));
+            HIPCHK(hipStreamSynchronize(e->st));
+        }
+        e->host_us[1] += t_enq - t_b0;
+        e->host_us[2] += now_us() - t_enq;
         roctxRangePop();
+        if (e->h_ctl->logpos > lp0 && e->h_ctl->logpos <= e->logcap &&
+            e->h_log[e->h_ctl->logpos - 1].err_code == E_PAIR_TIMEOUT) {
+            // a step workgroup gave up waiting for its grid: the stragglers still counted
+            // themselves in, so the arrival count is reset once the stream is idle, and the
+            // engine takes no more work (the error is returned with this batch's log)
+            HIPCHK(hipStreamSynchronize(e->st));
+            HIPCHK(hipMemsetAsync(e->pair_cnt, 0, PAIR_SHARDS * PAIR_STRIDE * 4, e->st));
+            HIPCHK(hipStreamSynchronize(e->st));
+            e->dead = true;
+        }
         fresh = true;
         reuse = false;
         harvest(e);
@@ -1196,6 +1282,7 @@ extern "C" int kb_engine_step(kb_engine* e, uint32_t step_mask, kb_change* out) 
         out->from_broker = out->to_broker = out->err_broker = -1;
         return KB_NOCHANGE;
     };
+    if (e->dead) return dead_result(e);
     if (e->pending) {
         // a validation error (create): returned by its own step and by every later one (the
         // engine holds no state past a failed validation); earlier steps change nothing
@@ -1239,6 +1326,8 @@ extern "C" int kb_engine_plan(kb_engine* e, int64_t max_steps, kb_change* out, i
     *n_out = 0;
     if (max_steps == 0) return KB_NOCHANGE;
     if (e->pending) { if (out) pending_result(e, out); *n_out = 1; return e->pending; }
+    if (e->dead) return dead_result(e);
+    e->host_us[4] += 1;
     for (int k = 0; k < TK_N; k++) { e->kms[k] = 0; e->klaunch[k] = 0; }
     e->tev_used = 0;
     e->last_ms = 0;
@@ -1250,12 +1339,14 @@ extern "C" int kb_engine_plan(kb_engine* e, int64_t max_steps, kb_change* out, i
         const int64_t m = std::min<int64_t>(max_steps - k, kLogChunk);
         const int nlog = run_steps(e, m);
         if (nlog < 0) { *n_out = k; return nlog; }
+        const double t_c0 = now_us();
         for (int64_t i = 0; i < nlog; i++) {         // (run_steps copied the log entries)
             kb_change tmp;
             rc = convert(e, e->h_log[i], out ? &out[k] : &tmp);
             k++;
-            if (rc != KB_CHANGE) { *n_out = k; return rc; }
+            if (rc != KB_CHANGE) { *n_out = k; e->host_us[3] += now_us() - t_c0; return rc; }
         }
+        e->host_us[3] += now_us() - t_c0;
         if (nlog < m) break;
     }
     *n_out = k;
@@ -1387,9 +1478,19 @@ extern "C" int kb_engine_timings(kb_engine* e, double* ms, int64_t* launches, in
     return TK_N + 5;
 }
 
+// diagnostic: cumulative host phases of the plan calls since the last kb_engine_set_timing
+// (us): [0] reset_ctl, [1] enqueue of the batches, [2] waiting for them (the batch-end
+// transfer included), [3] log conversion, [4] kb_engine_plan calls
+extern "C" int kb_engine_host_timings(kb_engine* e, double* us, int n) {
+    if (!e || !us) return KB_ERR_INVALID;
+    for (int k = 0; k < 5 && k < n; k++) us[k] = e->host_us[k];
+    return 5;
+}
+
 extern "C" int kb_engine_set_timing(kb_engine* e, int32_t on) {
     if (e) { e->ctl_mirror = false; e->recs_fresh = false; }            // (the device block changes behind the host copy)
     if (!e) return KB_ERR_INVALID;
+    for (double& v : e->host_us) v = 0;
     HIPCHK(hipStreamSynchronize(e->st));
     e->tev_used = 0;
     for (int k = 0; k < TK_N; k++) { e->kms[k] = 0; e->klaunch[k] = 0; }
@@ -1547,6 +1648,7 @@ extern "C" void kb_engine_destroy(kb_engine* e) {
                     e->L.lstart, e->L.llen, e->L.lcap, e->L.lent, e->L.ck, e->L.dpos, e->rf_dev};
     for (void* p : ptrs) if (p) hipFree(p);
     if (e->h_ctl) hipHostFree(e->h_ctl);
+    if (e->h_flag) hipHostFree(e->h_flag);
     if (e->h_log) hipHostFree(e->h_log);
     if (e->ev0) hipEventDestroy(e->ev0);
     if (e->ev1) hipEventDestroy(e->ev1);
@@ -1618,6 +1720,7 @@ extern "C" int kb_engine_set_stream(kb_engine* e, void* s) {
 extern "C" int kb_engine_step_begin(kb_engine* e, void* summary_dev) {
     if (e) { e->ctl_mirror = false; e->recs_fresh = false; }            // (the device block changes behind the host copy)
     if (!e || !summary_dev) return KB_ERR_INVALID;
+    if (e->dead) return dead_result(e);
     if (e->pending) return e->pending;
     if (const int rc = reset_ctl(e, 1); rc != KB_OK) return rc;
     if (!e->h_ctl->prepped) enqueue_step(e);       // prep only (nothing to resolve yet)
@@ -1636,6 +1739,7 @@ extern "C" int kb_engine_step_begin(kb_engine* e, void* summary_dev) {
 extern "C" int kb_engine_sharded_reset(kb_engine* e, int64_t budget_steps) {
     if (e) { e->ctl_mirror = false; e->recs_fresh = false; }            // (the device block changes behind the host copy)
     if (!e || budget_steps < 1) return KB_ERR_INVALID;
+    if (e->dead) return dead_result(e);
     if (e->pending) return e->pending;
     if (const int rc = reset_ctl(e, budget_steps); rc != KB_OK) return rc;
     if (!e->h_ctl->prepped) enqueue_step(e);       // prep only (nothing to resolve yet)

@@ -1516,11 +1516,13 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
             const unsigned long long t0 = wall_clock64();
             int to = 0;
             for (;;) {
+                // (the bound is tested first: a zero bound -- the tests' forced timeout --
+                // gives up before the first poll)
+                if (wall_clock64() - t0 >= a.wait_ticks) { to = 1; break; }
                 const uint32_t v = lane < PAIR_SHARDS
                     ? __hip_atomic_load(a.wait_cnt + lane * PAIR_STRIDE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
                 if (wave_sum(v) >= (uint32_t)a.wait_n) break;
                 __builtin_amdgcn_s_sleep(1);
-                if (wall_clock64() - t0 > 200000000ull) { to = 1; break; }
             }
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // (the other XCDs' writes)
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -3734,6 +3736,11 @@ __global__ __launch_bounds__(1024) void k_summary(SumArgs a) {
     RecHdr* out = a.out.h(0);
     Contender* okeys = a.out.k(0);
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    // a halted batch: the rounds after the halt are no-ops (k_step returns at once), and
+    // the summary is left as the halted round wrote it, so the gathered flags every rank
+    // reads when it grows its summaries (grow_summary: bit 2, a spill it can still grow)
+    // are that round's, whichever round of the batch halted
+    if (!(ctl->halted == H_RUN && ctl->prepped)) return;
     __shared__ uint32_t s_key[DEDUP_STEP];
     __shared__ unsigned long long s_wb[DEDUP_STEP], s_it[DEDUP_STEP];
     __shared__ uint32_t s_n, s_fail;
@@ -4012,6 +4019,28 @@ void launch_refresh(const RefreshArgs& a, hipStream_t st) {
 }
 void launch_summary(const SumArgs& a, hipStream_t st) {
     hipLaunchKernelGGL(k_summary, dim3(1), dim3(1024), 0, st, a);
+}
+
+// Control-block / step-log transfers between the device and the host's pinned
+// (fine-grained, mapped) mirror as one small kernel on the engine's stream instead of
+// hipMemcpyAsync: a copy engine round trip costs more than a one-workgroup launch, and a
+// kernel in the stream needs no cross-engine dependency.  Plain vector loads / stores;
+// with a flag, the copies are released to system scope before the flag's store, so the
+// host may read them as soon as it sees the sequence number.
+__global__ void __launch_bounds__(256) k_xfer(XferArgs a) {
+    const int tid = threadIdx.x;
+    for (int k = 0; k < 2; k++)
+        for (int i = tid; i < a.n[k]; i += 256) a.dst[k][i] = a.src[k][i];
+    if (!a.flag) return;
+    __syncthreads();
+    if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        __hip_atomic_store(a.flag, a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+void launch_xfer(const XferArgs& a, hipStream_t st) {
+    hipLaunchKernelGGL(k_xfer, dim3(1), dim3(256), 0, st, a);
 }
 
 }  // namespace kbe

@@ -120,6 +120,7 @@ struct StepArgs {
     uint32_t* wait_cnt;       // k_pair's step workgroup: waits until *wait_cnt == wait_n (the
     int wait_n;               //    grid's other workgroups), then resets it
     int fuse_pre;             // k_pair: stage the broker tables before the wait (diagnostic 0: after)
+    unsigned long long wait_ticks;   // k_pair: the wait's bound (100 MHz ticks; 2 s, tests: 0)
 };
 
 
@@ -146,5 +147,16 @@ void launch_touch(double* r, int B, int32_t* blm, int32_t* posm, uint4* setrec, 
 void launch_listop(DevCtl* ctl, const Lists& L, hipStream_t st);
 void launch_refresh(const RefreshArgs& a, hipStream_t st);
 void launch_summary(const SumArgs& a, hipStream_t st);
+
+// k_xfer: up to two 32-bit word copies (device <-> the host's mapped pinned mirror), then,
+// if flag is set, a system-scope release and *flag = seq (the host waits on it)
+struct XferArgs {
+    const uint32_t* src[2];
+    uint32_t* dst[2];
+    int n[2];
+    uint32_t* flag;
+    uint32_t seq;
+};
+void launch_xfer(const XferArgs& a, hipStream_t st);
 
 }  // namespace kbe

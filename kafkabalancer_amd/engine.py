@@ -28,7 +28,8 @@ EXPORTS = ["kb_abi_version", "kb_engine_create", "kb_engine_balance", "kb_engine
            "kb_engine_last_error", "kb_engine_destroy", "kb_engine_summary_bytes",
            "kb_engine_step_begin", "kb_engine_step_finish", "kb_engine_set_stream",
            "kb_engine_sharded_reset", "kb_engine_sharded_scan", "kb_engine_sharded_resolve",
-           "kb_engine_sharded_collect", "kb_engine_set_incremental", "kb_engine_step"]
+           "kb_engine_sharded_collect", "kb_engine_set_incremental", "kb_engine_step",
+           "kb_engine_host_timings"]
 
 P64 = C.POINTER(C.c_int64)
 PD = C.POINTER(C.c_double)
@@ -97,6 +98,9 @@ def lib():
         L.kb_engine_stats.restype = C.c_int
         L.kb_engine_timings.argtypes = [vp, PD, P64, C.c_int]
         L.kb_engine_timings.restype = C.c_int
+        if hasattr(L, "kb_engine_host_timings"):        # (diagnostic; older builds in A/B runs lack it)
+            L.kb_engine_host_timings.argtypes = [vp, PD, C.c_int]
+            L.kb_engine_host_timings.restype = C.c_int
         L.kb_engine_set_timing.argtypes = [vp, C.c_int32]
         L.kb_engine_set_timing.restype = C.c_int
         L.kb_engine_stamps.argtypes = [vp, P64, C.c_int]
@@ -130,7 +134,7 @@ def lib():
         if hasattr(L, "kb_engine_set_incremental"):
             L.kb_engine_set_incremental.argtypes = [vp, C.c_int32]
             L.kb_engine_set_incremental.restype = C.c_int
-        if L.kb_abi_version() != 8 and not any_abi:
+        if L.kb_abi_version() != 9 and not any_abi:
             raise ImportError("libkbengine.so ABI mismatch")
         _lib = L
     return _lib
@@ -231,6 +235,8 @@ class Engine:
     def __init__(self, cluster, cfg, semantics=KB_SEM_APPLIED, device=0, shard=None, list_slack=0,
                  exact_unbalance=False, time_kernels=False, incremental=False):
         L = lib()
+        self._cap = 1024                  # plan_raw's change buffer (grown by doubling)
+        self._buf = (kb_change * self._cap)()
         if not isinstance(cluster, ClusterSoA):
             cluster = ClusterSoA.from_plist(cluster)
         self.cluster = cluster
@@ -299,7 +305,14 @@ class Engine:
         if isinstance(mask, str):
             mask = [mask]
         if not isinstance(mask, int):
-            mask = sum(1 << STEP_NAMES.index(n) for n in mask)
+            bits = 0
+            for n in mask:
+                if n not in STEP_NAMES:
+                    raise ValueError("unknown step %r" % (n,))
+                bits |= 1 << STEP_NAMES.index(n)      # (a repeated name sets its bit once)
+            mask = bits
+        if not 0 <= mask <= KB_STEPS_ALL:
+            raise ValueError("step mask %#x outside the steps table (0..%#x)" % (mask, KB_STEPS_ALL))
         ch = kb_change()
         rc = lib().kb_engine_step(self.h, mask, C.byref(ch))
         if rc == KB_NOCHANGE:
@@ -313,11 +326,17 @@ class Engine:
         return self.changes(*self.plan_raw(max_steps))
 
     def plan_raw(self, max_steps):
-        """The plan call alone (the bench's timed region): (kb_change array, n, rc)."""
-        buf = (kb_change * max(1, max_steps))()
+        """The plan call alone (the bench's timed region): (kb_change buffer, n, rc).  The
+        buffer is the engine's own and is reused by the next plan_raw: read it (changes())
+        first.  (A ctypes array type of a new length costs 15-25 us to create, so the
+        buffer keeps one type per capacity and grows by doubling.)"""
+        if max_steps > self._cap:
+            while self._cap < max_steps:
+                self._cap *= 2
+            self._buf = (kb_change * self._cap)()
         n = C.c_int64()
-        rc = lib().kb_engine_plan(self.h, max_steps, buf, C.byref(n))
-        return buf, n.value, rc
+        rc = lib().kb_engine_plan(self.h, max_steps, self._buf, C.byref(n))
+        return self._buf, n.value, rc
 
     def changes(self, buf, n, rc):
         """plan_raw's result as (changes, error_or_None)."""
@@ -372,6 +391,12 @@ class Engine:
         rc = lib().kb_engine_set_timing(self.h, 2 if on == 2 else int(bool(on)))
         if rc != 0:
             raise EngineError(rc, self.last_error())
+
+    def host_timings(self):
+        """Diagnostic: host phases of the plan calls since set_timing (us) and their count."""
+        us = np.zeros(5)
+        lib().kb_engine_host_timings(self.h, us.ctypes.data_as(PD), 5)
+        return {"reset": us[0], "enqueue": us[1], "wait": us[2], "convert": us[3], "calls": int(us[4])}
 
     def stamps(self):
         """Diagnostic build only: accumulated phase ticks (100 MHz) of the k_step phases."""

@@ -379,21 +379,39 @@ static int g_window;                      /* see or_set_window (move_window) */
  * (utils.go:81-90): a replica always has a load, so that is a replica outside p.Brokers.
  * One hash set per distinct Brokers slice; O(P R) instead of the list intersections. */
 static int64_t first_disallowed(const or_plist *pl) {
-    const int64_t *key = NULL;
-    int has_key = 0;
-    lmap set; lm_init(&set, 64);
+    /* dense ids of every broker named by a Brokers slice, one bitmap per distinct slice
+       (keyed by its backing array: partitions share the slice FillDefaults gave them) */
+    lmap ids; lm_init(&ids, 64);
+    lmap keys; lm_init(&keys, 64);
+    for (int64_t i = 0; i < pl->n; i++) {
+        const or_partition *p = &pl->parts[i];
+        if (lm_find(&keys, (int64_t)(intptr_t)p->brokers.a) >= 0) continue;
+        lm_slot(&keys, (int64_t)(intptr_t)p->brokers.a);
+        for (int64_t q = 0; q < p->brokers.len; q++) lm_slot(&ids, p->brokers.a[q]);
+    }
+    const int64_t W = (ids.n + 63) / 64 + 1;
+    uint64_t *bits = (uint64_t *)calloc((size_t)(keys.n * W + 1), sizeof(uint64_t));
+    for (int64_t i = 0; i < pl->n; i++) {
+        const or_partition *p = &pl->parts[i];
+        const int32_t j = lm_find(&keys, (int64_t)(intptr_t)p->brokers.a);
+        uint64_t *b = bits + (int64_t)j * W;
+        if (b[W - 1]) continue;                       /* (word W-1: this slice is done) */
+        for (int64_t q = 0; q < p->brokers.len; q++) {
+            const int64_t k = lm_find(&ids, p->brokers.a[q]);
+            b[k >> 6] |= 1ull << (k & 63);
+        }
+        b[W - 1] = 1;
+    }
     int64_t first = pl->n;
     for (int64_t i = 0; i < pl->n && first == pl->n; i++) {
         const or_partition *p = &pl->parts[i];
-        if (!has_key || p->brokers.a != key) {
-            lm_free(&set); lm_init(&set, p->brokers.len + 1);
-            for (int64_t q = 0; q < p->brokers.len; q++) lm_slot(&set, p->brokers.a[q]);
-            key = p->brokers.a; has_key = 1;
+        const uint64_t *b = bits + (int64_t)lm_find(&keys, (int64_t)(intptr_t)p->brokers.a) * W;
+        for (int64_t r = 0; r < p->replicas.len; r++) {
+            const int64_t k = lm_find(&ids, p->replicas.a[r]);
+            if (k < 0 || !((b[k >> 6] >> (k & 63)) & 1ull)) { first = i; break; }
         }
-        for (int64_t r = 0; r < p->replicas.len; r++)
-            if (lm_find(&set, p->replicas.a[r]) < 0) { first = i; break; }
     }
-    lm_free(&set);
+    free(bits); lm_free(&ids); lm_free(&keys);
     return first;
 }
 
@@ -589,11 +607,17 @@ static int move_window(const or_plist *pl, const or_config *cfg, int leaders, bl
     uint64_t *bits = NULL;
     const int64_t **skey = NULL;
     int64_t nset = 0, setcap = 0, last = -1;
+    lmap kmap; lm_init(&kmap, 64);                  /* slice backing array -> set index */
     for (int64_t i = 0; i < np; i++) {
         const int64_t *key = pl->parts[i].brokers.a;
         int64_t j = last >= 0 && skey[last] == key ? last : -1;
-        for (int64_t q = 0; j < 0 && q < nset; q++) if (skey[q] == key) j = q;
         if (j < 0) {
+            const int32_t q = lm_find(&kmap, (int64_t)(intptr_t)key);
+            if (q >= 0) j = (int64_t)kmap.loads[q];
+        }
+        if (j < 0) {
+            const int32_t q = lm_slot(&kmap, (int64_t)(intptr_t)key);
+            kmap.loads[q] = (double)nset;
             if (nset == setcap) {
                 setcap = setcap ? 2 * setcap : 16;
                 skey = (const int64_t **)realloc((void *)skey, (size_t)setcap * sizeof(int64_t *));
@@ -612,6 +636,22 @@ static int move_window(const or_plist *pl, const or_config *cfg, int leaders, bl
         sidx[i] = (int32_t)j;
         last = j;
     }
+    int64_t *setcnt = (int64_t *)malloc((size_t)(nset ? nset : 1) * sizeof(int64_t));
+    for (int64_t j = 0; j < nset; j++) {
+        setcnt[j] = 0;
+        for (int64_t q = 0; q < W; q++) setcnt[j] += __builtin_popcountll(bits[j * W + q]);
+    }
+    /* Early stop of a slot's target walk (n >= 64 only).  For a fixed source the real value
+       of the O(1) score is h(L_t) = f((L_t + w)/avg - 1) - f(L_t/avg - 1) plus constants, and
+       h is nondecreasing in L_t (f is convex); targets come in bl order, i.e. ascending L_t.
+       The computed score is within d of that real value: w/avg <= L_s/avg = 1 + r_s, so
+       every term is at most 3 (V + 1) and its argument errs by ~2 u (|x| + 1); with the four
+       adds d <= 100 u (V + |su| + 1) < eps / 2 once n >= 64 (eps is 16 (n + 1) u
+       (V + |su| + 1) >= 1040 u (...)).  So a computed score above best + 3 eps puts the real
+       value of this and every later target above best + 2.5 eps and their computed scores
+       above best + 2 eps: outside the window (best only falls, so the thread's running best
+       is conservative). */
+    const int walk = n >= 64;
     int T = g_threads < 1 ? 1 : g_threads;
     if (T > np) T = np > 0 ? (int)np : 1;
     wlist *TL = (wlist *)calloc((size_t)T, sizeof(wlist));
@@ -636,21 +676,33 @@ static int move_window(const or_plist *pl, const or_config *cfg, int leaders, bl
             }
             const uint64_t *b = bits + (int64_t)sidx[i] * W;
             const double w = p->weight;
+            /* candidates of one slot = set members minus the partition's replicas (distinct:
+               ValidateReplicas ran) */
+            int64_t nin = 0;
+            for (int64_t q = 0; q < nr; q++) nin += rk[q] >= 0 && ((b[rk[q] >> 6] >> (rk[q] & 63)) & 1ull);
             for (int64_t s = lo; s < hi; s++) {
                 const int64_t ridx = s < 64 ? rk[s] : -1;
                 if (ridx < 0) { terr[t] = 2; break; }
                 const double ds = f_unb((bl[ridx].load - w) / avg - 1.0) - fr[ridx];
-                for (int64_t k = 0; k < n; k++) {
-                    if (!((b[k >> 6] >> (k & 63)) & 1ull)) continue;
-                    int isrep = 0;
-                    for (int64_t q = 0; q < nr; q++) isrep |= rk[q] == k;
-                    if (isrep) continue;
-                    const double ua = su + ds + (f_unb((bl[k].load + w) / avg - 1.0) - fr[k]);
-                    tcnt[t]++;
-                    if (ua <= L->best + 2 * eps) {
-                        wcand c = {ua, i, s, k, ridx};
-                        wl_push(L, c);
-                        if (ua < L->best) L->best = ua;
+                tcnt[t] += setcnt[sidx[i]] - nin;
+                /* targets in bl order = ascending load: set bits word by word */
+                for (int64_t wd = 0, stop = 0; wd < W && !stop; wd++) {
+                    uint64_t m = b[wd];
+                    while (m) {
+                        const int64_t k = wd * 64 + __builtin_ctzll(m);
+                        m &= m - 1;
+                        int isrep = 0;
+                        for (int64_t q = 0; q < nr; q++) isrep |= rk[q] == k;
+                        if (isrep) continue;
+                        const double ua = su + ds + (f_unb((bl[k].load + w) / avg - 1.0) - fr[k]);
+                        if (ua <= L->best + 2 * eps) {
+                            wcand c = {ua, i, s, k, ridx};
+                            wl_push(L, c);
+                            if (ua < L->best) L->best = ua;
+                        } else if (walk && ua > L->best + 3 * eps) {
+                            stop = 1;          /* every later target scores above the window */
+                            break;
+                        }
                     }
                 }
             }
@@ -686,7 +738,7 @@ static int move_window(const or_plist *pl, const or_config *cfg, int leaders, bl
         fprintf(stderr, "window: eps %.3g best %.17g listed %lld folded %lld\n", eps, best, (long long)tot, (long long)in);
     }
     for (int t = 0; t < T; t++) free(TL[t].v);
-    free(TL); free(tcnt); free(terr); free(fr); free(bits); free((void *)skey); free(sidx); lm_free(&pos);
+    free(TL); free(tcnt); free(terr); free(fr); free(bits); free(setcnt); lm_free(&kmap); free((void *)skey); free(sidx); lm_free(&pos);
     return err;
 }
 

@@ -93,12 +93,20 @@ CASES = {
                    dict(O.default_cfg(), min_unbalance=0.0), 30),
     "b12000_uniform": (dict(P=40000, B=12000, rf=3, weights="uniform", seed=0x5EEDC000),
                        dict(O.default_cfg(), min_unbalance=0.0), 12),
+    # the benchmarked plans end to end: BASELINE.json configs[2]'s whole 1000-move plan (the
+    # headline, -allow-leader), the same cluster's 1000 MoveNonLeaders steps without
+    # -allow-leader, and configs[4] (c5) over the 200 steps bench.py times there; their
+    # first 20 / 20 / 12 steps are c3_full, c3nl_full and c5_full (tests/test_golden_scale.py)
+    "c3_full1000": (dict(config="c3", scale=1.0), None, 1000),
+    "c3nl_1000": (dict(config="c3", scale=1.0), dict(O.default_cfg(), min_unbalance=0.0), 1000),
+    "c5_200": (dict(config="c5", scale=1.0), None, 200),
 }
 
 # cases generated with the oracle's windowed exact move() (or_set_window: the literal
 # loop's result, tests/test_oracle.py::test_windowed_oracle_*; the literal loop would take
 # hours to days per step at these sizes)
-WINDOWED = {"c3nl_full", "b4096_50k", "c5_full", "b6000_zipf", "b8000_sets", "b16384_int", "b12000_uniform"}
+WINDOWED = {"c3nl_full", "b4096_50k", "c5_full", "b6000_zipf", "b8000_sets", "b16384_int", "b12000_uniform",
+            "c3_full1000", "c3nl_1000", "c5_200"}
 
 
 def build(params):

@@ -64,3 +64,54 @@ def test_small_shard_keeps_two_launches():
     eng = E.Engine(cl, cfg)
     assert eng.stats()["fused_pairs"] == 0
     eng.close()
+
+
+def _with_env(name, value, fn):
+    old = os.environ.get(name)
+    os.environ[name] = value
+    try:
+        return fn()
+    finally:
+        if old is None:
+            del os.environ[name]
+        else:
+            os.environ[name] = old
+
+
+def test_pair_timeout_poisons_engine():
+    """k_pair's step workgroup gives up waiting for its grid (forced: a zero wait bound):
+    the plan stops with the explicit error, the arrival count is reset once the stream is
+    idle, and the engine refuses further plans; a new engine then plans normally."""
+    cl, cfg, _ = synth.config("c3", scale=1.0)          # (fused only with full scan tiles)
+    eng = _with_env("KB_PAIR_WAIT_TICKS", "0", lambda: E.Engine(cl, cfg))
+    assert eng.stats()["fused_pairs"] == 1
+    changes, err = eng.plan(5)
+    assert err is not None and "timed out" in str(err), err
+    changes, err = eng.plan(5)
+    assert changes == [] and err is not None and "unusable" in str(err), err
+    with pytest.raises(E.EngineError) as ei:
+        eng.balance()
+    assert "unusable" in str(ei.value)
+    eng.close()
+    ref = E.Engine(cl, cfg)
+    want, err = ref.plan(20)
+    assert err is None and len(want) == 20
+    ref.close()
+
+
+@pytest.mark.parametrize("mode", ["0", "1"])
+def test_control_transfer_modes_match(mode):
+    """The batch-end control-block / log transfer (k_xfer polled by the host, the default)
+    against a k_xfer with a stream synchronisation and hipMemcpyAsync (KB_XFER=1 / 0): the
+    same plans and loads bit for bit, across several batches and kb_engine_balance calls."""
+    cl, cfg, _ = synth.config("c3", scale=1.0)
+    a = run(cl, cfg, 150, True)
+    b = _with_env("KB_XFER", mode, lambda: run(cl, cfg, 150, True))
+    assert keyed(a[0]) == keyed(b[0])
+    assert a[3] == b[3]
+    eng = _with_env("KB_XFER", mode, lambda: E.Engine(cl, cfg))
+    ref = E.Engine(cl, cfg)
+    for _ in range(5):
+        assert keyed([eng.balance()]) == keyed([ref.balance()])
+    eng.close()
+    ref.close()

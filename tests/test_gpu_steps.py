@@ -252,3 +252,47 @@ def test_table_walk_at_scale_matches_plan(workload):
     assert eng.loads() == ref.loads()
     ref.close()
     eng.close()
+
+
+@pytest.mark.parametrize("shape", ["c3", "zipf4096"])
+def test_table_walk_full_size_reuses_fused_records(shape):
+    """The scan-reuse path (a masked step that changed nothing leaves its scan records to the
+    next masked step, no second scan) on the production launches: c3 at full size (fused
+    k_pair launches) and 1M partitions x 4096 brokers, Zipf (fused launches with eager
+    refolds and fold checkpoints).  The host table walk equals kb_engine_plan change for
+    change, with bit-identical loads after it."""
+    if shape == "c3":
+        cl, cfg, _ = synth.config("c3", scale=1.0)
+        steps = 20
+    else:
+        cl = synth.make_cluster(1_000_000, 4096, 3, "zipf", seed=0x5EED5005)
+        cfg = {"allow_leader": False, "rebalance_leaders": False, "min_replicas": 2, "min_unbalance": 0.0,
+               "brokers": None}
+        steps = 12
+    ref = E.Engine(cl, cfg)
+    want, err = ref.plan(steps)
+    assert err is None, err
+    assert ref.stats()["fused_pairs"] == 1
+    eng = E.Engine(cl, cfg)
+    got = walk_table(eng, steps)
+    assert got == want
+    assert eng.loads() == ref.loads()
+    ref.close()
+    eng.close()
+
+
+def test_step_mask_names_combine_once():
+    """A repeated step name sets its bit once; unknown names and masks outside the table are
+    rejected before the C call."""
+    pl = golden("test.json")
+    eng = E.Engine(pl, default_cfg())
+    a = eng.step(["MoveNonLeaders", "MoveNonLeaders"])
+    eng2 = E.Engine(pl, default_cfg())
+    b = eng2.step(["MoveNonLeaders"])
+    assert a == b
+    with pytest.raises(ValueError):
+        eng.step(["MoveSideways"])
+    with pytest.raises(ValueError):
+        eng.step(1 << 9)
+    eng.close()
+    eng2.close()
