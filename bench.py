@@ -343,6 +343,9 @@ def main():
                     help="what a drop-in user pays: kb_engine_balance per call and the CLI end to end "
                          "(decode / create / plan / encode) on the workload's JSON; a separate line")
     ap.add_argument("--cli-reassign", type=int, default=1000)
+    ap.add_argument("--sharded", action="store_true",
+                    help="one GPU: the sharded protocol (RCCL all-gather per step, plan driven from C) at "
+                         "world size 1 against the plain plan over the same steps; a separate line")
     ap.add_argument("--step-alone", action="store_true",
                     help="diagnostic: k_step alone on a fixed input after the warm-up plan "
                          "(kb_engine_bench_step; with a -DKB_STOP_AT=k library: the cost up to phase k)")
@@ -385,7 +388,10 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         from kafkabalancer_amd import dist
-        return dist.bench_main(args, world, rank, local)
+        return dist.bench_main(args, world, rank, local, cpu_baseline=cpu_baseline)
+    if args.sharded:
+        from kafkabalancer_amd import dist
+        return dist.bench_world1(args)
 
     import torch
     from kafkabalancer_amd import engine as E
@@ -413,23 +419,53 @@ def main():
     cand = st1["candidates"] - st0["candidates"]
     dev_s = st1["device_ms"] / 1e3
     ms_per_step = 1e3 * wall / max(steps, 1)
-    # per-kernel durations over two more stretches of the same plan, outside the headline
-    # timing: (a) the device clock (scan workgroups and k_step stamp the 100 MHz clock):
-    # each launch's span from the end of the kernel before it to its own end -- dispatch
+    if args.stamps:
+        st = eng.stamps()
+        n = max(1, eng.stats()["steps"])       # every step since the engine was created
+        # (stamp ids as placed in kernels.hip; 6..20 name the fused incremental prep's phases)
+        names = ["prep.S+r+ubloop", "step.loads", "res.reduce", "res.pred", "res.move", "res.apply(tail)", "prep.P1", None,
+                 "prep.P2", "prep.P3", "prep.end", "res.move->apply", "loads.bro+ctl", "loads.rec_reduce", "loads.keys", None, "prep.P4",
+                 "eps.sync1", "eps.wave0red", "prep.positions", "prep.sets", "apply.loads", "apply.update"]
+        counts = {"waves_scored": 7, "waves_gated_in": 15, "emits": 31, "spills": 30, "walks": 29, "walk_steps": 28, "walk_global": 27}
+        mhz = 100.0 * st[25] / max(st[24], 1)           # shader clock (the phase stamps' unit)
+        names = names + ["loads.broker", None, None, "stamp.overhead", "loads.setbits", "loads.hdr"]
+        print(json.dumps({"k_step_clock_mhz": mhz,
+                          "k_step_us": st[24] / 100.0 / n,
+                          "stamps_us_per_step": {k: st[i] / mhz / n for i, k in enumerate(names) if k},
+                          "counts_per_step": {k: st[i] / n for k, i in counts.items()},
+                          "stats": eng.stats()}))
+        return
+    eng.close()
+    # per-kernel durations, outside the headline timing, over the SAME steps of the plan as
+    # the headline: a fresh engine replays the warm-up and the timed steps (the plan is
+    # deterministic), so the kernel figures describe the timed steps and a rocprofv3 trace
+    # of this command averages over those steps only (every stretch covers steps 0..W+K).
+    # (a) the device clock (scan workgroups and k_step stamp the 100 MHz clock): each
+    # launch's span from the end of the kernel before it to its own end -- dispatch
     # included, the interval rocprofv3 --kernel-trace reports, so the scan + step spans add
     # up to the step time (the roofline's figure) -- and the inner interval, first workgroup
     # start .. last end; (b) HIP events around every launch (each event adds its own
-    # ~2-3 us: an upper bound, a side figure)
-    kt_steps = min(args.steps, 200)
-    stk0 = eng.stats()
-    kdc = kernel_times(eng, kt_steps, 1)
-    stk1 = eng.stats()
-    kev = kernel_times(eng, kt_steps, 2)
+    # ~2-3 us: an upper bound, a side figure), on a third replay
+    kt_steps = steps
+
+    def replay(mode):
+        e = E.Engine(cl, cfg, device=0, time_kernels=False, incremental=incr)
+        if args.warmup:
+            _, err2 = e.plan(args.warmup)
+            assert err2 is None, err2
+        s0 = e.stats()
+        kt = kernel_times(e, kt_steps, mode)
+        s1 = e.stats()
+        iso = e.bench_scan(200) if (mode == 1 and args.isolated_scan) else None
+        e.close()
+        return kt, s0, s1, iso
+
+    kdc, stk0, stk1, scan_iso_us = replay(1)
+    kev, _, _, _ = replay(2)
     scan_us, scan_n = kdc["scan"]
     if not scan_n:                      # (no back-to-back launch: the inner interval)
         scan_us, scan_n = kdc["scan_inner"]
     scan_clock_us = kdc["scan_inner"][0]
-    scan_iso_us = eng.bench_scan(200) if args.isolated_scan else None
     bytes_scan = st1["scan_bytes"]
     if incr:
         # bytes the incremental scans actually read: their blocks' partition words
@@ -514,7 +550,7 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic (numpy PCG64 seed 0x5EED000%s), %s" % (args.workload[-1], weights),
+        "data": "synthetic (numpy PCG64 seed %#x), %s" % (synth.SEEDS[args.workload], weights),
         "config": dict(desc, parallelism="single-gpu", device_ms_per_step=1e3 * dev_s / max(steps, 1),
                        mode=args.mode, fused_pairs=fused),
         "roofline": roof,
@@ -524,25 +560,10 @@ def main():
         "incremental": ({"blocks_per_scan": (stk1["blocks_scanned"] - stk0["blocks_scanned"]) / max(kdc["scan_inner"][1], 1),
                          "blocks_total": (cl.n + 127) // 128} if incr else None),
         "kernel_timing_steps": kt_steps,
+        "kernel_timing_def": "fresh engines replay the warm-up and the same %d timed steps (device clock, then "
+                             "HIP events); every kernel figure describes the timed steps" % kt_steps,
         "engine_events": {k: st1[k] - st0[k] for k in ("retries", "refreshes", "exact_halts", "exact_folds")},
     }
-    if args.stamps:
-        st = eng.stamps()
-        n = max(1, eng.stats()["steps"])       # every step since the engine was created
-        # (stamp ids as placed in kernels.hip; 6..20 name the fused incremental prep's phases)
-        names = ["prep.S+r+ubloop", "step.loads", "res.reduce", "res.pred", "res.move", "res.apply(tail)", "prep.P1", None,
-                 "prep.P2", "prep.P3", "prep.end", "res.move->apply", "loads.bro+ctl", "loads.rec_reduce", "loads.keys", None, "prep.P4",
-                 "eps.sync1", "eps.wave0red", "prep.positions", "prep.sets", "apply.loads", "apply.update"]
-        counts = {"waves_scored": 7, "waves_gated_in": 15, "emits": 31, "spills": 30, "walks": 29, "walk_steps": 28, "walk_global": 27}
-        mhz = 100.0 * st[25] / max(st[24], 1)           # shader clock (the phase stamps' unit)
-        names = names + ["loads.broker", None, None, "stamp.overhead", "loads.setbits", "loads.hdr"]
-        print(json.dumps({"k_step_clock_mhz": mhz,
-                          "k_step_us": st[24] / 100.0 / n,
-                          "stamps_us_per_step": {k: st[i] / mhz / n for i, k in enumerate(names) if k},
-                          "counts_per_step": {k: st[i] / n for k, i in counts.items()},
-                          "stats": eng.stats()}))
-        return
-    eng.close()
     if not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(cl, cfg, desc, cand / max(steps, 1), args.cpu_seconds)
         cb = out["cpu_baseline"]

@@ -265,6 +265,20 @@ int kb_engine_sharded_scan(kb_engine *e, void *summary_dev);
 int kb_engine_sharded_resolve(kb_engine *e, const void *gathered_dev, int32_t n_ranks);
 int kb_engine_sharded_collect(kb_engine *e, kb_change *out, int64_t cap, int64_t *n_out);
 
+/* ---- RCCL-driven sharded plan (ABI 9): the per-step exchange without a host in the loop.
+ * Rank 0 calls kb_comm_unique_id and the caller broadcasts the KB_COMM_ID_BYTES bytes to
+ * every rank (any channel: torch.distributed, MPI, a file); each rank then binds its engine
+ * (created with its shard in kb_config.shard_begin / shard_end) to the communicator and
+ * calls kb_engine_sharded_plan with the same max_steps.  Per step: the shard's scan and
+ * rank summary, ncclAllGather of the fixed-size summaries on the engine's stream, the
+ * identical resolve + apply + prep on every rank; 64 steps per host round trip.  RCCL is
+ * bound at run time (KB_ERR_UNSUPPORTED without it).  Result convention of kb_engine_plan;
+ * every rank returns the same changes. */
+#define KB_COMM_ID_BYTES 128
+int kb_comm_unique_id(unsigned char *id);
+int kb_engine_comm_init(kb_engine *e, int32_t n_ranks, int32_t rank, const unsigned char *id);
+int kb_engine_sharded_plan(kb_engine *e, int64_t max_steps, kb_change *out, int64_t *n_out);
+
 #ifdef __cplusplus
 }
 #endif

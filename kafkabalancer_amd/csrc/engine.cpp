@@ -14,7 +14,9 @@
 #define roctxRangePush(msg) ((void)0)
 #define roctxRangePop() ((void)0)
 #endif
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>          // (types only: the symbols are resolved at run time, rccl_api)
 #include <algorithm>
 #include <cfloat>
 #include <chrono>
@@ -158,6 +160,13 @@ struct kb_engine {
     // a k_pair step workgroup timed out waiting for its grid (never expected): the engine
     // refuses further work (its arrival count was reset, but a plan may have been cut short)
     bool dead = false;
+    // the RCCL communicator of kb_engine_sharded_plan (kb_engine_comm_init) and its
+    // exchange buffers: this rank's summary and the gathered summaries of every rank
+    ncclComm_t comm = nullptr;
+    int nranks = 1, rank = 0;
+    unsigned char* sum_buf = nullptr;
+    unsigned char* gath_buf = nullptr;
+    int64_t xbuf_bytes = 0;            // summary bytes the buffers were sized for
     unsigned long long pair_wait_ticks = 200000000ull;   // k_pair's wait bound: 2 s of the 100 MHz clock
     std::string last_err;
 };
@@ -207,6 +216,42 @@ static hipError_t dalloc(T** p, size_t n) {
 static int upload_rf(kb_engine* e);   // (step launch section)
 
 static const int kRcChoices[] = {1, 2, 3, 4, 6, 8, 12, 16};
+
+// ------------------------------------------------------------- RCCL (run-time bound)
+
+// The sharded plan's all-gather goes through RCCL over xGMI.  The library is bound at run
+// time (dlopen), not at link time: the engine (and the C++ CLI, which never shards) loads
+// without it, and in a process that already holds an RCCL -- torch's -- the same copy is
+// reused (RTLD_NOLOAD on its soname) rather than a second one loaded beside it.
+struct RcclApi {
+    ncclResult_t (*get_unique_id)(ncclUniqueId*) = nullptr;
+    ncclResult_t (*comm_init_rank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+    ncclResult_t (*all_gather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
+    const char* (*error_string)(ncclResult_t) = nullptr;
+    std::string err;
+};
+
+static RcclApi& rccl_api() {
+    static RcclApi api = [] {
+        RcclApi a;
+        void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);
+        if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) { const char* d = dlerror(); a.err = std::string("RCCL not loadable: ") + (d ? d : "librccl.so.1"); return a; }
+        a.get_unique_id = (decltype(a.get_unique_id))dlsym(h, "ncclGetUniqueId");
+        a.comm_init_rank = (decltype(a.comm_init_rank))dlsym(h, "ncclCommInitRank");
+        a.all_gather = (decltype(a.all_gather))dlsym(h, "ncclAllGather");
+        a.comm_destroy = (decltype(a.comm_destroy))dlsym(h, "ncclCommDestroy");
+        a.error_string = (decltype(a.error_string))dlsym(h, "ncclGetErrorString");
+        if (!a.get_unique_id || !a.comm_init_rank || !a.all_gather || !a.comm_destroy || !a.error_string) {
+            a.err = "RCCL: a required symbol is missing";
+            a.get_unique_id = nullptr;
+        }
+        return a;
+    }();
+    return api;
+}
 
 // ------------------------------------------------------------- create
 
@@ -1478,6 +1523,18 @@ extern "C" int kb_engine_timings(kb_engine* e, double* ms, int64_t* launches, in
     return TK_N + 5;
 }
 
+// diagnostic: the control block's scalars (after a plan: the prep of the next step):
+// [0..1] ub per kind, [2] eps, [3] U0, [4] V, [5] avg, [6] rlo, [7] rhi, [8] E, [9] S
+extern "C" int kb_engine_ctl_scalars(kb_engine* e, double* out, int n) {
+    if (!e || !out) return KB_ERR_INVALID;
+    DevCtl c;
+    HIPCHK(hipStreamSynchronize(e->st));
+    HIPCHK(hipMemcpy(&c, e->ctl, sizeof c, hipMemcpyDeviceToHost));
+    const double v[10] = {c.ub[0], c.ub[1], c.eps, c.U0, c.V, c.avg, c.rlo, c.rhi, c.E, c.S};
+    for (int k = 0; k < 10 && k < n; k++) out[k] = v[k];
+    return 10;
+}
+
 // diagnostic: cumulative host phases of the plan calls since the last kb_engine_set_timing
 // (us): [0] reset_ctl, [1] enqueue of the batches, [2] waiting for them (the batch-end
 // transfer included), [3] log conversion, [4] kb_engine_plan calls
@@ -1647,6 +1704,9 @@ extern "C" void kb_engine_destroy(kb_engine* e) {
                     e->bset_off, e->bset_ids, e->gscr, e->pair_cnt, e->recs, e->cont, e->ctl, e->log, e->bdesc, e->ubdesc,
                     e->L.lstart, e->L.llen, e->L.lcap, e->L.lent, e->L.ck, e->L.dpos, e->rf_dev};
     for (void* p : ptrs) if (p) hipFree(p);
+    if (e->sum_buf) hipFree(e->sum_buf);
+    if (e->gath_buf) hipFree(e->gath_buf);
+    if (e->comm) { hipStreamSynchronize(e->st); rccl_api().comm_destroy(e->comm); }
     if (e->h_ctl) hipHostFree(e->h_ctl);
     if (e->h_flag) hipHostFree(e->h_flag);
     if (e->h_log) hipHostFree(e->h_log);
@@ -1835,4 +1895,103 @@ extern "C" int kb_engine_step_finish(kb_engine* e, const void* gathered_dev, int
     memset(out, 0, sizeof *out);
     out->status = KB_RETRY;
     return KB_RETRY;
+}
+
+// ----------------------------------------------------- RCCL-driven sharded plan
+
+extern "C" int kb_comm_unique_id(unsigned char* id) {
+    if (!id) return KB_ERR_INVALID;
+    RcclApi& R = rccl_api();
+    if (!R.get_unique_id) return KB_ERR_UNSUPPORTED;
+    ncclUniqueId u;
+    if (R.get_unique_id(&u) != ncclSuccess) return KB_ERR_HIP;
+    static_assert(sizeof(ncclUniqueId) == KB_COMM_ID_BYTES, "RCCL unique id size");
+    memcpy(id, &u, sizeof u);
+    return KB_OK;
+}
+
+extern "C" int kb_engine_comm_init(kb_engine* e, int32_t n_ranks, int32_t rank, const unsigned char* id) {
+    if (!e || !id || n_ranks < 1 || rank < 0 || rank >= n_ranks) return KB_ERR_INVALID;
+    RcclApi& R = rccl_api();
+    if (!R.comm_init_rank) { e->last_err = R.err; return KB_ERR_UNSUPPORTED; }
+    if (e->comm) { HIPCHK(hipStreamSynchronize(e->st)); R.comm_destroy(e->comm); e->comm = nullptr; }
+    HIPCHK(hipSetDevice(e->dev));
+    ncclUniqueId u;
+    memcpy(&u, id, sizeof u);
+    const ncclResult_t r = R.comm_init_rank(&e->comm, n_ranks, u, rank);
+    if (r != ncclSuccess) {
+        e->comm = nullptr;
+        e->last_err = std::string("ncclCommInitRank: ") + R.error_string(r);
+        return KB_ERR_HIP;
+    }
+    e->nranks = n_ranks;
+    e->rank = rank;
+    return KB_OK;
+}
+
+// (re-)size the exchange buffers to the current summary size (it grows after a KB_GROW,
+// alike on every rank)
+static int ensure_xbufs(kb_engine* e) {
+    const int64_t sb = (int64_t)summary_bytes(e->sum_keys);
+    if (sb == e->xbuf_bytes && e->sum_buf) return KB_OK;
+    HIPCHK(hipStreamSynchronize(e->st));
+    if (e->sum_buf) hipFree(e->sum_buf);
+    if (e->gath_buf) hipFree(e->gath_buf);
+    e->sum_buf = e->gath_buf = nullptr;
+    HIPCHK(hipMalloc((void**)&e->sum_buf, (size_t)sb));
+    HIPCHK(hipMalloc((void**)&e->gath_buf, (size_t)sb * e->nranks));
+    HIPCHK(hipMemset(e->sum_buf, 0, (size_t)sb));
+    HIPCHK(hipMemset(e->gath_buf, 0, (size_t)sb * e->nranks));
+    e->xbuf_bytes = sb;
+    return KB_OK;
+}
+
+// The whole -max-reassign plan of a partition-sharded engine, driven from C: batches of up
+// to 64 rounds (scan + rank summary, ncclAllGather of the summaries on the engine's stream,
+// the identical resolve + apply + prep on every rank) per host round trip; a halted round
+// turns the rest of the batch into no-ops on every rank alike.  Every rank calls it with
+// the same max_steps; the changes are the same on every rank.  Same result convention as
+// kb_engine_plan.
+extern "C" int kb_engine_sharded_plan(kb_engine* e, int64_t max_steps, kb_change* out, int64_t* n_out) {
+    if (!e || !n_out || max_steps < 0) return KB_ERR_INVALID;
+    *n_out = 0;
+    if (!e->comm) { e->last_err = "kb_engine_sharded_plan: no communicator (kb_engine_comm_init)"; return KB_ERR_INVALID; }
+    if (max_steps == 0) return KB_NOCHANGE;
+    if (e->pending) { if (out) pending_result(e, out); *n_out = 1; return e->pending; }
+    if (e->dead) return dead_result(e);
+    RcclApi& R = rccl_api();
+    e->last_ms = 0;
+    HIPCHK(hipEventRecord(e->ev0, e->st));
+    std::vector<kb_change> tmp;
+    int64_t k = 0;
+    int rc = KB_CHANGE;
+    while (k < max_steps) {
+        if (const int r = ensure_xbufs(e); r != KB_OK) { *n_out = k; return r; }
+        const int64_t b = std::min<int64_t>(kStepBatch, max_steps - k);
+        if (const int r = kb_engine_sharded_reset(e, b); r < 0) { *n_out = k; return r; }
+        for (int64_t i = 0; i < b; i++) {
+            if (const int r = kb_engine_sharded_scan(e, e->sum_buf); r < 0) { *n_out = k; return r; }
+            const ncclResult_t nr = R.all_gather(e->sum_buf, e->gath_buf, (size_t)e->xbuf_bytes, ncclUint8, e->comm, e->st);
+            if (nr != ncclSuccess) {
+                e->last_err = std::string("ncclAllGather: ") + R.error_string(nr);
+                *n_out = k;
+                return KB_ERR_HIP;
+            }
+            if (const int r = kb_engine_sharded_resolve(e, e->gath_buf, e->nranks); r < 0) { *n_out = k; return r; }
+        }
+        tmp.resize((size_t)b + 1);
+        int64_t n = 0;
+        rc = kb_engine_sharded_collect(e, tmp.data(), b + 1, &n);
+        for (int64_t i = 0; i < n && k < max_steps; i++, k++)
+            if (out) out[k] = tmp[(size_t)i];
+        if (rc == KB_CHANGE || rc == KB_RETRY || rc == KB_GROW) { rc = KB_CHANGE; continue; }
+        break;                                        // no change / error: the plan ends
+    }
+    HIPCHK(hipEventRecord(e->ev1, e->st));
+    HIPCHK(hipEventSynchronize(e->ev1));
+    float ms = 0;
+    hipEventElapsedTime(&ms, e->ev0, e->ev1);
+    e->last_ms = ms;
+    *n_out = k;
+    return rc;
 }

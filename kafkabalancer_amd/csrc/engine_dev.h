@@ -28,8 +28,10 @@ constexpr uint32_t NONE32 = 0xFFFFFFFFu;
 constexpr unsigned long long NONE64 = ~0ull;
 constexpr uint16_t NONE16 = 0xFFFFu;
 constexpr int TILE_KEYS = 16;       // near-tie keys carried in a scan workgroup record
-constexpr int SUMMARY_KEYS = 56;    // near-tie keys per rank summary to start with (1936-B
-                                    // summaries); grown 8x (up to DEDUP_STEP) when one overflows
+constexpr int SUMMARY_KEYS = 56;    // key slots per rank summary to start with (1936-B summaries):
+                                    // near-tie keys in the first 54, the last two the second-best
+                                    // keys per kind (k_summary); grown 8x (up to DEDUP_STEP) when
+                                    // the near-tie keys overflow
 constexpr int SUMMARY_KEYS_MAX = 2048;
 constexpr int DEDUP_STEP = 2048;    // LDS key table of k_step / k_summary
 constexpr int DEDUP_SCAN = 256;     // LDS key table of one k_scan workgroup

@@ -1986,13 +1986,17 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
                 for (int b = tid; b < B; b += STEP_THREADS) s_e[b] = 0.0;
                 __syncthreads();
             };
-            if (s_exact_need >= 2) {
-                bool take = s_exact_need == 3;
-                if (s_exact_need == 2) {
+            // (read into a register: thread 0 clears the word below, and a wave that read it
+            // only after that would skip the block and its barriers)
+            const int xneed = s_exact_need;
+            if (xneed >= 2) {
+                bool take = xneed == 3;
+                if (xneed == 2) {
                     exact_su();
                     unstage();
                     take = !(s_sux < a.min_unbalance);
                 }
+                __syncthreads();                 // every thread has read s_exact_need
                 if (tid == 0) {
                     s_exact_need = 0;
                     const uint32_t* F = s_first;
@@ -2510,6 +2514,19 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
     // ================================================================== prep
     // (next step): getBL's (load, id) order, bl_move, relative loads, eps, sets
     const bool full = C.full_prep != 0;
+    // The next step's census bound ub is the minimum of last step's best keys (one per
+    // record and kind) re-scored on the new loads: any legal move bounds the new minimum
+    // from above.  A key whose brokers the applied move touched is still a legal move after
+    // a replace that left bl_move's membership alone (its partition kept its replicas, its
+    // target is still in the set and in bl_move): only the moved partition's keys are
+    // dropped.  (Dropping every touched key as well left no key at all on most steps of a
+    // non-leader plan -- the records' keys come from the census waves, which mostly share
+    // the step's source or target -- so the bound went open and every wave walked its
+    // targets: 4000 of 5400 waves per step, c3nl 0.47 ms/step.)  After a remove / add /
+    // swap or a membership change the touched brokers' keys are dropped as before.
+    auto keep_touched_keys = [&]() -> bool {
+        return do_res && D.status == 1 && D.kind == 1 && !s_memb;
+    };
 #if KB_ABL & 2
     // diagnostic timing build (tools/ablate.sh): no incremental prep at all
     if (!full) { if (tid == 0) C.prepped = 1; write_back(); return; }
@@ -2575,9 +2592,12 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
         // (held in registers from the header load, they would stay live through the
         // resolve, the apply and the exact folds)
         const bool bkeys = do_res && tid < a.R.n;
-        Contender bk0, bk1;
-        bk0.s = bk1.s = -1;
+        Contender bk0, bk1, bx0, bx1;
+        bk0.s = bk1.s = bx0.s = bx1.s = -1;
         if (bkeys) { bk0 = ldobj(&a.R.h(tid)->best[0]); bk1 = ldobj(&a.R.h(tid)->best[1]); }
+        if (bkeys && !a.use_spill) {                  // rank summaries: the second-best keys too
+            bx0 = ldobj(a.R.k(tid) + (a.R.cap - 2)); bx1 = ldobj(a.R.k(tid) + (a.R.cap - 1));
+        }
         if (tid < nT) { s_fl[s_T[tid]] |= BF_TOUCHED; s_cntT[tid] = 0; }
         if (tid == 0) { s_unc = 0; s_nsub = 0; }
         if (wid < NRW) {
@@ -2675,6 +2695,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
             double ub0 = HUGE_VAL, ub1 = HUGE_VAL;
             if (bkeys) {
                 const long long pm = s_moved;
+                const bool keep_t = keep_touched_keys();
 #pragma unroll
                 for (int k = 0; k < 2; k++) {
                     const Contender& c = k ? bk1 : bk0;
@@ -2692,7 +2713,16 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
                         if (keep) atomicAdd(&s_nsub, 1);
                     }
                     if (!keep) continue;
-                    if ((s_fl[c.s] | s_fl[c.t]) & BF_TOUCHED) continue;
+                    if (!keep_t && ((s_fl[c.s] | s_fl[c.t]) & BF_TOUCHED)) continue;
+                    const double d2 = cont_delta_ld(s_ld, c, iav);
+                    if (k == 0) ub0 = d2 < ub0 ? d2 : ub0;
+                    else ub1 = d2 < ub1 ? d2 : ub1;
+                }
+#pragma unroll
+                for (int k = 0; k < 2; k++) {                 // (rank summaries' second-best keys)
+                    const Contender& c = k ? bx1 : bx0;
+                    if (c.s < 0 || (long long)(c.iter >> 21) == pm) continue;
+                    if (!keep_t && ((s_fl[c.s] | s_fl[c.t]) & BF_TOUCHED)) continue;
                     const double d2 = cont_delta_ld(s_ld, c, iav);
                     if (k == 0) ub0 = d2 < ub0 ? d2 : ub0;
                     else ub1 = d2 < ub1 ? d2 : ub1;
@@ -3121,9 +3151,12 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
     // the records' best keys (re-scored below for the next step's upper bound; one
     // record per thread): loaded first, their latency overlaps the sums
     const bool bkeys = do_res && !full && tid < a.R.n;
-    Contender bk0, bk1;
-    bk0.s = bk1.s = -1;
+    Contender bk0, bk1, bx0, bx1;
+    bk0.s = bk1.s = bx0.s = bx1.s = -1;
     if (bkeys) { bk0 = ldobj(&a.R.h(tid)->best[0]); bk1 = ldobj(&a.R.h(tid)->best[1]); }
+    if (bkeys && !a.use_spill) {                      // rank summaries: the second-best keys too
+        bx0 = ldobj(a.R.k(tid) + (a.R.cap - 2)); bx1 = ldobj(a.R.k(tid) + (a.R.cap - 1));
+    }
     // approximate S (exact in integral mode: integers below 2^52), total load error E
     double sS = 0.0, sE = 0.0;
     for (int b = tid; b < B; b += STEP_THREADS)
@@ -3160,13 +3193,14 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
     double ub0 = HUGE_VAL, ub1 = HUGE_VAL;
     if (bkeys) {
         const long long pm = s_moved;
+        const bool keep_t = keep_touched_keys();
 #pragma unroll
-        for (int k = 0; k < 2; k++) {
-            const Contender& c = k ? bk1 : bk0;
+        for (int k = 0; k < 4; k++) {
+            const Contender& c = k == 0 ? bk0 : k == 1 ? bk1 : k == 2 ? bx0 : bx1;
             if (c.s < 0 || (long long)(c.iter >> 21) == pm) continue;
-            if ((s_fl[c.s] | s_fl[c.t]) & BF_TOUCHED) continue;
+            if (!keep_t && ((s_fl[c.s] | s_fl[c.t]) & BF_TOUCHED)) continue;
             const double d = cont_delta_ld(s_ld, c, iav);
-            if (k == 0) ub0 = d < ub0 ? d : ub0;
+            if ((k & 1) == 0) ub0 = d < ub0 ? d : ub0;          // (k = 0, 2: leader keys)
             else ub1 = d < ub1 ? d : ub1;
         }
     }
@@ -3284,8 +3318,12 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
         if (tid == 0) s_cursor = 0;
         __syncthreads();
         const int lim = bigm ? (full ? a.nsets : s_bo[nT]) : nwords;
-        while (s_cursor < lim) {
+        for (;;) {
+            // (every thread reads the cursor before wave 0 may advance it: a wave reading
+            // the advanced cursor would leave the loop, skip its records and the barriers)
             const int c0 = s_cursor;
+            if (c0 >= lim) break;
+            __syncthreads();
             int bn = 0;
             if (bigm) {
                 // the next CH sets of the list
@@ -3302,7 +3340,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
                 if (tid == 0) s_mn = bn;
             } else if (wid == 0) {
                 // the next marked sets, up to CH, in set order
-                int n = 0, w = s_cursor;
+                int n = 0, w = c0;
                 while (w < nwords) {
                     const int ww = w + lane;
                     const uint32_t bits = ww < nwords ? s_smark[ww] : 0u;
@@ -3755,7 +3793,13 @@ __global__ __launch_bounds__(1024) void k_summary(SumArgs a) {
     dedup_clear(T);
     if (tid == 0) { s_n = 0; s_fail = 0; }
     if (tid < NF) s_f[tid] = NONE32;
-    if (tid < 2) { s_benc[tid] = NONE64; s_brec[tid] = NONE32; }
+    __shared__ unsigned long long s_benc2[2];
+    __shared__ uint32_t s_brec2[2];
+    if (tid < 2) { s_benc[tid] = NONE64; s_brec[tid] = NONE32; s_benc2[tid] = NONE64; s_brec2[tid] = NONE32; }
+    // the near-tie keys take the first cap - 2 slots; the last two carry, per kind, the best
+    // key of another partition than the summary's best (k_step's census bound: the best key
+    // is most often the applied move itself, whose partition's keys are dropped)
+    const uint32_t capk = (uint32_t)a.out.cap - 2u;
     const bool ran = ctl->halted == H_RUN && ctl->prepped;
     const double eps = ctl->eps, inv_avg = ctl->inv_avg;
     double d0 = HUGE_VAL, d1 = HUGE_VAL;
@@ -3829,16 +3873,46 @@ __global__ __launch_bounds__(1024) void k_summary(SumArgs a) {
     __shared__ uint32_t s_nkk[2];
     if (tid < 2) s_nkk[tid] = 0;
     __syncthreads();
+    {
+        // second-best keys: the best key per kind among the records whose best key lies in
+        // another partition than the summary's best
+        long long bp[2];
+        unsigned long long e2[2] = {NONE64, NONE64};
+        for (int k = 0; k < 2; k++)
+            bp[k] = s_brec[k] != NONE32 ? (long long)(a.R.h((int)s_brec[k])->best[k].iter >> 21) : -1;
+        for (int i = tid; i < a.R.n; i += 1024)
+            for (int k = 0; k < 2; k++) {
+                const Contender c = a.R.h(i)->best[k];
+                if (c.s < 0 || (long long)(c.iter >> 21) == bp[k]) continue;
+                const unsigned long long e = enc(cont_delta(a.r, c, inv_avg));
+                if (e < e2[k]) e2[k] = e;
+                atomicMin(&s_benc2[k], e);
+            }
+        __syncthreads();
+        for (int i = tid; i < a.R.n; i += 1024)
+            for (int k = 0; k < 2; k++) {
+                const Contender c = a.R.h(i)->best[k];
+                if (c.s >= 0 && (long long)(c.iter >> 21) != bp[k] && e2[k] == s_benc2[k] &&
+                    enc(cont_delta(a.r, c, inv_avg)) == s_benc2[k])
+                    atomicMin(&s_brec2[k], (uint32_t)i);
+            }
+    }
     for (int h = tid; h < DEDUP_STEP; h += 1024) {
         if (s_key[h] == NONE32) continue;
         const uint32_t k = atomicAdd(&s_n, 1u);
         atomicAdd(&s_nkk[s_key[h] >> 30], 1u);
-        if (k < (uint32_t)a.out.cap) okeys[k] = dedup_entry(T, h);
+        if (k < capk) okeys[k] = dedup_entry(T, h);
     }
     __syncthreads();
+    if (tid < 2) {
+        Contender x;
+        if (s_brec2[tid] != NONE32) x = a.R.h((int)s_brec2[tid])->best[tid];
+        else { x.s = x.t = -1; x.w = 0.0; x.iter = NONE64; x.kind = tid; x.pad = 0; }
+        okeys[capk + tid] = x;
+    }
     if (tid == 0) {
-        out->nkeys = s_n < (uint32_t)a.out.cap ? s_n : (uint32_t)a.out.cap;
-        out->flags = ((ran && ctl->cont_overflow) || s_fail || s_n > (uint32_t)a.out.cap) ? 1u : 0u;
+        out->nkeys = s_n < capk ? s_n : capk;
+        out->flags = ((ran && ctl->cont_overflow) || s_fail || s_n > capk) ? 1u : 0u;
         if (ran) out->flags |= 2u;
         if (ran && ctl->cont_overflow && a.spill_growable) out->flags |= 4u;   // (grow_summary)
         out->nkk[0] = (uint16_t)min(s_nkk[0], 0xFFFFu);

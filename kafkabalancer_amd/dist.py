@@ -146,14 +146,39 @@ class _DeviceEngineAdapter:
         return self.eng.sharded_collect(cap)
 
 
-def bench_main(args, world, rank, local):
-    """bench.py for N > 1 (launched by torch.distributed.run)."""
+def _timed(fn, steps):
+    import torch
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    out = fn(steps)
+    torch.cuda.synchronize()
+    return out, time.perf_counter() - t0
+
+
+def _rccl_engine(E, cl, cfg, local, shard, world, rank, uid):
+    eng = E.Engine(cl, cfg, device=local, shard=shard)
+    eng.comm_init(world, rank, uid)
+    return eng
+
+
+def _plan_or_raise(fn, steps):
+    changes, err = fn(steps)
+    if err is not None:
+        raise err
+    return changes
+
+
+def bench_main(args, world, rank, local, cpu_baseline=None):
+    """bench.py for N > 1 (launched by torch.distributed.run).  With RCCL (the default) the
+    whole plan runs in C: kb_engine_sharded_plan enqueues 64 rounds of (scan + rank summary,
+    ncclAllGather on the engine's stream, resolve) per host round trip; the communicator's
+    unique id goes from rank 0 to the others over torch.distributed.  KB_DIST_BACKEND=gloo:
+    the host-staged rehearsal (ShardedPlanner, ranks may share a GPU)."""
     import torch
     import torch.distributed as dist
     from . import engine as E
     from . import synth
     import os
-    # KB_DIST_BACKEND=gloo: rehearsal with host-staged summaries (ranks may share a GPU)
     backend = os.environ.get("KB_DIST_BACKEND", "nccl")
     local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
@@ -162,40 +187,61 @@ def bench_main(args, world, rank, local):
     # sharded N ways; weak: every rank adds a full cluster's worth of partitions
     scaling = getattr(args, "scaling", None) or ("strong" if args.workload == "c5" else "weak")
     cl, cfg, desc = synth.config(args.workload, scale=args.scale * (world if scaling == "weak" else 1))
-    begin, end = shard_bounds(cl.n, world, rank)
-    eng = E.Engine(cl, cfg, device=local, shard=(begin, end))
-    eng.set_stream(torch.cuda.current_stream().cuda_stream)
-    sp = ShardedPlanner(_DeviceEngineAdapter(eng), world, device_tensors=True, staged=backend != "nccl")
-    sp.plan(args.warmup)
+    shard = shard_bounds(cl.n, world, rank)
+    rccl = backend == "nccl"
+    uid = None
+    if rccl:
+        box = [E.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(box, src=0)
+        uid = box[0]
+
+    def make():
+        if rccl:
+            e = _rccl_engine(E, cl, cfg, local, shard, world, rank, uid)
+            return e, (lambda n: _plan_or_raise(e.sharded_plan, n))
+        e = E.Engine(cl, cfg, device=local, shard=shard)
+        e.set_stream(torch.cuda.current_stream().cuda_stream)
+        sp = ShardedPlanner(_DeviceEngineAdapter(e), world, device_tensors=True, staged=True)
+        return e, sp.plan
+
+    eng, plan = make()
+    plan(args.warmup)
     st0 = eng.stats()
     torch.cuda.synchronize()
     dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    changes = sp.plan(args.steps)
-    torch.cuda.synchronize()
+    changes, wall_r = _timed(plan, args.steps)
     dist.barrier()
     torch.cuda.synchronize()
     if rank == 0 and getattr(args, "plan_out", None):
         with open(args.plan_out, "w") as f:
             json.dump(changes, f)
-    dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64,
-                      device="cuda" if backend == "nccl" else "cpu")
+    dt = torch.tensor([wall_r], dtype=torch.float64, device="cuda" if rccl else "cpu")
     dist.all_reduce(dt, op=dist.ReduceOp.MAX)
     wall = float(dt.item())
     st1 = eng.stats()
     steps = max(1, len(changes))
     cand = st1["candidates"] - st0["candidates"]       # merged counts: the whole job
-    # per-kernel device-clock durations over a second stretch (this rank's shard)
+    eng.close()
+    # per-kernel device-clock durations over the same steps (a fresh engine replays the
+    # warm-up and the timed steps): the scan launch's span, as on one GPU -- the end of
+    # the kernel before it (the last round's k_step) to the last scan workgroup's end
+    eng, plan = make()
+    plan(args.warmup)
     eng.set_timing(True)
-    sp.plan(min(args.steps, 100))
+    plan(steps)
     tk = eng.timings()
-    scan_ms, scan_n = tk["scan_inner"]     # (first workgroup start .. last end; the summary and
-                                          # the all-gather sit between the scan and k_step)
+    eng.close()
+    dist.barrier()
+    scan_ms, scan_n = tk["scan"]
+    timing = "device clock: the previous round's k_step end to the last scan workgroup's end (dispatch included)"
+    if not scan_n:
+        scan_ms, scan_n = tk["scan_inner"]
+        timing = "device clock: earliest scan workgroup start to latest end"
     scan_us = 1e3 * scan_ms / max(scan_n, 1)
     shard_bytes = st1["scan_bytes"]
     achieved = shard_bytes / (scan_us * 1e-6) / 1e9 if scan_us > 0 else 0.0
     if rank == 0:
+        b8d = cl.n * (8 + 4 * st1["max_replicas"] + 1 + 1 + 4) + 12 * st1["n_brokers"]
         out = {
             "metric": "candidate moves scored/sec (+ ms per reassignment step)",
             "value": cand / wall,
@@ -208,17 +254,60 @@ def bench_main(args, world, rank, local):
             "scaling": scaling,
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic (numpy PCG64), %s" % ("Zipf weights r^-1.1" if desc.get("weights") == "zipf"
-                                                      else "uniform weights"),
+            "data": "synthetic (numpy PCG64 seed %#x), %s" % (synth.SEEDS[args.workload],
+                                                             "Zipf weights r^-1.1" if desc.get("weights") == "zipf"
+                                                             else "uniform weights"),
             "config": dict(desc, parallelism="partition-sharded x%d, replicated broker state, "
-                                              "1 all-gather per step" % world),
+                                              "1 all-gather per step (%s)" % (world, "RCCL, plan driven from C"
+                                                                              if rccl else "gloo, host-staged")),
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": 8000.0, "unit": "GB/s",
                          "frac": achieved / 8000.0, "traffic": None, "kernel": "k_scan (rank 0 shard)",
-                         "bytes_per_launch": shard_bytes, "avg_launch_us": scan_us,
-                         "timing": "device clock: earliest workgroup start to latest workgroup end"},
+                         "bytes_per_launch": shard_bytes, "avg_launch_us": scan_us, "timing": timing,
+                         "launches": scan_n,
+                         "frac_step": b8d / (wall / steps) / 8e12,
+                         "frac_step_def": "SURVEY.md 8(d) bytes of the whole cluster per step / ms_per_step / 8 TB/s"},
             "kernels_us_per_launch": {k: 1e3 * v[0] / max(v[1], 1) for k, v in tk.items() if v[1]},
-            "exchange": backend,
+            "kernel_timing_def": "a fresh engine per rank replays the warm-up and the same timed steps",
+            "exchange": "rccl" if rccl else backend,
         }
-        print(json.dumps(out))
-    eng.close()
+        if cpu_baseline is not None and not getattr(args, "no_cpu_baseline", False):
+            out["cpu_baseline"] = cpu_baseline(cl, cfg, desc, cand / steps, args.cpu_seconds)
+        print(json.dumps(out), flush=True)
+    dist.barrier()
     dist.destroy_process_group()
+
+
+def bench_world1(args, cpu_baseline=None):
+    """`bench.py --sharded` (one GPU): the sharded protocol at world size 1 -- a shard of
+    every partition, kb_engine_sharded_plan with a one-rank RCCL communicator -- against the
+    plain plan (kb_engine_plan) over the same steps: the protocol's own overhead per step
+    (the extra launches, the all-gather, the unfused resolve).  One JSON line; not the
+    headline."""
+    import torch
+    from . import engine as E
+    from . import synth
+    torch.cuda.set_device(0)
+    cl, cfg, desc = synth.config(args.workload, scale=args.scale)
+    uid = E.comm_unique_id()
+    eng = _rccl_engine(E, cl, cfg, 0, (0, cl.n), 1, 0, uid)
+    _plan_or_raise(eng.sharded_plan, args.warmup)
+    (buf, n, rc), wall_s = _timed(eng.sharded_plan_raw, args.steps)
+    sh_changes, err = eng.changes(buf, n, rc)
+    assert err is None, err
+    eng.close()
+    ref = E.Engine(cl, cfg, device=0)
+    _plan_or_raise(ref.plan, args.warmup)
+    (buf, n, rc), wall_p = _timed(ref.plan_raw, args.steps)
+    pl_changes, err = ref.changes(buf, n, rc)
+    assert err is None, err
+    fused = ref.stats()["fused_pairs"]
+    ref.close()
+    key = lambda ch: [(c["step"], c["pidx"], c["from_"], c["to"], c["slot"]) for c in ch]
+    steps = max(1, len(sh_changes))
+    out = {"metric": "sharded protocol at world size 1 (%s)" % args.workload, "unit": "ms/step",
+           "ms_per_step_sharded": 1e3 * wall_s / steps, "ms_per_step_plain": 1e3 * wall_p / max(1, len(pl_changes)),
+           "ratio": (wall_s / steps) / (wall_p / max(1, len(pl_changes))), "steps": steps, "warmup": args.warmup,
+           "plans_equal": key(sh_changes) == key(pl_changes), "plain_fused_pairs": fused,
+           "def": "kb_engine_sharded_plan (scan + k_summary, ncclAllGather on a 1-rank communicator, k_step "
+                  "resolve; 64 rounds per host round trip) vs kb_engine_plan, same warm-up and steps"}
+    print(json.dumps(out), flush=True)

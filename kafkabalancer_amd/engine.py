@@ -29,7 +29,7 @@ EXPORTS = ["kb_abi_version", "kb_engine_create", "kb_engine_balance", "kb_engine
            "kb_engine_step_begin", "kb_engine_step_finish", "kb_engine_set_stream",
            "kb_engine_sharded_reset", "kb_engine_sharded_scan", "kb_engine_sharded_resolve",
            "kb_engine_sharded_collect", "kb_engine_set_incremental", "kb_engine_step",
-           "kb_engine_host_timings"]
+           "kb_engine_host_timings", "kb_comm_unique_id", "kb_engine_comm_init", "kb_engine_sharded_plan"]
 
 P64 = C.POINTER(C.c_int64)
 PD = C.POINTER(C.c_double)
@@ -130,6 +130,16 @@ def lib():
         L.kb_engine_sharded_resolve.restype = C.c_int
         L.kb_engine_sharded_collect.argtypes = [vp, C.POINTER(kb_change), C.c_int64, P64]
         L.kb_engine_sharded_collect.restype = C.c_int
+        if hasattr(L, "kb_engine_ctl_scalars"):         # (diagnostic)
+            L.kb_engine_ctl_scalars.argtypes = [vp, PD, C.c_int]
+            L.kb_engine_ctl_scalars.restype = C.c_int
+        if hasattr(L, "kb_engine_sharded_plan"):        # (ABI 9; older builds in A/B runs lack it)
+            L.kb_comm_unique_id.argtypes = [C.c_char_p]
+            L.kb_comm_unique_id.restype = C.c_int
+            L.kb_engine_comm_init.argtypes = [vp, C.c_int32, C.c_int32, C.c_char_p]
+            L.kb_engine_comm_init.restype = C.c_int
+            L.kb_engine_sharded_plan.argtypes = [vp, C.c_int64, C.POINTER(kb_change), P64]
+            L.kb_engine_sharded_plan.restype = C.c_int
         any_abi = os.environ.get("KB_ABI_ANY") == "1"      # diagnostic: older builds (bisecting)
         if hasattr(L, "kb_engine_set_incremental"):
             L.kb_engine_set_incremental.argtypes = [vp, C.c_int32]
@@ -138,6 +148,18 @@ def lib():
             raise ImportError("libkbengine.so ABI mismatch")
         _lib = L
     return _lib
+
+
+KB_COMM_ID_BYTES = 128
+
+
+def comm_unique_id():
+    """RCCL unique id (rank 0; the caller broadcasts the bytes): kb_comm_unique_id."""
+    buf = C.create_string_buffer(KB_COMM_ID_BYTES)
+    rc = lib().kb_comm_unique_id(buf)
+    if rc != 0:
+        raise EngineError(rc, "kb_comm_unique_id failed (%s)" % ERRORS.get(rc, rc))
+    return buf.raw
 
 
 class EngineError(RuntimeError):
@@ -398,6 +420,13 @@ class Engine:
         lib().kb_engine_host_timings(self.h, us.ctypes.data_as(PD), 5)
         return {"reset": us[0], "enqueue": us[1], "wait": us[2], "convert": us[3], "calls": int(us[4])}
 
+    def ctl_scalars(self):
+        """Diagnostic: the control block's scalars for the next step (ub per kind, eps, U0, V,
+        avg, r range, E, S)."""
+        v = np.zeros(10)
+        lib().kb_engine_ctl_scalars(self.h, v.ctypes.data_as(PD), 10)
+        return dict(zip(("ub0", "ub1", "eps", "U0", "V", "avg", "rlo", "rhi", "E", "S"), v.tolist()))
+
     def stamps(self):
         """Diagnostic build only: accumulated phase ticks (100 MHz) of the k_step phases."""
         out = np.zeros(32, np.int64)
@@ -419,6 +448,27 @@ class Engine:
         if rc < 0:
             raise EngineError(rc, self.last_error())
         return v.value
+
+    # ---- RCCL-driven sharded plan (kb_engine_comm_init / kb_engine_sharded_plan)
+    def comm_init(self, n_ranks, rank, uid):
+        assert len(uid) == KB_COMM_ID_BYTES
+        rc = lib().kb_engine_comm_init(self.h, n_ranks, rank, uid)
+        if rc != 0:
+            raise EngineError(rc, self.last_error())
+
+    def sharded_plan_raw(self, max_steps):
+        """The sharded plan call alone (RCCL all-gather per step, 64 steps per host round
+        trip): (change buffer, n, rc); the buffer is reused like plan_raw's."""
+        if max_steps > self._cap:
+            while self._cap < max_steps:
+                self._cap *= 2
+            self._buf = (kb_change * self._cap)()
+        n = C.c_int64()
+        rc = lib().kb_engine_sharded_plan(self.h, max_steps, self._buf, C.byref(n))
+        return self._buf, n.value, rc
+
+    def sharded_plan(self, max_steps):
+        return self.changes(*self.sharded_plan_raw(max_steps))
 
     # multi-GPU step phases
     def summary_bytes(self):

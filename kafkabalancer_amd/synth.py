@@ -74,12 +74,19 @@ def make_cluster(P, B, rf=3, weights="uniform", nsets=0, set_size=0, seed=0, wit
     return ClusterSoA(reps.reshape(-1), off, w, nr, set_ids, set_off, set_idx, None, names, pids)
 
 
+# c3nl: BASELINE.json configs[2]'s cluster without -allow-leader (MoveNonLeaders at 1M x 1000
+# with 256 allowed sets of 64: the 2-slot scan the headline's leader 2-cycle never reaches);
+# w16k: the engine's widest broker universe (1M partitions x 16384 brokers, Zipf, auto lists)
+SEEDS = {"c2": 0x5EED0002, "c3": 0x5EED0003, "c3nl": 0x5EED0003, "c4": 0x5EED0004, "c5": 0x5EED0005,
+         "w16k": 0x5EED0016}
+WORKLOADS = tuple(SEEDS)
+
+
 def config(name, scale=1.0, seed=None, with_names=False):
-    """BASELINE.json configs c2..c5 (optionally scaled down in partitions)."""
+    """BASELINE.json configs c2..c5 (optionally scaled down in partitions), c3nl, w16k."""
     base = {"allow_leader": False, "rebalance_leaders": False, "min_replicas": 2,
             "min_unbalance": 0.01, "brokers": None}
-    s = seed if seed is not None else {"c2": 0x5EED0002, "c3": 0x5EED0003,
-                                       "c4": 0x5EED0004, "c5": 0x5EED0005}[name]
+    s = seed if seed is not None else SEEDS[name]
     if name == "c2":
         P = max(1, int(10000 * scale))
         cl = make_cluster(P, 50, 3, "uniform", seed=s, with_names=with_names)
@@ -93,6 +100,19 @@ def config(name, scale=1.0, seed=None, with_names=False):
         return cl, cfg, {"workload": "c3", "partitions": P, "brokers": 1000, "rf": 3,
                          "weights": "zipf", "allowed_sets": "256x64", "allow_leader": True,
                          "max_reassign": 1000}
+    if name == "c3nl":
+        P = max(1, int(1_000_000 * scale))
+        cl = make_cluster(P, 1000, 3, "zipf", nsets=256, set_size=64, seed=s, with_names=with_names)
+        cfg = dict(base, min_unbalance=0.0)
+        return cl, cfg, {"workload": "c3nl", "partitions": P, "brokers": 1000, "rf": 3,
+                         "weights": "zipf", "allowed_sets": "256x64", "allow_leader": False,
+                         "max_reassign": 1000}
+    if name == "w16k":
+        P = max(1, int(1_000_000 * scale))
+        cl = make_cluster(P, 16384, 3, "zipf", seed=s, with_names=with_names)
+        cfg = dict(base, min_unbalance=0.0)
+        return cl, cfg, {"workload": "w16k", "partitions": P, "brokers": 16384, "rf": 3,
+                         "weights": "zipf", "max_reassign": 1000}
     if name == "c4":
         P = max(1, int(1_000_000 * scale))
         rng = np.random.default_rng(s + 1)

@@ -516,6 +516,62 @@ def test_rccl_world1_matches_oracle():
     assert st == opl.state()
 
 
+def _rccl_c_worker(steps, q):
+    """kb_engine_sharded_plan at world size 1: the RCCL communicator bound by the engine
+    itself (kb_comm_unique_id / kb_engine_comm_init), the whole plan driven from C."""
+    try:
+        torch.cuda.set_device(0)
+        from kafkabalancer_amd import engine as E
+        cl, cfg = _gpu_cluster()
+        uid = E.comm_unique_id()
+        eng = E.Engine(cl, cfg, shard=shard_bounds(cl.n, 1, 0))
+        eng.comm_init(1, 0, uid)
+        a, err = eng.sharded_plan(10)                 # two calls: the plan resumes
+        assert err is None, err
+        b, err = eng.sharded_plan(steps - 10)
+        assert err is None, err
+        q.put(([(c["step"], c["pidx"], c["kind"], c["from_"], c["to"], c["slot"]) for c in a + b],
+               eng.state(), None))
+        eng.close()
+    except Exception as ex:                        # reported to the parent, not swallowed
+        q.put((None, None, repr(ex)))
+
+
+@pytest.mark.gpu
+def test_rccl_sharded_plan_from_c_matches_oracle():
+    """The RCCL path driven from C (kb_engine_sharded_plan: scan + summary, ncclAllGather on
+    the engine's stream, resolve; 64 rounds per host round trip) equals the oracle's plan
+    and final state, in a child process started before it touches the GPU."""
+    from kafkabalancer_amd import synth
+    from helpers import oracle_plan
+    steps = 24
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_c_worker, args=(steps, q))
+    p.start()
+    ch, st, err = q.get(timeout=240)
+    p.join(timeout=60)
+    assert err is None, err
+    cl, cfg = _gpu_cluster()
+    och, oerr, opl = oracle_plan(synth.to_plist(cl), cfg, steps)
+    assert oerr is None
+    assert ch == [(c["step"], c["pidx"], c["kind"], c["from_"], c["to"], c["slot"]) for c in och]
+    assert st == opl.state()
+
+
+@pytest.mark.gpu
+def test_bench_sharded_world1_line():
+    """`bench.py --sharded`: the world-1 sharded protocol line, with the sharded plan equal
+    to the plain plan over the same steps."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--sharded", "--workload", "c3",
+                        "--scale", "0.05", "--steps", "40", "--warmup", "5"],
+                       cwd=root, capture_output=True, text=True, timeout=400)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["plans_equal"] and line["steps"] == 40, line
+
+
 @pytest.mark.gpu
 def test_bench_gpus2_spawns_two_ranks(tmp_path):
     """`bench.py --gpus 2` with no launcher starts two ranks itself (torch.distributed.run as
