@@ -161,7 +161,8 @@ struct kb_engine {
     // refuses further work (its arrival count was reset, but a plan may have been cut short)
     bool dead = false;
     // the RCCL communicator of kb_engine_sharded_plan (kb_engine_comm_init) and its
-    // exchange buffers: this rank's summary and the gathered summaries of every rank
+    // exchange buffer: the gathered summaries of every rank, this rank's summary written in
+    // place into its own slot (an in-place ncclAllGather)
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
     unsigned char* sum_buf = nullptr;
@@ -1535,6 +1536,16 @@ extern "C" int kb_engine_ctl_scalars(kb_engine* e, double* out, int n) {
     return 10;
 }
 
+// diagnostic: the last scan's record headers (RecHdr, include/kbengine.h does not describe
+// them: kafkabalancer_amd/csrc/engine_dev.h); returns the record count
+extern "C" int64_t kb_engine_debug_records(kb_engine* e, void* out, int64_t cap) {
+    if (!e) return KB_ERR_INVALID;
+    const int64_t n = std::min<int64_t>(e->nscan, cap);
+    HIPCHK(hipStreamSynchronize(e->st));
+    if (out && n > 0) HIPCHK(hipMemcpy(out, e->recs, (size_t)n * sizeof(RecHdr), hipMemcpyDeviceToHost));
+    return e->nscan;
+}
+
 // diagnostic: cumulative host phases of the plan calls since the last kb_engine_set_timing
 // (us): [0] reset_ctl, [1] enqueue of the batches, [2] waiting for them (the batch-end
 // transfer included), [3] log conversion, [4] kb_engine_plan calls
@@ -1704,8 +1715,7 @@ extern "C" void kb_engine_destroy(kb_engine* e) {
                     e->bset_off, e->bset_ids, e->gscr, e->pair_cnt, e->recs, e->cont, e->ctl, e->log, e->bdesc, e->ubdesc,
                     e->L.lstart, e->L.llen, e->L.lcap, e->L.lent, e->L.ck, e->L.dpos, e->rf_dev};
     for (void* p : ptrs) if (p) hipFree(p);
-    if (e->sum_buf) hipFree(e->sum_buf);
-    if (e->gath_buf) hipFree(e->gath_buf);
+    if (e->gath_buf) hipFree(e->gath_buf);         // (sum_buf is a slot of it)
     if (e->comm) { hipStreamSynchronize(e->st); rccl_api().comm_destroy(e->comm); }
     if (e->h_ctl) hipHostFree(e->h_ctl);
     if (e->h_flag) hipHostFree(e->h_flag);
@@ -1935,13 +1945,12 @@ static int ensure_xbufs(kb_engine* e) {
     const int64_t sb = (int64_t)summary_bytes(e->sum_keys);
     if (sb == e->xbuf_bytes && e->sum_buf) return KB_OK;
     HIPCHK(hipStreamSynchronize(e->st));
-    if (e->sum_buf) hipFree(e->sum_buf);
     if (e->gath_buf) hipFree(e->gath_buf);
     e->sum_buf = e->gath_buf = nullptr;
-    HIPCHK(hipMalloc((void**)&e->sum_buf, (size_t)sb));
+    // in-place all-gather: this rank's summary is its own slot of the gathered buffer
     HIPCHK(hipMalloc((void**)&e->gath_buf, (size_t)sb * e->nranks));
-    HIPCHK(hipMemset(e->sum_buf, 0, (size_t)sb));
     HIPCHK(hipMemset(e->gath_buf, 0, (size_t)sb * e->nranks));
+    e->sum_buf = e->gath_buf + (size_t)sb * e->rank;
     e->xbuf_bytes = sb;
     return KB_OK;
 }

@@ -722,6 +722,7 @@ __device__ __forceinline__ double dec(unsigned long long e) {
     return u2d(u);
 }
 
+
 // the control values one scan round runs on (from DevCtl)
 struct ScanParams {
     int run;
@@ -761,7 +762,7 @@ template <> struct ScanTabs<true> { RfMem rf; I32Mem pos; I32Mem blm; };
 
 // One scan round of a workgroup over its tiles (its first tile and the tables already
 // loaded into A / T): stage the tables, score, write the workgroup record.
-template <int RC, bool LSETS, bool INCR, bool GT>
+template <int RC, bool LSETS, bool INCR, bool GT, bool BK>
 __device__ __forceinline__ void scan_round(const ScanArgs& a, const ScanParams& q, unsigned char* smem,
                                            PartRaw<RC>& A, const TabRaw& TR,
                                            unsigned long long t_in,
@@ -795,6 +796,8 @@ __device__ __forceinline__ void scan_round(const ScanArgs& a, const ScanParams& 
     __shared__ uint32_t s_nk;
     __shared__ unsigned long long s_benc[2];
     __shared__ uint32_t s_bslot[2], s_nkk[2];
+    __shared__ unsigned long long s_bke[2][NW];      // per wave and kind: its best non-census key
+    __shared__ Contender s_bkc[2][NW];
 
     int tile = wg;
     // the lookup tables (loaded by the caller with the control block when they are small)
@@ -835,6 +838,7 @@ __device__ __forceinline__ void scan_round(const ScanArgs& a, const ScanParams& 
     for (int i = tid; i < DEDUP_SCAN; i += SCAN_THREADS) { s_key[i] = NONE32; s_wb[i] = NONE64; s_it[i] = NONE64; }
     if (tid == 0) s_nk = 0;
     if (tid < 2) { s_benc[tid] = NONE64; s_bslot[tid] = NONE32; s_nkk[tid] = 0; }
+    if (tid < 2 * NW) (&s_bke[0][0])[tid] = NONE64;
     const bool run = q.run != 0;
     const double inv_avg = q.inv_avg, eps = q.eps;
     const double ubL = q.ubL, ubN = q.ubN;
@@ -997,6 +1001,49 @@ __device__ __forceinline__ void scan_round(const ScanArgs& a, const ScanParams& 
         const bool hasL = __ballot(lL < HUGE_VAL && lL <= ubL + 12.0 * eps) != 0;
         const bool hasN = __ballot(lN < HUGE_VAL && lN <= ubN + 12.0 * eps) != 0;
         const double tL = hasL ? wave_min(lL) : HUGE_VAL, tN = hasN ? wave_min(lN) : HUGE_VAL;
+        // A scored wave the census gate kept out still keeps its best candidate per kind (in
+        // its slot of s_bk*, the minimum over its tiles): a workgroup whose waves all stayed
+        // out of the census carries that as its record's best key, so every workgroup that
+        // scored carries one.  The next step's census bound ub is the minimum of the records'
+        // best keys re-scored; with keys only from the census waves -- the few around the
+        // step's minimum, most often just the winning move -- no key survived the move and
+        // the bound went open on every step (c3nl: 4000 of 5400 waves walked their targets,
+        // 0.47 ms/step).  The record's minimum and key list stay the census waves' (k_step's
+        // windows); this key only bounds.  (The lane holding the wave minimum finds its
+        // (partition, slot) again by re-scoring its two partitions, the same arithmetic, rather
+        // than the scoring loop carrying an argmin in registers for every lane.)
+        if (BK && !census_off) {
+            const bool needL = !hasL && a.allow_leader && __ballot(lL < HUGE_VAL);
+            const bool needN = !hasN && __ballot(lN < HUGE_VAL);
+            const double wL = needL ? wave_min(lL) : HUGE_VAL, wN = needN ? wave_min(lN) : HUGE_VAL;
+            const unsigned long long bl = needL ? __ballot(lL == wL) : 0ull, bn = needN ? __ballot(lN == wN) : 0ull;
+            const bool myL = bl && lane == __ffsll((long long)bl) - 1, myN = bn && lane == __ffsll((long long)bn) - 1;
+            if ((myL && enc(wL) < s_bke[0][wid]) || (myN && enc(wN) < s_bke[1][wid])) {
+                for (int j = 0; j < PER_LANE; j++) {
+                    const uint32_t m = P.mt(j);
+                    const int nrep = (int)meta_nrep(m);
+                    uint32_t reps[RC];
+                    for (int k = 0; k < RC; k++) reps[k] = P.rp(k, j);
+                    int nelig;
+                    const int tb0 = first_target<RC, LSETS>(a, s_set, set_of<RC, LSETS>(P, j), reps, nrep, &nelig);
+                    if (!(base + j < a.shard_end && meta_elig(m) && nrep > 0 && tb0 >= 0)) continue;
+                    const double delta = P.wt(j) * inv_avg;
+                    const double dt = dtgt_f(s_rf[tb0], delta);
+                    for (int k = 0; k < nrep && k < RC; k++) {
+                        const int kind = k ? 1 : 0;
+                        if (!(kind ? myN : myL)) continue;
+                        const double d = dsrc_f(s_rf[reps[k]], delta) + dt;
+                        const unsigned long long e = enc(d);
+                        if (d != (kind ? wN : wL) || !(e < s_bke[kind][wid])) continue;
+                        Contender c;
+                        c.s = (int)reps[k]; c.t = tb0; c.w = P.wt(j); c.kind = kind; c.pad = 0;
+                        c.iter = ((unsigned long long)(base + j) << 21) | ((unsigned long long)k << 16) |
+                                 (unsigned long long)s_pos[tb0];
+                        s_bke[kind][wid] = e; s_bkc[kind][wid] = c;
+                    }
+                }
+            }
+        }
 #ifdef KB_WALK_COUNTS
         if (lane == 0) {
             KB_COUNT(a.ctl, 7, 1);                                  // waves scored
@@ -1175,7 +1222,12 @@ __device__ __forceinline__ void scan_round(const ScanArgs& a, const ScanParams& 
         r.nkk[1] = (uint16_t)min(s_nkk[1], 0xFFFFu);
 #pragma unroll
         for (int k = 0; k < 2; k++) {
-            if (s_bslot[k] != NONE32) r.best[k] = dedup_entry(T, (int)s_bslot[k]);
+            if (s_bslot[k] != NONE32) { r.best[k] = dedup_entry(T, (int)s_bslot[k]); continue; }
+            // no census key: the best key of the waves outside the census (or none)
+            int bw = -1;
+            unsigned long long be = NONE64;
+            for (int x = 0; x < NW; x++) if (s_bke[k][x] < be) { be = s_bke[k][x]; bw = x; }
+            if (bw >= 0) r.best[k] = s_bkc[k][bw];
             else { r.best[k].s = r.best[k].t = -1; r.best[k].w = 0.0; r.best[k].iter = NONE64; r.best[k].kind = k; r.best[k].pad = 0; }
         }
         stobj_wt(hdr, r);
@@ -1197,7 +1249,7 @@ __device__ __attribute__((noinline)) void refresh_in_scan(const RefreshArgs* rfp
                                                           uint32_t part, double* buf, int ng);   // (k_refresh below)
 __device__ __attribute__((noinline)) void eager_refold(const RefreshArgs* rfp, int k, double* buf, int cap);
 
-template <int RC, bool LSETS, bool INCR, bool GT>
+template <int RC, bool LSETS, bool INCR, bool GT, bool BK = false>
 __device__ __forceinline__ void scan_kernel_body(const ScanArgs& a) {
     extern __shared__ __align__(16) unsigned char smem[];
     __shared__ int s_li;
@@ -1295,7 +1347,7 @@ __device__ __forceinline__ void scan_kernel_body(const ScanArgs& a) {
         c0 = d0.blk * BLK;
         load_parts<RC, LSETS>(a, c0 + (long long)(threadIdx.x & 63) * PER_LANE, A);
     }
-    scan_round<RC, LSETS, INCR, GT>(a, q, smem, A, TR, t_in, (int)blockIdx.x, c0);
+    scan_round<RC, LSETS, INCR, GT, BK>(a, q, smem, A, TR, t_in, (int)blockIdx.x, c0);
 }
 
 template <int RC, bool LSETS, bool INCR, bool GT = false>
@@ -3473,7 +3525,9 @@ __global__ __launch_bounds__(STEP_THREADS) void k_step(StepArgs a) {
 // workgroup waits for was dispatched before it or on another XCD: no wait can starve.
 // (Replaces the k_step launch of a pair: its dispatch gap behind the scan and the staging
 // round trip leave the step's critical path.)
-template <int RC, bool LSETS>
+// (BK: the scanning workgroups keep bound keys -- the best key of every scored wave outside
+// the census, scan_round -- the instantiation launched for plans without -allow-leader)
+template <int RC, bool LSETS, bool BK = false>
 __global__ __launch_bounds__(SCAN_THREADS) void k_pair(ScanArgs a, StepArgs sa) {
     static_assert(SCAN_THREADS == STEP_THREADS, "one workgroup shape for both roles");
     if ((int)blockIdx.x == (int)gridDim.x - 1) {
@@ -3484,7 +3538,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_pair(ScanArgs a, StepArgs sa) 
     // (a scanning workgroup's hand-off is write-through stores; the list and eager workgroups
     // and an in-stream refresh write plain and publish with an agent-scope release)
     const bool wt = (int)blockIdx.x < a.nscan && !(a.rfpass && a.ctl->halted == H_NEED_EXACT);
-    scan_kernel_body<RC, LSETS, false, false>(a);
+    scan_kernel_body<RC, LSETS, false, false, BK>(a);
     // publish (MI355X_MICROARCH.md, inter-workgroup visibility): every wave drains its stores,
     // then one lane (after an L2 write-back where the stores were plain) counts the
     // workgroup in
@@ -3841,6 +3895,7 @@ __global__ __launch_bounds__(1024) void k_summary(SumArgs a) {
     __syncthreads();
     auto ins = [&](const Contender& c) {
         const double g = s_g[c.kind];
+        if (!(g < HUGE_VAL)) return;               // (no census wave on this rank for the kind)
         if (!(cont_delta(a.r, c, inv_avg) <= g + 4.0 * eps)) return;
         if (dedup_insert(T, c.kind, c.s, c.t, c.w, c.iter) < 0) s_fail = 1;
     };
@@ -4056,16 +4111,24 @@ void launch_step(const StepArgs& a, hipStream_t st) {
 // the fused pair (k_pair) for the device slot counts of the common replication factors
 bool pair_supported(int rc) { return rc == 3 || rc == 4; }
 
-template <int RC>
-static int pair_attr(bool lds_sets, size_t lds, int* static_lds) {
+template <int RC, bool BK>
+static int pair_attr1(bool lds_sets, size_t lds, int* static_lds) {
     hipFuncAttributes fa;
-    const void* f = lds_sets ? (const void*)k_pair<RC, true> : (const void*)k_pair<RC, false>;
+    const void* f = lds_sets ? (const void*)k_pair<RC, true, BK> : (const void*)k_pair<RC, false, BK>;
     if (hipFuncGetAttributes(&fa, f) != hipSuccess) return -1;
     *static_lds = (int)fa.sharedSizeBytes;
     int n = 0;
-    if (lds_sets) hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_pair<RC, true>, SCAN_THREADS, lds);
-    else hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_pair<RC, false>, SCAN_THREADS, lds);
+    if (lds_sets) hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_pair<RC, true, BK>, SCAN_THREADS, lds);
+    else hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_pair<RC, false, BK>, SCAN_THREADS, lds);
     return n;
+}
+// (both instantiations: the grid is sized so every workgroup is resident in either)
+template <int RC>
+static int pair_attr(bool lds_sets, size_t lds, int* static_lds) {
+    int s0 = 0, s1 = 0;
+    const int n0 = pair_attr1<RC, false>(lds_sets, lds, &s0), n1 = pair_attr1<RC, true>(lds_sets, lds, &s1);
+    *static_lds = s0 > s1 ? s0 : s1;
+    return n0 < n1 ? n0 : n1;
 }
 
 int pair_blocks_per_cu(int rc, bool lds_sets, size_t lds, int* static_lds) {
@@ -4076,13 +4139,21 @@ int pair_blocks_per_cu(int rc, bool lds_sets, size_t lds, int* static_lds) {
 
 void launch_pair(const ScanArgs& a, const StepArgs& sa, int rc, bool lds_sets, size_t lds, hipStream_t st) {
     const int grid = a.nscan + (a.listwg ? 1 : 0) + a.eager + 1;
+    // bound keys for plans without -allow-leader: there every step moves another partition
+    // and the census waves' keys rarely outlive it (the -allow-leader headline keeps the
+    // instantiation without them: its kernel is unchanged)
+    const bool bk = !a.allow_leader;
+#define KB_PAIR_LAUNCH(R, L)                                                                          \
+    do {                                                                                              \
+        if (bk) hipLaunchKernelGGL((k_pair<R, L, true>), dim3(grid), dim3(SCAN_THREADS), lds, st, a, sa);  \
+        else hipLaunchKernelGGL((k_pair<R, L, false>), dim3(grid), dim3(SCAN_THREADS), lds, st, a, sa);    \
+    } while (0)
     if (rc == 3) {
-        if (lds_sets) hipLaunchKernelGGL((k_pair<3, true>), dim3(grid), dim3(SCAN_THREADS), lds, st, a, sa);
-        else hipLaunchKernelGGL((k_pair<3, false>), dim3(grid), dim3(SCAN_THREADS), lds, st, a, sa);
+        if (lds_sets) KB_PAIR_LAUNCH(3, true); else KB_PAIR_LAUNCH(3, false);
     } else {
-        if (lds_sets) hipLaunchKernelGGL((k_pair<4, true>), dim3(grid), dim3(SCAN_THREADS), lds, st, a, sa);
-        else hipLaunchKernelGGL((k_pair<4, false>), dim3(grid), dim3(SCAN_THREADS), lds, st, a, sa);
+        if (lds_sets) KB_PAIR_LAUNCH(4, true); else KB_PAIR_LAUNCH(4, false);
     }
+#undef KB_PAIR_LAUNCH
 }
 
 void launch_listop(DevCtl* ctl, const Lists& L, hipStream_t st) {

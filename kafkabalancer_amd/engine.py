@@ -130,6 +130,9 @@ def lib():
         L.kb_engine_sharded_resolve.restype = C.c_int
         L.kb_engine_sharded_collect.argtypes = [vp, C.POINTER(kb_change), C.c_int64, P64]
         L.kb_engine_sharded_collect.restype = C.c_int
+        if hasattr(L, "kb_engine_debug_records"):       # (diagnostic)
+            L.kb_engine_debug_records.argtypes = [vp, vp, C.c_int64]
+            L.kb_engine_debug_records.restype = C.c_int64
         if hasattr(L, "kb_engine_ctl_scalars"):         # (diagnostic)
             L.kb_engine_ctl_scalars.argtypes = [vp, PD, C.c_int]
             L.kb_engine_ctl_scalars.restype = C.c_int
@@ -419,6 +422,17 @@ class Engine:
         us = np.zeros(5)
         lib().kb_engine_host_timings(self.h, us.ctypes.data_as(PD), 5)
         return {"reset": us[0], "enqueue": us[1], "wait": us[2], "convert": us[3], "calls": int(us[4])}
+
+    def debug_records(self):
+        """Diagnostic: the last scan's record headers as a numpy structured array."""
+        ct = np.dtype([("s", "<i4"), ("t", "<i4"), ("w", "<f8"), ("iter", "<u8"), ("kind", "<i4"), ("pad", "<i4")])
+        dt = np.dtype([("dmin", "<f8", 2), ("cand", "<u8", 2), ("nkeys", "<u4"), ("flags", "<u4"),
+                       ("fmask", "<u4"), ("nkk", "<u2", 2), ("best", ct, 2)])
+        assert dt.itemsize == 112
+        n = lib().kb_engine_debug_records(self.h, None, 0)
+        out = np.zeros(max(n, 1), dt)
+        lib().kb_engine_debug_records(self.h, out.ctypes.data_as(C.c_void_p), n)
+        return out[:n]
 
     def ctl_scalars(self):
         """Diagnostic: the control block's scalars for the next step (ub per kind, eps, U0, V,

@@ -37,3 +37,36 @@ def test_cpu_engine_matches_oracle(case):
         assert (c["step"], c["pidx"], c["from_"], c["to"], c["slot"]) == (r["step"], r["pidx"], r["from_"], r["to"], r["slot"]), k
         assert (c["su"], c["cu"]) == (r["su"], r["cu"]), k
     ce.close()
+
+
+@pytest.mark.parametrize("thr", [1, 4])
+def test_cpu_engine_first_index_stages_match_oracle(thr):
+    """c4's shape (broker add / decommission, replica-count changes): RemoveExtraReplicas,
+    AddMissingReplicas and MoveDisallowedReplicas (steps.go:70-143) before move(), against
+    the oracle step for step."""
+    import numpy as np
+    P, B = 3000, 80
+    rng = np.random.default_rng(11)
+    nr = np.zeros(P, np.int64)
+    pick = rng.choice(P, size=60, replace=False)
+    nr[pick[:30]] = 2
+    nr[pick[30:]] = 4
+    cl = synth.make_cluster(P, B, 3, "zipf", seed=0x5EED4404, with_names=True, num_replicas=nr)
+    cfg = default_cfg(min_unbalance=0.0)
+    cfg["brokers"] = [b for b in range(1, 91) if not 79 <= b <= 80]
+    ce = cpu_engine.CpuEngine(cl, cfg, threads=thr)
+    o = O.OraclePL(synth.to_plist(cl))
+    seen = set()
+    for k in range(420):
+        r = O.balance(o, cfg, O.SEM_APPLIED)
+        c = ce.step()
+        if r["status"] != 1:
+            assert c is None, (k, c)
+            break
+        assert c is not None, (k, r)
+        seen.add(r["step"])
+        assert (c["step"], c["pidx"], c["from_"], c["to"], c["slot"]) == (r["step"], r["pidx"], r["from_"], r["to"], r["slot"]), k
+        if r["step"] in ("MoveLeaders", "MoveNonLeaders"):
+            assert (c["su"], c["cu"]) == (r["su"], r["cu"]), k
+    assert {"RemoveExtraReplicas", "AddMissingReplicas", "MoveDisallowedReplicas", "MoveNonLeaders"} <= seen, seen
+    ce.close()

@@ -8,7 +8,8 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 LIB = os.path.join(ROOT, "kafkabalancer_amd", "lib", "libkbcpu.so")
-STEPS = {7: "MoveLeaders", 8: "MoveNonLeaders"}
+STEPS = {3: "RemoveExtraReplicas", 4: "AddMissingReplicas", 5: "MoveDisallowedReplicas",
+         7: "MoveLeaders", 8: "MoveNonLeaders"}
 _lib = None
 
 
@@ -53,12 +54,15 @@ class CpuEngine:
                                          int(bool(cfg.get("allow_leader"))), int(cfg.get("min_replicas", 2)),
                                          float(cfg.get("min_unbalance", 0.01)), int(threads))
         if not self.h:
-            raise ValueError("cluster outside the CPU engine's scope (first-index stages)")
+            raise ValueError("cluster outside the CPU engine's scope (empty replica lists or > 64 slots)")
 
     def step(self):
         oi = (C.c_int64 * 5)()
         od = (C.c_double * 2)()
-        if lib().cpu_engine_step(self.h, oi, od) != 1:
+        rc = lib().cpu_engine_step(self.h, oi, od)
+        if rc < 0:
+            raise RuntimeError("%s: the reference errors here" % STEPS.get(oi[0], "step"))
+        if rc != 1:
             return None
         return {"step": STEPS[oi[0]], "pidx": oi[1], "slot": oi[2], "from_": oi[3], "to": oi[4],
                 "su": od[0], "cu": od[1]}

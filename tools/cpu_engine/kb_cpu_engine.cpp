@@ -13,9 +13,13 @@
 //     exact loads: E = 0) is refolded exactly in the reference's order and the
 //     lexicographic (U, iteration index) minimum wins (steps.go:211);
 //   * MoveLeaders then MoveNonLeaders (steps.go:284-298), cu < su - MinUnbalance.
-// Scope: move() plans (the first-index stages RemoveExtra / AddMissing /
-// MoveDisallowed / ReassignLeaders are not implemented; create refuses a cluster that
-// would reach them), applied semantics.
+//   * the first-index stages before move() (steps.go:70-143): the first partition whose
+//     replica count differs from NumReplicas (RemoveExtraReplicas / AddMissingReplicas) or
+//     that holds a replica outside its allowed list (MoveDisallowedReplicas), found by a
+//     parallel first-index search, then the reference's pick over the allowed list sorted by
+//     (load, id) (utils.go:66-90).
+// Scope: applied semantics, no ReassignLeaders (create refuses a cluster with an error
+// stage: an empty replica list).
 #include <omp.h>
 
 #include <algorithm>
@@ -48,6 +52,7 @@ struct Engine {
     std::vector<double> w;
     std::vector<int32_t> nc;
     std::vector<uint8_t> elig;
+    std::vector<int32_t> want;               // NumReplicas (after FillDefaults)
     std::vector<int32_t> pset;               // set index
     std::vector<std::vector<uint8_t>> setmask;   // [nsets][B]
     std::vector<uint8_t> incfg;              // -broker-ids member
@@ -96,17 +101,20 @@ void* cpu_engine_create(int64_t n, const int64_t* rid, const int64_t* roff, cons
     std::unordered_map<int64_t, int> dm;
     for (int i = 0; i < e->B; i++) dm[all[i]] = i;
     int rc = 1;
-    for (int64_t i = 0; i < n; i++) rc = std::max<int>(rc, (int)(roff[i + 1] - roff[i]));
+    for (int64_t i = 0; i < n; i++)
+        rc = std::max<int>(rc, (int)std::max<int64_t>(roff[i + 1] - roff[i], num_replicas[i]));   // (room for adds)
+    if (rc > 64) { delete e; return nullptr; }
     e->RC = rc;
     e->rep.assign((size_t)n * rc, -1);
     e->nrep.resize(n); e->w.assign(weight, weight + n); e->nc.assign(n, 0);
-    e->elig.resize(n); e->pset.resize(n);
+    e->elig.resize(n); e->pset.resize(n); e->want.resize(n);
     for (int64_t i = 0; i < n; i++) {
         e->nrep[i] = (int8_t)(roff[i + 1] - roff[i]);
+        if (e->nrep[i] == 0) { delete e; return nullptr; }               // (a panic path: not in scope)
         for (int k = 0; k < e->nrep[i]; k++) e->rep[(size_t)i * rc + k] = dm[rid[roff[i] + k]];
         if (num_consumers) e->nc[i] = (int32_t)num_consumers[i];
         e->elig[i] = num_replicas[i] >= min_replicas;
-        if (num_replicas[i] != e->nrep[i]) { delete e; return nullptr; }   // Remove/Add stage
+        e->want[i] = (int32_t)num_replicas[i];
     }
     e->incfg.assign(e->B, 0);
     if (!brokers_nil) for (int64_t k = 0; k < nbrokers; k++) e->incfg[dm[brokers[k]]] = 1;
@@ -121,12 +129,7 @@ void* cpu_engine_create(int64_t n, const int64_t* rid, const int64_t* roff, cons
         else if (e->cnt[b]) e->setmask[nsets][b] = 1;                  // getBrokerList (utils.go:49-64)
         refold(*e, b);
     }
-    for (int64_t i = 0; i < n; i++) {
-        e->pset[i] = set_idx && set_idx[i] >= 0 ? (int32_t)set_idx[i] : (int32_t)nsets;
-        const std::vector<uint8_t>& m = e->setmask[e->pset[i]];
-        for (int k = 0; k < e->nrep[i]; k++)
-            if (!m[e->rep[(size_t)i * rc + k]] || !e->cnt[e->rep[(size_t)i * rc + k]]) { delete e; return nullptr; }  // Disallowed
-    }
+    for (int64_t i = 0; i < n; i++) e->pset[i] = set_idx && set_idx[i] >= 0 ? (int32_t)set_idx[i] : (int32_t)nsets;
     return e;
 }
 
@@ -136,8 +139,117 @@ int64_t cpu_engine_candidates(void* h) { return ((Engine*)h)->cand_total; }
 
 // One Balance() of the move() steps; returns 1 change (out: kind step 7/8, partition,
 // slot, from id, to id, su, cu), 0 no change.
+// the brokers of a partition's allowed list sorted by (load, id), brokers absent from the
+// load map at 0 (getBrokerListByLoad, utils.go:66-79), or only those holding a replica
+// (getBrokerListByLoadBL over getBL, utils.go:81-90)
+static std::vector<int> by_load(const Engine& e, int set, bool present_only) {
+    std::vector<int> v;
+    for (int b = 0; b < e.B; b++)
+        if (e.setmask[set][b] && (!present_only || e.cnt[b])) v.push_back(b);
+    std::sort(v.begin(), v.end(), [&](int x, int y) {
+        const double lx = e.cnt[x] ? e.load[x] : 0.0, ly = e.cnt[y] ? e.load[y] : 0.0;
+        return lx != ly ? lx < ly : x < y;
+    });
+    return v;
+}
+
+// the partition's replica list changed: move it between the per-broker lists and refold
+// every broker whose contribution changed (the leader's is W * (len(R) + NumConsumers))
+static void relist_partition(Engine& e, int64_t p, const std::vector<int>& before) {
+    const int32_t* rp = &e.rep[(size_t)p * e.RC];
+    std::vector<int> after(rp, rp + e.nrep[p]);
+    for (int b : before)
+        if (std::find(after.begin(), after.end(), b) == after.end()) {
+            auto& l = e.lists[b];
+            l.erase(std::lower_bound(l.begin(), l.end(), p));
+            e.cnt[b]--;
+        }
+    for (int b : after)
+        if (std::find(before.begin(), before.end(), b) == before.end()) {
+            auto& l = e.lists[b];
+            l.insert(std::lower_bound(l.begin(), l.end(), p), p);
+            e.cnt[b]++;
+        }
+    std::vector<int> touched(before);
+    touched.insert(touched.end(), after.begin(), after.end());
+    std::sort(touched.begin(), touched.end());
+    touched.erase(std::unique(touched.begin(), touched.end()), touched.end());
+    for (int b : touched) refold(e, b);
+}
+
+// RemoveExtraReplicas / AddMissingReplicas / MoveDisallowedReplicas (steps.go:70-143):
+// 1 = a change (out as cpu_engine_step), 0 = none of them applies, -1 = the reference's error
+static int first_index_stages(Engine& e, int64_t* out_i, double* out_d) {
+    const int64_t P = e.P;
+    int64_t fr = P, fa = P, fd = P;
+#pragma omp parallel for num_threads(e.threads) reduction(min : fr, fa, fd) schedule(static)
+    for (int64_t p = 0; p < P; p++) {
+        if (e.want[p] < e.nrep[p]) fr = std::min(fr, p);
+        if (e.want[p] > e.nrep[p]) fa = std::min(fa, p);
+        const std::vector<uint8_t>& m = e.setmask[e.pset[p]];
+        const int32_t* rp = &e.rep[(size_t)p * e.RC];
+        for (int k = 0; k < e.nrep[p]; k++) if (!m[rp[k]]) { fd = std::min(fd, p); break; }
+    }
+    out_d[0] = out_d[1] = 0.0;
+    auto emit = [&](int step, int64_t p, int slot, int from, int to) {
+        out_i[0] = step; out_i[1] = p; out_i[2] = slot;
+        out_i[3] = from >= 0 ? e.ids[from] : -1; out_i[4] = to >= 0 ? e.ids[to] : -1;
+        return 1;
+    };
+    if (fr < P) {                                    // steps.go:70-89: the lightest allowed replica
+        const int64_t p = fr;
+        int32_t* rp = &e.rep[(size_t)p * e.RC];
+        const std::vector<int> before(rp, rp + e.nrep[p]);
+        for (int b : by_load(e, e.pset[p], false)) {
+            int slot = -1;
+            for (int k = 0; k < e.nrep[p] && slot < 0; k++) if (rp[k] == b) slot = k;
+            if (slot < 0) continue;
+            for (int k = slot; k + 1 < e.nrep[p]; k++) rp[k] = rp[k + 1];   // replacepl(-1): the first slot
+            rp[--e.nrep[p]] = -1;
+            relist_partition(e, p, before);
+            return emit(3, p, slot, b, -1);
+        }
+        return -1;
+    }
+    if (fa < P) {                                    // steps.go:93-113: the heaviest allowed non-replica
+        const int64_t p = fa;
+        int32_t* rp = &e.rep[(size_t)p * e.RC];
+        const std::vector<int> before(rp, rp + e.nrep[p]);
+        const std::vector<int> v = by_load(e, e.pset[p], false);
+        for (int i = (int)v.size() - 1; i >= 0; i--) {
+            const int b = v[i];
+            if (std::find(before.begin(), before.end(), b) != before.end()) continue;
+            if (e.nrep[p] >= e.RC) return -1;
+            rp[e.nrep[p]++] = b;                     // addpl
+            relist_partition(e, p, before);
+            return emit(4, p, e.nrep[p] - 1, -1, b);
+        }
+        return -1;
+    }
+    if (fd < P) {                                    // steps.go:117-143: the heaviest allowed holder
+        const int64_t p = fd;
+        int32_t* rp = &e.rep[(size_t)p * e.RC];
+        const std::vector<int> before(rp, rp + e.nrep[p]);
+        const std::vector<int> v = by_load(e, e.pset[p], true);
+        const std::vector<uint8_t>& m = e.setmask[e.pset[p]];
+        int slot = -1;
+        for (int k = 0; k < e.nrep[p] && slot < 0; k++) if (!m[rp[k]] || !e.cnt[rp[k]]) slot = k;
+        for (int i = (int)v.size() - 1; i >= 0; i--) {
+            const int b = v[i];
+            if (std::find(before.begin(), before.end(), b) != before.end()) continue;
+            const int from = rp[slot];
+            rp[slot] = b;                            // replacepl at the slot
+            relist_partition(e, p, before);
+            return emit(5, p, slot, from, b);
+        }
+        return -1;
+    }
+    return 0;
+}
+
 int cpu_engine_step(void* h, int64_t* out_i, double* out_d) {
     Engine& e = *(Engine*)h;
+    if (const int r = first_index_stages(e, out_i, out_d); r != 0) return r;
     const int B = e.B, RC = e.RC;
     // bl: brokers in the load map or in -broker-ids (steps.go:150-157), by (load, id)
     std::vector<int> bl;
