@@ -24,7 +24,7 @@ def main():
         for ln in open(pr):
             x = json.loads(ln)
             print("probe", x["k"], x["pidx"], "d=%.3e ub0=%.3e ub1=%.3e" % (x["d"], x["ub0"], x["ub1"]), x.get("rec"))
-    for wl in ("c3", "c3nl", "c5"):
+    for wl in ("c2", "c3", "c3nl", "c5"):
         x = last_json(os.path.join(d, wl + ".json"))
         if not x:
             continue
