@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define KB_ABI_VERSION 9
+#define KB_ABI_VERSION 10
 
 /* step indices == position in the reference's steps table (balancer.go:34-44) */
 enum kb_step {
@@ -147,6 +147,8 @@ typedef struct {
     int64_t relists;                /* per-broker partition lists laid out again after one ran
                                        out of slack (kb_config.list_slack, ABI 8) */
     int64_t fused_pairs;            /* 1: a plan's scan + step run as one launch (k_pair, ABI 8) */
+    int64_t fused_summaries;        /* 1: a sharded scan and its rank summary run as one launch
+                                       (k_scansum, ABI 10) */
 } kb_stats;
 
 typedef struct kb_engine kb_engine;

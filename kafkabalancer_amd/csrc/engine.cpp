@@ -97,6 +97,7 @@ struct kb_engine {
     unsigned char* gscr = nullptr;    // k_step's per-broker tables past MAXB brokers (StepArgs.gscr)
     uint32_t* pair_cnt = nullptr;     // k_pair's arrival count (ScanArgs.done / StepArgs.wait_cnt)
     bool fuse = false;                // pairs run as one k_pair launch (scan grid + step workgroup)
+    bool fuse_sum = false;            // sharded scans: scan + rank summary as one k_scansum launch
     int fuse_pre = 1;                 // k_pair stages the tables before its wait (KB_FUSE_PRE=0: after)
     size_t pair_lds = 0;              // k_pair's dynamic LDS: max(scan, step)
     bool gb = false;                  // B > MAXB: broker tables in memory (k_scan GT, k_step GB)
@@ -169,6 +170,7 @@ struct kb_engine {
     unsigned char* gath_buf = nullptr;
     int64_t xbuf_bytes = 0;            // summary bytes the buffers were sized for
     unsigned long long pair_wait_ticks = 200000000ull;   // k_pair's wait bound: 2 s of the 100 MHz clock
+    int pair_acq = 0;                                     // k_pair: acquire after the wait always (A/B)
     std::string last_err;
 };
 
@@ -179,9 +181,20 @@ static double now_us() {
                       std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
-// after a k_pair timeout (run_steps) every step entry point refuses with this
+// a fused launch's waiting workgroup (k_pair's step, k_scansum's summary) gave up on its grid:
+// the stragglers still counted themselves in, so the arrival count is reset once the
+// stream is idle, and the engine takes no more work
+static int poison_after_timeout(kb_engine* e) {
+    HIPCHK(hipStreamSynchronize(e->st));
+    HIPCHK(hipMemsetAsync(e->pair_cnt, 0, PAIR_SHARDS * PAIR_STRIDE * 4, e->st));
+    HIPCHK(hipStreamSynchronize(e->st));
+    e->dead = true;
+    return KB_OK;
+}
+
+// after a fused launch's timeout every step entry point refuses with this
 static int dead_result(kb_engine* e) {
-    e->last_err = "engine unusable: an earlier fused scan + step launch timed out waiting for its grid";
+    e->last_err = "engine unusable: an earlier fused launch (scan + step or scan + summary) timed out waiting for its grid";
     return KB_ERR_HIP;
 }
 
@@ -609,6 +622,7 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
     if (const char* v = getenv("KB_EAGER")) e->eager = e->rf_stream && *v == '1';          // diagnostic
     e->nscan = std::min<int64_t>(e->ntiles, std::max<int64_t>(1, (int64_t)per_cu * ncu - (e->eager ? EGW + 1 : 0)));
     if (const char* v = getenv("KB_NSCAN")) if (atoi(v) > 0) e->nscan = std::min<int64_t>(e->ntiles, atoi(v));  // diagnostic
+    e->nscan = std::min<int64_t>(e->nscan, SUM_RECS);     // (a rank summary reads one record per thread)
     if (const char* v = getenv("KB_DEBUG_SCAN")) e->dbg_scan = atoi(v);                                   // diagnostic
     {
         // k_step's LDS: static tables + per-broker arrays (+ every set's words when they fit)
@@ -634,6 +648,7 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
         if (const char* v = getenv("KB_FUSE")) e->fuse = e->fuse && *v != '0';                      // A/B
         if (const char* v = getenv("KB_FUSE_PRE")) e->fuse_pre = *v != '0';                          // diagnostic
         if (const char* v = getenv("KB_PAIR_WAIT_TICKS")) e->pair_wait_ticks = strtoull(v, nullptr, 10);   // tests
+        if (const char* v = getenv("KB_PAIR_ACQ")) e->pair_acq = *v == '1';                          // A/B
         if (e->fuse) {
             e->pair_lds = std::max(e->scan_lds, (size_t)e->step_lds_bytes);
             int pst = 0;
@@ -643,6 +658,18 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
             // eager ones and the step workgroup)
             else e->nscan = std::min<int64_t>(e->ntiles, std::max<int64_t>(1, (int64_t)pcu * ncu -
                                               (e->eager ? EGW + 1 : (e->integral ? 0 : 1)) - 1));
+        }
+        // the sharded protocol's scan + rank summary as one launch (k_scansum): the scan's
+        // grid plus one resident summary workgroup; every workgroup resident at once, as in
+        // k_pair (an engine whose k_pair grid would have to shrink for it keeps two launches)
+        e->fuse_sum = !e->gb && pair_supported(e->rc_dev) && e->nsets <= (int64_t)MAX_SETS && e->nscan > 1;
+        if (const char* v = getenv("KB_FUSE_SUM")) e->fuse_sum = e->fuse_sum && *v != '0';          // A/B
+        if (e->fuse_sum) {
+            int sst = 0;
+            const int scu = scansum_blocks_per_cu(e->rc_dev, e->lds_sets, e->scan_lds, &sst);
+            const int64_t cap = (int64_t)scu * ncu - (e->eager ? EGW + 1 : (e->integral ? 0 : 1)) - 1;
+            if (scu < 1 || sst + e->scan_lds > 160 * 1024 || cap < 1 || (e->fuse && cap < e->nscan)) e->fuse_sum = false;
+            else e->nscan = std::min<int64_t>(e->nscan, cap);
         }
     }
     HIPCHK(hipStreamCreateWithFlags(&e->st, hipStreamNonBlocking));
@@ -823,7 +850,7 @@ static void fill_step_args(kb_engine* e, StepArgs& a, const Recs& R, int use_spi
     a.nsets = (int)e->nsets; a.NP2 = e->NP2;
     a.sb_lds = e->sb_lds; a.lds_bytes = e->step_lds_bytes;
     a.gscr = e->gscr;
-    a.wait_cnt = e->pair_cnt; a.wait_n = 0; a.fuse_pre = 1; a.wait_ticks = e->pair_wait_ticks;
+    a.wait_cnt = e->pair_cnt; a.wait_n = 0; a.fuse_pre = 1; a.wait_ticks = e->pair_wait_ticks; a.pair_acq = e->pair_acq;
     a.setbits = e->setbits; a.setrec = e->setrec;
     a.order = e->order; a.posu = e->posu; a.blm = e->blm; a.posm = e->posm; a.r = e->r;
     a.load = e->load; a.lerr = e->lerr; a.eb = e->eb; a.bfl = e->bfl; a.cnt = e->cnt;
@@ -1260,13 +1287,8 @@ static int run_steps(kb_engine* e, int64_t max_steps) {
         roctxRangePop();
         if (e->h_ctl->logpos > lp0 && e->h_ctl->logpos <= e->logcap &&
             e->h_log[e->h_ctl->logpos - 1].err_code == E_PAIR_TIMEOUT) {
-            // a step workgroup gave up waiting for its grid: the stragglers still counted
-            // themselves in, so the arrival count is reset once the stream is idle, and the
-            // engine takes no more work (the error is returned with this batch's log)
-            HIPCHK(hipStreamSynchronize(e->st));
-            HIPCHK(hipMemsetAsync(e->pair_cnt, 0, PAIR_SHARDS * PAIR_STRIDE * 4, e->st));
-            HIPCHK(hipStreamSynchronize(e->st));
-            e->dead = true;
+            // (the error is returned with this batch's log)
+            if (const int r = poison_after_timeout(e); r != KB_OK) return r;
         }
         fresh = true;
         reuse = false;
@@ -1469,6 +1491,7 @@ extern "C" int kb_engine_stats(kb_engine* e, kb_stats* o) {
     o->blocks_scanned = (int64_t)c.total_blocks;
     o->relists = e->relists;
     o->fused_pairs = e->fuse && !e->incr ? 1 : 0;
+    o->fused_summaries = e->fuse_sum ? 1 : 0;
     return KB_OK;
 }
 
@@ -1787,6 +1810,27 @@ extern "C" int kb_engine_set_stream(kb_engine* e, void* s) {
     return KB_OK;
 }
 
+// this rank's scan and its summary into summary_dev: one k_scansum launch (the summary
+// workgroup waits in the scan's grid), or k_scan then k_summary
+static int enqueue_scan_summary(kb_engine* e, void* summary_dev) {
+    SumArgs s;
+    s.ctl = e->ctl; s.R = scan_recs(e->recs, (int)e->nscan); s.cont = e->cont; s.cont_cap = e->cont_cap;
+    s.r = e->r; s.out = summary_recs((unsigned char*)summary_dev, 1, e->sum_keys);
+    s.spill_growable = e->cont_cap < kContMax ? 1 : 0;
+    s.wait_cnt = e->pair_cnt; s.wait_n = 0; s.wait_ticks = e->pair_wait_ticks; s.log = e->log;
+    if (e->fuse_sum) {
+        ScanArgs a;
+        fill_scan_args(e, a);
+        s.wait_n = a.nscan + (a.listwg ? 1 : 0) + a.eager;
+        launch_scansum(a, s, e->rc_dev, e->lds_sets, e->scan_lds, e->st);
+    } else {
+        enqueue_scan(e);
+        launch_summary(s, e->st);
+    }
+    HIPCHK(hipGetLastError());
+    return KB_OK;
+}
+
 extern "C" int kb_engine_step_begin(kb_engine* e, void* summary_dev) {
     if (e) { e->ctl_mirror = false; e->recs_fresh = false; }            // (the device block changes behind the host copy)
     if (!e || !summary_dev) return KB_ERR_INVALID;
@@ -1794,14 +1838,7 @@ extern "C" int kb_engine_step_begin(kb_engine* e, void* summary_dev) {
     if (e->pending) return e->pending;
     if (const int rc = reset_ctl(e, 1); rc != KB_OK) return rc;
     if (!e->h_ctl->prepped) enqueue_step(e);       // prep only (nothing to resolve yet)
-    enqueue_scan(e);
-    SumArgs s;
-    s.ctl = e->ctl; s.R = scan_recs(e->recs, (int)e->nscan); s.cont = e->cont; s.cont_cap = e->cont_cap;
-    s.r = e->r; s.out = summary_recs((unsigned char*)summary_dev, 1, e->sum_keys);
-    s.spill_growable = e->cont_cap < kContMax ? 1 : 0;
-    launch_summary(s, e->st);
-    HIPCHK(hipGetLastError());
-    return KB_OK;
+    return enqueue_scan_summary(e, summary_dev);
 }
 
 // ---- batched multi-GPU steps: the host enqueues several (scan, summary, all-gather,
@@ -1820,14 +1857,8 @@ extern "C" int kb_engine_sharded_reset(kb_engine* e, int64_t budget_steps) {
 extern "C" int kb_engine_sharded_scan(kb_engine* e, void* summary_dev) {
     if (e) { e->ctl_mirror = false; e->recs_fresh = false; }            // (the device block changes behind the host copy)
     if (!e || !summary_dev) return KB_ERR_INVALID;
-    enqueue_scan(e);
-    SumArgs s;
-    s.ctl = e->ctl; s.R = scan_recs(e->recs, (int)e->nscan); s.cont = e->cont; s.cont_cap = e->cont_cap;
-    s.r = e->r; s.out = summary_recs((unsigned char*)summary_dev, 1, e->sum_keys);
-    s.spill_growable = e->cont_cap < kContMax ? 1 : 0;
-    launch_summary(s, e->st);
-    HIPCHK(hipGetLastError());
-    return KB_OK;
+    if (e->dead) return dead_result(e);
+    return enqueue_scan_summary(e, summary_dev);
 }
 
 extern "C" int kb_engine_sharded_resolve(kb_engine* e, const void* gathered_dev, int32_t n_ranks) {
@@ -1853,6 +1884,9 @@ extern "C" int kb_engine_sharded_collect(kb_engine* e, kb_change* out, int64_t c
     if (nlog) HIPCHK(hipMemcpy(logv.data(), e->log, (size_t)nlog * sizeof(ChangeDev), hipMemcpyDeviceToHost));
     int rc = KB_CHANGE;
     int64_t k = 0;
+    for (int i = 0; i < nlog; i++)
+        if (logv[i].err_code == E_PAIR_TIMEOUT)
+            if (const int r = poison_after_timeout(e); r != KB_OK) return r;
     for (int i = 0; i < nlog; i++) {
         kb_change tmp;
         const int r = convert(e, logv[i], out ? &out[k] : &tmp);
@@ -1888,6 +1922,8 @@ extern "C" int kb_engine_step_finish(kb_engine* e, const void* gathered_dev, int
         // the prep that followed the apply only asks for exact loads before the next step
         ChangeDev d;
         HIPCHK(hipMemcpy(&d, e->log, sizeof d, hipMemcpyDeviceToHost));
+        if (d.err_code == E_PAIR_TIMEOUT)
+            if (const int r = poison_after_timeout(e); r != KB_OK) return r;
         const int rc = convert(e, d, out);
         if (rc == KB_CHANGE && (c.halted == H_NEED_EXACT || c.want_refresh))
             if (const int rc = refresh(e); rc != KB_OK) return rc;

@@ -72,7 +72,30 @@ __device__ __forceinline__ void stobj_wt(T* p, const T& v) {
         __hip_atomic_store(dst + i, src[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ void st32_wt(uint32_t* p, uint32_t v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // (global address space: a global_store sc1 even where the pointer is generic)
+    __hip_atomic_store((__attribute__((address_space(1))) uint32_t*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// ... and the matching sc1 loads (L2-served: never a stale L1 line).  k_pair's step workgroup
+// reads everything the scan workgroups of its own launch stored write-through with these,
+// so after its poll it needs no agent acquire (MI355X_MICROARCH.md, valid forms: the
+// first row -- one lane's atomic add per workgroup after every wave's drain, an sc1 poll
+// of every shard, a barrier, then only sc1 loads of those bytes)
+template <typename T>
+__device__ __forceinline__ T ldobj_wt(const T* p) {
+    static_assert(sizeof(T) % 8 == 0, "8-byte granules");
+    T v;
+    unsigned long long* dst = (unsigned long long*)&v;
+    unsigned long long* src = (unsigned long long*)p;
+#pragma unroll
+    for (int i = 0; i < (int)(sizeof(T) / 8); i++)
+        dst[i] = __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return v;
+}
+__device__ __forceinline__ uint32_t ld32_wt(const void* p) {
+    return __hip_atomic_load((uint32_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ldd_wt(const double* p) {
+    return __hip_atomic_load((double*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // reference term (utils.go:136-143): r = L/avg - 1; r>0 ? r*r : r*r/2 (exact ops)
@@ -569,8 +592,9 @@ __device__ void do_list_op(DevCtl* ctl, Lists L, int* s_i) {
     else if (kind == 3) ok = list_insert(L, to, p, s_i);
     __syncthreads();
     if (threadIdx.x == 0) {
-        if (!ok) ctl->list_overflow = 1;
-        ctl->pending_list = 0;
+        // (write-through: k_pair's step workgroup reads them with sc1 loads, no acquire)
+        if (!ok) st32_wt((uint32_t*)&ctl->list_overflow, 1u);
+        st32_wt((uint32_t*)&ctl->pending_list, 0u);
     }
     __syncthreads();
 }
@@ -1387,11 +1411,11 @@ __device__ __forceinline__ void for_each_contender(const StepArgs& a, const doub
     const int nt = blockDim.x;
     for (int i = threadIdx.x; i < a.R.n; i += nt) {
         const RecHdr* h = a.R.h(i);
-        if (!(ldd(&h->dmin[kind]) <= g + 8.0 * eps)) continue;
+        if (!(ldd_wt(&h->dmin[kind]) <= g + 8.0 * eps)) continue;
         const Contender* keys = a.R.k(i);
-        const int nk = (int)min(ld32(&h->nkeys), (uint32_t)a.R.cap);
+        const int nk = (int)min(ld32_wt(&h->nkeys), (uint32_t)a.R.cap);
         for (int k = 0; k < nk; k++) {
-            const Contender c = ldobj(keys + k);
+            const Contender c = ldobj_wt(keys + k);
             if (c.kind != kind) continue;
             if (cont_delta_ld(s_ld, c, inv_avg) <= g + 4.0 * eps) f(c);
         }
@@ -1399,7 +1423,7 @@ __device__ __forceinline__ void for_each_contender(const StepArgs& a, const doub
     if (a.use_spill) {
         const uint32_t n = min(ncont, a.cont_cap);
         for (uint32_t i = threadIdx.x; i < n; i += nt) {
-            const Contender c = ldobj(a.cont + i);
+            const Contender c = ldobj_wt(a.cont + i);
             if (c.kind != kind) continue;
             if (cont_delta_ld(s_ld, c, inv_avg) <= g + 4.0 * eps) f(c);
         }
@@ -1559,7 +1583,8 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
         }
         __shared__ int s_wait_to;
         if (wid == 0) {
-            if (lane == 0) s_prehalt = ctl->halted;
+            const int ph = ctl->halted;
+            if (lane == 0) s_prehalt = ph;
             // the arrival count is sharded over PAIR_SHARDS words (a workgroup adds to the
             // shard of blockIdx % 8, the blocks that share an XCD: 32 arrivals per word instead
             // of 255 serialised on one); lanes 0..7 poll one shard each.  (A bounded wait: 2 s
@@ -1576,8 +1601,15 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
                 if (wave_sum(v) >= (uint32_t)a.wait_n) break;
                 __builtin_amdgcn_s_sleep(1);
             }
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // (the other XCDs' writes)
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            // the scanning workgroups and the list workgroup stored what this workgroup reads
+            // write-through and it reads them with sc1 loads (ldobj_wt, the control block
+            // below): no acquire.  The eager workgroups and an in-stream refresh write plain
+            // (loads, lists) and publish with a release: then the acquire, as every staged
+            // table they touch is read again with plain loads
+            if (a.pair_acq || ph == H_NEED_EXACT || (KB_EAGER_CODE && a.eager && ctl->eg_n > 0)) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // (the other XCDs' writes)
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
             if (!to && lane < PAIR_SHARDS)
                 __hip_atomic_store(a.wait_cnt + lane * PAIR_STRIDE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (lane == 0) s_wait_to = to;
@@ -1596,8 +1628,10 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
             return;
         }
         t_in = wall_clock64();
-        ts_b = ctl->ts_beg; ts_e = ctl->ts_end; ts_pe = ctl->ts_prev_end;
-        if (tid < CTL_WORDS) ((uint32_t*)&C)[tid] = ((const uint32_t*)ctl)[tid];
+        ts_b = __hip_atomic_load(&ctl->ts_beg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ts_e = __hip_atomic_load(&ctl->ts_end, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ts_pe = ctl->ts_prev_end;
+        if (tid < CTL_WORDS) ((uint32_t*)&C)[tid] = ld32_wt((const uint32_t*)ctl + tid);
         if (s_prehalt == H_NEED_EXACT || !a.fuse_pre) stage_tables();
         else if (egb >= 0 && egb < B) { s_ld[egb] = a.load[egb]; s_e[egb] = a.eb[egb]; s_fl[egb] = a.bfl[egb]; }
     } else {
@@ -1617,13 +1651,14 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
     KB_STAMP(ctl, 27);
     double hd0 = HUGE_VAL, hd1 = HUGE_VAL;
     unsigned long long hc0 = 0, hc1 = 0;
-    uint32_t hflg = 0, hfm = 0, hnk0 = 0, hnk1 = 0;
+    uint32_t hflg = 0, hfm = 0, hnk0 = 0, hnk1 = 0, hnks = 0;
     if (tid < a.R.n) {
         const RecHdr* h = a.R.h(tid);
-        hd0 = ldd(&h->dmin[0]); hd1 = ldd(&h->dmin[1]);
-        hc0 = ldobj(&h->cand[0]); hc1 = ldobj(&h->cand[1]);
-        hflg = ld32(&h->flags) & 1u; hfm = ld32(&h->fmask);
-        const uint32_t nkk = ld32(&h->nkk[0]);
+        hd0 = ldd_wt(&h->dmin[0]); hd1 = ldd_wt(&h->dmin[1]);
+        hc0 = ldobj_wt(&h->cand[0]); hc1 = ldobj_wt(&h->cand[1]);
+        hnks = ld32_wt(&h->nkeys);
+        hflg = ld32_wt(&h->flags) & 1u; hfm = ld32_wt(&h->fmask);
+        const uint32_t nkk = ld32_wt(&h->nkk[0]);
         hnk0 = nkk & 0xFFFFu; hnk1 = nkk >> 16;
     }
     KB_STAMP(ctl, 28);
@@ -1690,7 +1725,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
     // round trip so they are not held in registers through it
     Contender hb0, hb1;
     hb0.s = hb1.s = -1;
-    if (do_res && tid < a.R.n) { hb0 = ldobj(&a.R.h(tid)->best[0]); hb1 = ldobj(&a.R.h(tid)->best[1]); }
+    if (do_res && tid < a.R.n) { hb0 = ldobj_wt(&a.R.h(tid)->best[0]); hb1 = ldobj_wt(&a.R.h(tid)->best[1]); }
     KB_STAMP(ctl, 12);
     KB_STOP(1);
     // ---- the scan records (or the gathered rank summaries): one per thread, reduced
@@ -1710,7 +1745,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
             unsigned long long c0 = hc0, c1 = hc1;
             uint32_t flg = hflg, fm = hfm;
             for (int i = tid + STEP_THREADS; i < a.R.n; i += STEP_THREADS) {
-                const RecHdr h = ldobj(a.R.h(i));
+                const RecHdr h = ldobj_wt(a.R.h(i));
                 d0 = h.dmin[0] < d0 ? h.dmin[0] : d0;
                 d1 = h.dmin[1] < d1 ? h.dmin[1] : d1;
                 c0 += h.cand[0]; c1 += h.cand[1];
@@ -1753,10 +1788,10 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
 #pragma unroll
             for (int q = 0; q < NF; q++) f[q] = NONE32;
             for (int i = tid; i < a.R.n; i += STEP_THREADS) {
-                if (!ld32(&a.R.h(i)->fmask)) continue;
+                if (!ld32_wt(&a.R.h(i)->fmask)) continue;
                 const uint32_t* fi = a.R.f(i);
 #pragma unroll
-                for (int q = 0; q < NF; q++) f[q] = min(f[q], ld32(fi + q));
+                for (int q = 0; q < NF; q++) f[q] = min(f[q], ld32_wt(fi + q));
             }
 #pragma unroll
             for (int q = 0; q < NF; q++) {
@@ -1799,19 +1834,52 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
             s_li[tid] = -2;
         }
 
-        for (int i = tid; (need0 || need1) && i < a.R.n; i += STEP_THREADS) {
-            const RecHdr* h = a.R.h(i);
-            const bool q0 = need0 && ldd(&h->dmin[0]) <= g0 + 8.0 * eps;
-            const bool q1 = need1 && ldd(&h->dmin[1]) <= g1 + 8.0 * eps;
-            if (!q0 && !q1) continue;
-            const Contender* keys = a.R.k(i);
-            const int nk = (int)min(ld32(&h->nkeys), (uint32_t)a.R.cap);
-            for (int k = 0; k < nk; k++) {
-                const Contender c = ldobj(keys + k);
-                if (!(c.kind ? q1 : q0)) continue;
+        if ((need0 || need1) && a.R.n <= NW * 128) {
+            // one record per thread: its window tests and key count into LDS (the exact folds'
+            // rows, free until the resolve); then every key slot of every record, one per
+            // thread, so a record's keys are loaded in parallel instead of one dependent
+            // round trip per key (c2's all-tie records: 7.1 -> ~1 us)
+            uint32_t* s_rq = (uint32_t*)s_fold;
+            const int cap = a.R.cap;
+            for (int i = tid; i < a.R.n; i += STEP_THREADS) {
+                double d0 = hd0, d1 = hd1;              // (this thread's record: its registers)
+                uint32_t nks = hnks;
+                if (i != tid) {
+                    const RecHdr* h = a.R.h(i);
+                    d0 = ldd_wt(&h->dmin[0]); d1 = ldd_wt(&h->dmin[1]); nks = ld32_wt(&h->nkeys);
+                }
+                const bool q0 = need0 && d0 <= g0 + 8.0 * eps;
+                const bool q1 = need1 && d1 <= g1 + 8.0 * eps;
+                const uint32_t nk = (q0 || q1) ? min(nks, (uint32_t)cap) : 0u;
+                s_rq[i] = (nk << 2) | (q1 ? 2u : 0u) | (q0 ? 1u : 0u);
+            }
+            __syncthreads();
+            const int tot = a.R.n * cap;
+            for (int x = tid; x < tot; x += STEP_THREADS) {
+                const int i = x / cap, k = x - i * cap;
+                const uint32_t rq = s_rq[i];
+                if (k >= (int)(rq >> 2)) continue;
+                const Contender c = ldobj_wt(a.R.k(i) + k);
+                if (!((rq >> (c.kind ? 1 : 0)) & 1u)) continue;
                 if (cont_delta_ld(s_ld, c, inv_avg) <= (c.kind ? g1 : g0) + 4.0 * eps &&
                     dedup_insert(T, c.kind, c.s, c.t, c.w, c.iter) < 0)
                     s_kfail[c.kind] = 1;
+            }
+        } else {
+            for (int i = tid; (need0 || need1) && i < a.R.n; i += STEP_THREADS) {
+                const RecHdr* h = a.R.h(i);
+                const bool q0 = need0 && ldd_wt(&h->dmin[0]) <= g0 + 8.0 * eps;
+                const bool q1 = need1 && ldd_wt(&h->dmin[1]) <= g1 + 8.0 * eps;
+                if (!q0 && !q1) continue;
+                const Contender* keys = a.R.k(i);
+                const int nk = (int)min(ld32_wt(&h->nkeys), (uint32_t)a.R.cap);
+                for (int k = 0; k < nk; k++) {
+                    const Contender c = ldobj_wt(keys + k);
+                    if (!(c.kind ? q1 : q0)) continue;
+                    if (cont_delta_ld(s_ld, c, inv_avg) <= (c.kind ? g1 : g0) + 4.0 * eps &&
+                        dedup_insert(T, c.kind, c.s, c.t, c.w, c.iter) < 0)
+                        s_kfail[c.kind] = 1;
+                }
             }
         }
     }
@@ -1822,7 +1890,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
         // raw spills of the scan (rare): every thread
         const uint32_t n = min(C.ncont, a.cont_cap);
         for (uint32_t i = tid; i < n; i += STEP_THREADS) {
-            const Contender c = ldobj(a.cont + i);
+            const Contender c = ldobj_wt(a.cont + i);
             if (cont_delta_ld(s_ld, c, inv_avg) <= s_g[c.kind] + 4.0 * eps &&
                 dedup_insert(T, c.kind, c.s, c.t, c.w, c.iter) < 0)
                 s_kfail[c.kind] = 1;
@@ -2646,9 +2714,9 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
         const bool bkeys = do_res && tid < a.R.n;
         Contender bk0, bk1, bx0, bx1;
         bk0.s = bk1.s = bx0.s = bx1.s = -1;
-        if (bkeys) { bk0 = ldobj(&a.R.h(tid)->best[0]); bk1 = ldobj(&a.R.h(tid)->best[1]); }
+        if (bkeys) { bk0 = ldobj_wt(&a.R.h(tid)->best[0]); bk1 = ldobj_wt(&a.R.h(tid)->best[1]); }
         if (bkeys && !a.use_spill) {                  // rank summaries: the second-best keys too
-            bx0 = ldobj(a.R.k(tid) + (a.R.cap - 2)); bx1 = ldobj(a.R.k(tid) + (a.R.cap - 1));
+            bx0 = ldobj_wt(a.R.k(tid) + (a.R.cap - 2)); bx1 = ldobj_wt(a.R.k(tid) + (a.R.cap - 1));
         }
         if (tid < nT) { s_fl[s_T[tid]] |= BF_TOUCHED; s_cntT[tid] = 0; }
         if (tid == 0) { s_unc = 0; s_nsub = 0; }
@@ -3205,9 +3273,9 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
     const bool bkeys = do_res && !full && tid < a.R.n;
     Contender bk0, bk1, bx0, bx1;
     bk0.s = bk1.s = bx0.s = bx1.s = -1;
-    if (bkeys) { bk0 = ldobj(&a.R.h(tid)->best[0]); bk1 = ldobj(&a.R.h(tid)->best[1]); }
+    if (bkeys) { bk0 = ldobj_wt(&a.R.h(tid)->best[0]); bk1 = ldobj_wt(&a.R.h(tid)->best[1]); }
     if (bkeys && !a.use_spill) {                      // rank summaries: the second-best keys too
-        bx0 = ldobj(a.R.k(tid) + (a.R.cap - 2)); bx1 = ldobj(a.R.k(tid) + (a.R.cap - 1));
+        bx0 = ldobj_wt(a.R.k(tid) + (a.R.cap - 2)); bx1 = ldobj_wt(a.R.k(tid) + (a.R.cap - 1));
     }
     // approximate S (exact in integral mode: integers below 2^52), total load error E
     double sS = 0.0, sE = 0.0;
@@ -3823,7 +3891,15 @@ __device__ __attribute__((noinline)) void eager_refold(const RefreshArgs* rfp, i
 
 // pack this rank's scan result + its distinct near-tie keys (within 4*eps of the
 // rank's minimum, a superset of those within 4*eps of the global one)
-__global__ __launch_bounds__(1024) void k_summary(SumArgs a) {
+// One rank's summary of its scan records (multi-GPU): minima, candidate counts and
+// first-index words of the rank, its best key per kind (the records' best keys re-scored on
+// r) and a second-best key of another partition, and its near-tie keys within 4 eps of its
+// own minima.  One record per thread (R.n <= SUM_RECS; the host keeps a sharded engine's
+// scan grid within it), so every record field is loaded once; the near-tie keys are then
+// loaded one key slot per thread, all in flight at once.  Every record byte is read with sc1
+// loads (ldobj_wt): the scan workgroups store them write-through, so the fused form
+// (k_scansum: this body in the scan grid's last workgroup, after its wait) needs no acquire.
+__device__ __forceinline__ void summary_body(const SumArgs& a) {
     DevCtl* ctl = a.ctl;
     RecHdr* out = a.out.h(0);
     Contender* okeys = a.out.k(0);
@@ -3841,32 +3917,39 @@ __global__ __launch_bounds__(1024) void k_summary(SumArgs a) {
     __shared__ uint32_t s_f[NF];
     __shared__ uint32_t s_fm[16];
     __shared__ double s_g[2];
-    __shared__ unsigned long long s_benc[2];
-    __shared__ uint32_t s_brec[2];
+    __shared__ unsigned long long s_benc[2], s_benc2[2];
+    __shared__ uint32_t s_brec[2], s_brec2[2], s_nkk[2];
+    __shared__ long long s_bp[2];
+    __shared__ uint32_t s_rk[SUM_RECS];              // stored keys per record
     Dedup T{s_key, s_wb, s_it, DEDUP_STEP};
     dedup_clear(T);
-    if (tid == 0) { s_n = 0; s_fail = 0; }
+    if (tid == 0) { s_n = 0; s_fail = a.R.n > SUM_RECS ? 1u : 0u; }   // (the host's clamp; never)
     if (tid < NF) s_f[tid] = NONE32;
-    __shared__ unsigned long long s_benc2[2];
-    __shared__ uint32_t s_brec2[2];
-    if (tid < 2) { s_benc[tid] = NONE64; s_brec[tid] = NONE32; s_benc2[tid] = NONE64; s_brec2[tid] = NONE32; }
+    if (tid < 2) {
+        s_benc[tid] = NONE64; s_brec[tid] = NONE32; s_benc2[tid] = NONE64; s_brec2[tid] = NONE32;
+        s_nkk[tid] = 0; s_bp[tid] = -1;
+    }
     // the near-tie keys take the first cap - 2 slots; the last two carry, per kind, the best
     // key of another partition than the summary's best (k_step's census bound: the best key
     // is most often the applied move itself, whose partition's keys are dropped)
     const uint32_t capk = (uint32_t)a.out.cap - 2u;
-    const bool ran = ctl->halted == H_RUN && ctl->prepped;
     const double eps = ctl->eps, inv_avg = ctl->inv_avg;
+    const bool mine = tid < a.R.n;
     double d0 = HUGE_VAL, d1 = HUGE_VAL;
     unsigned long long c0 = 0, c1 = 0;
-    uint32_t fm = 0;
-    if (ran)
-        for (int i = tid; i < a.R.n; i += 1024) {
-            const RecHdr* h = a.R.h(i);
-            d0 = h->dmin[0] < d0 ? h->dmin[0] : d0;
-            d1 = h->dmin[1] < d1 ? h->dmin[1] : d1;
-            c0 += h->cand[0]; c1 += h->cand[1];
-            fm |= h->fmask;
-        }
+    uint32_t fm = 0, nks = 0;
+    Contender bk[2];
+    bk[0].s = bk[1].s = -1;
+    if (mine) {
+        const RecHdr* h = a.R.h(tid);
+        d0 = ldd_wt(&h->dmin[0]); d1 = ldd_wt(&h->dmin[1]);
+        c0 = ldobj_wt(&h->cand[0]); c1 = ldobj_wt(&h->cand[1]);
+        nks = min(ld32_wt(&h->nkeys), (uint32_t)a.R.cap);
+        fm = ld32_wt(&h->fmask);
+        bk[0] = ldobj_wt(&h->best[0]); bk[1] = ldobj_wt(&h->best[1]);
+    }
+    if (tid < SUM_RECS) s_rk[tid] = nks;
+    const uint32_t myfm = fm;
     d0 = wave_min(d0); d1 = wave_min(d1); c0 = wave_sum(c0); c1 = wave_sum(c1);
     fm = wave_red_or(fm);
     if (lane == 0) {
@@ -3874,13 +3957,11 @@ __global__ __launch_bounds__(1024) void k_summary(SumArgs a) {
         s_fm[wid] = fm;
     }
     __syncthreads();
-    fm = 0;
-    for (int x = 0; x < 16; x++) fm |= s_fm[x];
-    if (ran && fm) {
-        for (int i = tid; i < a.R.n; i += 1024) {
-            if (!a.R.h(i)->fmask) continue;
-            const uint32_t* fi = a.R.f(i);
-            for (int q = 0; q < NF; q++) if (fi[q] != NONE32) atomicMin(&s_f[q], fi[q]);
+    if (myfm) {
+        const uint32_t* fi = a.R.f(tid);
+        for (int q = 0; q < NF; q++) {
+            const uint32_t v = ld32_wt(fi + q);
+            if (v != NONE32) atomicMin(&s_f[q], v);
         }
     }
     if (tid == 0) {
@@ -3892,6 +3973,13 @@ __global__ __launch_bounds__(1024) void k_summary(SumArgs a) {
         s_g[0] = d0; s_g[1] = d1;
         out->dmin[0] = d0; out->dmin[1] = d1; out->cand[0] = c0; out->cand[1] = c1;
     }
+    // the rank's best key per kind: the records' best keys re-scored on r
+    unsigned long long me[2] = {NONE64, NONE64};
+    for (int k = 0; k < 2; k++)
+        if (bk[k].s >= 0) {
+            me[k] = enc(cont_delta(a.r, bk[k], inv_avg));
+            atomicMin(&s_benc[k], me[k]);
+        }
     __syncthreads();
     auto ins = [&](const Contender& c) {
         const double g = s_g[c.kind];
@@ -3899,59 +3987,32 @@ __global__ __launch_bounds__(1024) void k_summary(SumArgs a) {
         if (!(cont_delta(a.r, c, inv_avg) <= g + 4.0 * eps)) return;
         if (dedup_insert(T, c.kind, c.s, c.t, c.w, c.iter) < 0) s_fail = 1;
     };
-    // the rank's best key per kind: the records' best keys re-scored on r
-    unsigned long long myenc[2] = {NONE64, NONE64};
-    if (ran) {
-        for (int i = tid; i < a.R.n; i += 1024) {
-            const RecHdr* h = a.R.h(i);
-            for (int k = 0; k < 2; k++) {
-                const Contender c = h->best[k];
-                if (c.s < 0) continue;
-                const unsigned long long e = enc(cont_delta(a.r, c, inv_avg));
-                if (e < myenc[k]) myenc[k] = e;
-                atomicMin(&s_benc[k], e);
-            }
-            const Contender* keys = a.R.k(i);
-            for (uint32_t k = 0; k < h->nkeys; k++) ins(keys[k]);
-        }
-        const uint32_t nc = min(ctl->ncont, a.cont_cap);
-        for (uint32_t i = tid; i < nc; i += 1024) ins(a.cont[i]);
-    }
-    __syncthreads();
-    if (ran)
-        for (int i = tid; i < a.R.n; i += 1024)
-            for (int k = 0; k < 2; k++) {
-                const Contender c = a.R.h(i)->best[k];
-                if (c.s >= 0 && myenc[k] == s_benc[k] && enc(cont_delta(a.r, c, inv_avg)) == s_benc[k])
-                    atomicMin(&s_brec[k], (uint32_t)i);
-            }
-    __shared__ uint32_t s_nkk[2];
-    if (tid < 2) s_nkk[tid] = 0;
-    __syncthreads();
     {
-        // second-best keys: the best key per kind among the records whose best key lies in
-        // another partition than the summary's best
-        long long bp[2];
-        unsigned long long e2[2] = {NONE64, NONE64};
-        for (int k = 0; k < 2; k++)
-            bp[k] = s_brec[k] != NONE32 ? (long long)(a.R.h((int)s_brec[k])->best[k].iter >> 21) : -1;
-        for (int i = tid; i < a.R.n; i += 1024)
-            for (int k = 0; k < 2; k++) {
-                const Contender c = a.R.h(i)->best[k];
-                if (c.s < 0 || (long long)(c.iter >> 21) == bp[k]) continue;
-                const unsigned long long e = enc(cont_delta(a.r, c, inv_avg));
-                if (e < e2[k]) e2[k] = e;
-                atomicMin(&s_benc2[k], e);
-            }
-        __syncthreads();
-        for (int i = tid; i < a.R.n; i += 1024)
-            for (int k = 0; k < 2; k++) {
-                const Contender c = a.R.h(i)->best[k];
-                if (c.s >= 0 && (long long)(c.iter >> 21) != bp[k] && e2[k] == s_benc2[k] &&
-                    enc(cont_delta(a.r, c, inv_avg)) == s_benc2[k])
-                    atomicMin(&s_brec2[k], (uint32_t)i);
-            }
+        const int kc = a.R.cap, tot = a.R.n * kc;
+        for (int x = tid; x < tot; x += 1024) {
+            const int i = x / kc, k = x - i * kc;
+            if (k < (int)s_rk[i]) ins(ldobj_wt(a.R.k(i) + k));
+        }
+        const uint32_t nc = min(__hip_atomic_load(&ctl->ncont, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), a.cont_cap);
+        for (uint32_t i = tid; i < nc; i += 1024) ins(ldobj_wt(a.cont + i));
     }
+    for (int k = 0; k < 2; k++)
+        if (me[k] != NONE64 && me[k] == s_benc[k]) atomicMin(&s_brec[k], (uint32_t)tid);
+    __syncthreads();
+    // second-best keys: the best key per kind among the records whose best key lies in
+    // another partition than the summary's best
+    for (int k = 0; k < 2; k++)
+        if ((uint32_t)tid == s_brec[k]) s_bp[k] = (long long)(bk[k].iter >> 21);
+    __syncthreads();
+    unsigned long long e2[2] = {NONE64, NONE64};
+    for (int k = 0; k < 2; k++)
+        if (me[k] != NONE64 && (long long)(bk[k].iter >> 21) != s_bp[k]) {
+            e2[k] = me[k];
+            atomicMin(&s_benc2[k], e2[k]);
+        }
+    __syncthreads();
+    for (int k = 0; k < 2; k++)
+        if (e2[k] != NONE64 && e2[k] == s_benc2[k]) atomicMin(&s_brec2[k], (uint32_t)tid);
     for (int h = tid; h < DEDUP_STEP; h += 1024) {
         if (s_key[h] == NONE32) continue;
         const uint32_t k = atomicAdd(&s_n, 1u);
@@ -3959,17 +4020,23 @@ __global__ __launch_bounds__(1024) void k_summary(SumArgs a) {
         if (k < capk) okeys[k] = dedup_entry(T, h);
     }
     __syncthreads();
+    for (int k = 0; k < 2; k++) {
+        // (the record that holds the best / second-best key writes it from its registers)
+        if ((uint32_t)tid == s_brec[k]) out->best[k] = bk[k];
+        if ((uint32_t)tid == s_brec2[k]) okeys[capk + k] = bk[k];
+    }
     if (tid < 2) {
         Contender x;
-        if (s_brec2[tid] != NONE32) x = a.R.h((int)s_brec2[tid])->best[tid];
-        else { x.s = x.t = -1; x.w = 0.0; x.iter = NONE64; x.kind = tid; x.pad = 0; }
-        okeys[capk + tid] = x;
+        x.s = x.t = -1; x.w = 0.0; x.iter = NONE64; x.kind = tid; x.pad = 0;
+        if (s_brec[tid] == NONE32) out->best[tid] = x;
+        if (s_brec2[tid] == NONE32) okeys[capk + tid] = x;
     }
     if (tid == 0) {
+        const uint32_t ovf = __hip_atomic_load(&ctl->cont_overflow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         out->nkeys = s_n < capk ? s_n : capk;
-        out->flags = ((ran && ctl->cont_overflow) || s_fail || s_n > capk) ? 1u : 0u;
-        if (ran) out->flags |= 2u;
-        if (ran && ctl->cont_overflow && a.spill_growable) out->flags |= 4u;   // (grow_summary)
+        out->flags = (ovf || s_fail || s_n > capk) ? 1u : 0u;
+        out->flags |= 2u;
+        if (ovf && a.spill_growable) out->flags |= 4u;   // (grow_summary)
         out->nkk[0] = (uint16_t)min(s_nkk[0], 0xFFFFu);
         out->nkk[1] = (uint16_t)min(s_nkk[1], 0xFFFFu);
         uint32_t m = 0;
@@ -3977,10 +4044,64 @@ __global__ __launch_bounds__(1024) void k_summary(SumArgs a) {
         out->fmask = m;
         uint32_t* fo = a.out.f(0);
         for (int q = 0; q < NF; q++) fo[q] = s_f[q];
-        for (int k = 0; k < 2; k++) {
-            if (s_brec[k] != NONE32) out->best[k] = a.R.h((int)s_brec[k])->best[k];
-            else { out->best[k].s = out->best[k].t = -1; out->best[k].w = 0.0; out->best[k].iter = NONE64; out->best[k].kind = k; out->best[k].pad = 0; }
+    }
+}
+
+__global__ __launch_bounds__(1024) void k_summary(SumArgs a) { summary_body(a); }
+
+// The scan and the rank summary in one launch (sharded engines): the scan's grid plus one
+// resident summary workgroup, the last of the grid, which waits for the others' arrivals
+// (k_pair's sharded count, bounded wait) and then runs summary_body.  The all-gather and
+// the resolve follow as before; this removes the summary's launch and dispatch gap.
+template <int RC, bool LSETS, bool BK>
+__global__ __launch_bounds__(SCAN_THREADS) void k_scansum(ScanArgs a, SumArgs sa) {
+    static_assert(SCAN_THREADS == 1024, "summary_body runs 1024 threads");
+    if ((int)blockIdx.x == (int)gridDim.x - 1) {
+        const int tid = threadIdx.x, lane = tid & 63;
+        __shared__ int s_to;
+        if (tid < 64) {
+            const unsigned long long t0 = wall_clock64();
+            int to = 0;
+            for (;;) {
+                if (wall_clock64() - t0 >= sa.wait_ticks) { to = 1; break; }
+                const uint32_t v = lane < PAIR_SHARDS
+                    ? __hip_atomic_load(sa.wait_cnt + lane * PAIR_STRIDE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+                if (wave_sum(v) >= (uint32_t)sa.wait_n) break;
+                __builtin_amdgcn_s_sleep(1);
+            }
+            if (!to && lane < PAIR_SHARDS)
+                __hip_atomic_store(sa.wait_cnt + lane * PAIR_STRIDE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (lane == 0) s_to = to;
         }
+        __syncthreads();
+        if (s_to) {
+            // (as k_pair's step workgroup: an explicit error in the step log, the plan halts;
+            // the host resets the count and refuses further work)
+            if (tid == 0) {
+                DevCtl* ctl = sa.ctl;
+                ChangeDev ch;
+                ch.status = -1; ch.step = -1; ch.kind = 0; ch.slot = -1; ch.part = -1; ch.from = ch.to = -1;
+                ch.su = ch.cu = 0.0; ch.exact = 0; ch.err_code = E_PAIR_TIMEOUT; ch.err_broker = -1; ch.pad = 0;
+                const int lp = ctl->logpos;
+                if (lp < ctl->logcap) sa.log[lp] = ch;
+                ctl->logpos = lp + 1;
+                ctl->halted = H_DONE;
+            }
+            return;
+        }
+        summary_body(sa);
+        return;
+    }
+    const bool wt = (int)blockIdx.x < a.nscan && !(a.rfpass && a.ctl->halted == H_NEED_EXACT);
+    scan_kernel_body<RC, LSETS, false, false, BK>(a);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        if (!wt) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __hip_atomic_fetch_add(a.done + (blockIdx.x % PAIR_SHARDS) * PAIR_STRIDE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
@@ -4164,6 +4285,43 @@ void launch_refresh(const RefreshArgs& a, hipStream_t st) {
 }
 void launch_summary(const SumArgs& a, hipStream_t st) {
     hipLaunchKernelGGL(k_summary, dim3(1), dim3(1024), 0, st, a);
+}
+
+template <int RC, bool LSETS, bool BK>
+static int scansum_attr1(size_t lds, int* static_lds) {
+    hipFuncAttributes fa;
+    if (hipFuncGetAttributes(&fa, (const void*)k_scansum<RC, LSETS, BK>) != hipSuccess) return -1;
+    *static_lds = (int)fa.sharedSizeBytes;
+    int n = 0;
+    hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_scansum<RC, LSETS, BK>, SCAN_THREADS, lds);
+    return n;
+}
+template <int RC, bool LSETS>
+static int scansum_attr(size_t lds, int* static_lds) {
+    int s0 = 0, s1 = 0;
+    const int n0 = scansum_attr1<RC, LSETS, false>(lds, &s0), n1 = scansum_attr1<RC, LSETS, true>(lds, &s1);
+    *static_lds = s0 > s1 ? s0 : s1;
+    return n0 < n1 ? n0 : n1;
+}
+int scansum_blocks_per_cu(int rc, bool lds_sets, size_t lds, int* static_lds) {
+    if (rc == 3) return lds_sets ? scansum_attr<3, true>(lds, static_lds) : scansum_attr<3, false>(lds, static_lds);
+    if (rc == 4) return lds_sets ? scansum_attr<4, true>(lds, static_lds) : scansum_attr<4, false>(lds, static_lds);
+    return -1;
+}
+void launch_scansum(const ScanArgs& a, const SumArgs& sa, int rc, bool lds_sets, size_t lds, hipStream_t st) {
+    const int grid = a.nscan + (a.listwg ? 1 : 0) + a.eager + 1;
+    const bool bk = !a.allow_leader;
+#define KB_SCANSUM_LAUNCH(R, L)                                                                          \
+    do {                                                                                                 \
+        if (bk) hipLaunchKernelGGL((k_scansum<R, L, true>), dim3(grid), dim3(SCAN_THREADS), lds, st, a, sa);  \
+        else hipLaunchKernelGGL((k_scansum<R, L, false>), dim3(grid), dim3(SCAN_THREADS), lds, st, a, sa);    \
+    } while (0)
+    if (rc == 3) {
+        if (lds_sets) KB_SCANSUM_LAUNCH(3, true); else KB_SCANSUM_LAUNCH(3, false);
+    } else {
+        if (lds_sets) KB_SCANSUM_LAUNCH(4, true); else KB_SCANSUM_LAUNCH(4, false);
+    }
+#undef KB_SCANSUM_LAUNCH
 }
 
 // Control-block / step-log transfers between the device and the host's pinned

@@ -121,6 +121,8 @@ struct StepArgs {
     int wait_n;               //    grid's other workgroups), then resets it
     int fuse_pre;             // k_pair: stage the broker tables before the wait (diagnostic 0: after)
     unsigned long long wait_ticks;   // k_pair: the wait's bound (100 MHz ticks; 2 s, tests: 0)
+    int pair_acq;             // k_pair: agent acquire after the wait even when every handed-off
+                              //    byte was stored write-through (A/B; 0 = sc1 loads only)
 };
 
 
@@ -132,6 +134,12 @@ struct SumArgs {
     const double* r;
     Recs out;                 // one summary (summary_recs layout)
     int spill_growable;       // 1: this rank's spill buffer can still grow (summary flag bit 2)
+    // k_scansum (the summary workgroup in the scan's grid): the arrival count it waits on
+    // (wait_n workgroups, bounded by wait_ticks), and the step log for a timeout's error
+    uint32_t* wait_cnt;
+    int wait_n;
+    unsigned long long wait_ticks;
+    ChangeDev* log;
 };
 
 void launch_scan(const ScanArgs& a, int rc, bool lds_sets, size_t lds_bytes, hipStream_t st);
@@ -147,6 +155,8 @@ void launch_touch(double* r, int B, int32_t* blm, int32_t* posm, uint4* setrec, 
 void launch_listop(DevCtl* ctl, const Lists& L, hipStream_t st);
 void launch_refresh(const RefreshArgs& a, hipStream_t st);
 void launch_summary(const SumArgs& a, hipStream_t st);
+int scansum_blocks_per_cu(int rc, bool lds_sets, size_t lds_bytes, int* static_lds);
+void launch_scansum(const ScanArgs& a, const SumArgs& sa, int rc, bool lds_sets, size_t lds_bytes, hipStream_t st);
 
 // k_xfer: up to two 32-bit word copies (device <-> the host's mapped pinned mirror), then,
 // if flag is set, a system-scope release and *flag = seq (the host waits on it)

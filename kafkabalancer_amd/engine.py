@@ -65,7 +65,7 @@ class kb_stats(C.Structure):
                 ("max_replicas", C.c_int32), ("refreshes", C.c_int64), ("exact_halts", C.c_int64),
                 ("scan_workgroups", C.c_int64), ("retries", C.c_int64), ("spill_grows", C.c_int64),
                 ("blocks_scanned", C.c_int64), ("relists", C.c_int64),
-                ("fused_pairs", C.c_int64)]
+                ("fused_pairs", C.c_int64), ("fused_summaries", C.c_int64)]
 
 
 _lib = None
@@ -147,7 +147,7 @@ def lib():
         if hasattr(L, "kb_engine_set_incremental"):
             L.kb_engine_set_incremental.argtypes = [vp, C.c_int32]
             L.kb_engine_set_incremental.restype = C.c_int
-        if L.kb_abi_version() != 9 and not any_abi:
+        if L.kb_abi_version() != 10 and not any_abi:
             raise ImportError("libkbengine.so ABI mismatch")
         _lib = L
     return _lib

@@ -115,3 +115,71 @@ def test_control_transfer_modes_match(mode):
         assert keyed([eng.balance()]) == keyed([ref.balance()])
     eng.close()
     ref.close()
+
+
+def _sharded_world1(cl, cfg, steps, env):
+    """The batched sharded protocol at world size 1 (the summary is its own gathered
+    buffer), with the given environment at engine creation; (changes, error, stats, loads)."""
+    import torch
+    eng = _with_env(*env, lambda: E.Engine(cl, cfg, shard=(0, cl.n)))
+    got, err = [], None
+    try:
+        done = False
+        while not done and len(got) < steps:
+            nb = eng.summary_bytes()
+            summ = torch.zeros(nb, dtype=torch.uint8, device="cuda")
+            torch.cuda.synchronize()
+            batch = min(16, steps - len(got))
+            eng.sharded_reset(batch)
+            for _ in range(batch):
+                eng.sharded_scan(summ.data_ptr())
+                eng.sharded_resolve(summ.data_ptr(), 1)
+            st, ch = eng.sharded_collect(batch + 1)
+            got.extend(ch)
+            done = st == "done"
+    except E.EngineError as ex:
+        err = ex
+    st = eng.stats()
+    loads = eng.loads() if err is None else None
+    eng.close()
+    return got, err, st, loads
+
+
+@pytest.mark.parametrize("allow_leader", [True, False])
+def test_fused_summary_matches_two_launches(allow_leader):
+    """k_scansum (the rank summary in the scan's grid) against k_scan + k_summary: the same
+    sharded plan and final loads, with and without -allow-leader (the BK instantiation)."""
+    cl, cfg, _ = synth.config("c3", scale=0.25)
+    cfg = dict(cfg, allow_leader=allow_leader)
+    a = _sharded_world1(cl, cfg, 60, ("KB_FUSE_SUM", "1"))
+    b = _sharded_world1(cl, cfg, 60, ("KB_FUSE_SUM", "0"))
+    assert a[2]["fused_summaries"] == 1 and b[2]["fused_summaries"] == 0
+    assert a[1] is None and b[1] is None
+    assert len(a[0]) == 60
+    assert keyed(a[0]) == keyed(b[0])
+    assert a[3] == b[3]
+
+
+def test_summary_timeout_poisons_engine():
+    """k_scansum's summary workgroup gives up waiting for its grid (a zero wait bound): the
+    batch ends with the explicit error, the arrival count is reset, and the engine refuses
+    further sharded work."""
+    import torch
+    cl, cfg, _ = synth.config("c3", scale=0.25)
+    eng = _with_env("KB_PAIR_WAIT_TICKS", "0", lambda: E.Engine(cl, cfg, shard=(0, cl.n)))
+    assert eng.stats()["fused_summaries"] == 1
+    summ = torch.zeros(eng.summary_bytes(), dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    eng.sharded_reset(4)
+    for _ in range(4):
+        eng.sharded_scan(summ.data_ptr())
+        eng.sharded_resolve(summ.data_ptr(), 1)
+    with pytest.raises(E.EngineError) as ei:
+        eng.sharded_collect(5)
+    assert "timed out" in str(ei.value)
+    with pytest.raises(E.EngineError) as ei:
+        eng.sharded_reset(1)
+    assert "unusable" in str(ei.value)
+    eng.close()
+    got, err, st, _ = _sharded_world1(cl, cfg, 10, ("KB_FUSE_SUM", "1"))
+    assert err is None and len(got) == 10 and st["fused_summaries"] == 1

@@ -24,7 +24,7 @@ def main():
         for ln in open(pr):
             x = json.loads(ln)
             print("probe", x["k"], x["pidx"], "d=%.3e ub0=%.3e ub1=%.3e" % (x["d"], x["ub0"], x["ub1"]), x.get("rec"))
-    for wl in ("c2", "c3", "c3nl", "c5"):
+    for wl in ("c2", "c3", "c3_acq", "c3b", "c3nl", "c5"):
         x = last_json(os.path.join(d, wl + ".json"))
         if not x:
             continue
@@ -32,9 +32,15 @@ def main():
         print(wl, "ms/step %.4f dev %.4f launch %.1f us frac %.3f scan %.1f" % (
             x["ms_per_step"], x["config"]["device_ms_per_step"], r["avg_launch_us"], r["frac"], r.get("scan_phase_us") or 0),
             {k: round(v, 1) for k, v in x["kernels_us_per_launch"].items()}, x["engine_events"])
-    x = last_json(os.path.join(d, "sharded.json"))
-    if x:
-        print("sharded", {k: x[k] for k in ("ms_per_step_sharded", "ms_per_step_plain", "ratio", "plans_equal")})
+    for wl in ("c2", "c3"):
+        x = last_json(os.path.join(d, wl + "_stamps.json"))
+        if x:
+            st = {k: round(v, 2) for k, v in x["stamps_us_per_step"].items() if v >= 0.3}
+            print(wl, "stamps k_step %.1f us" % x["k_step_us"], st)
+    for f in ("sharded", "sharded_nofuse"):
+        x = last_json(os.path.join(d, f + ".json"))
+        if x:
+            print(f, {k: x[k] for k in ("ms_per_step_sharded", "ms_per_step_plain", "ratio", "plans_equal")})
 
 
 if __name__ == "__main__":
