@@ -149,6 +149,9 @@ typedef struct {
     int64_t fused_pairs;            /* 1: a plan's scan + step run as one launch (k_pair, ABI 8) */
     int64_t fused_summaries;        /* 1: a sharded scan and its rank summary run as one launch
                                        (k_scansum, ABI 10) */
+    int64_t eager;                  /* 1: touched brokers are refolded beside the next scan
+                                       (eager refolds; ABI 10) */
+    int64_t eager_switches;         /* plans switched from lazy loads to eager refolds (ABI 10) */
 } kb_stats;
 
 typedef struct kb_engine kb_engine;

@@ -98,6 +98,11 @@ struct kb_engine {
     uint32_t* pair_cnt = nullptr;     // k_pair's arrival count (ScanArgs.done / StepArgs.wait_cnt)
     bool fuse = false;                // pairs run as one k_pair launch (scan grid + step workgroup)
     bool fuse_sum = false;            // sharded scans: scan + rank summary as one k_scansum launch
+    // resident workgroup slots of the scan / k_pair / k_scansum grids (blocks per CU x CUs),
+    // kept for the switch to eager refolds, whose extra workgroups must fit beside them
+    int64_t slots_scan = 0, slots_pair = 0, slots_sum = 0;
+    bool eager_auto = false;          // lazy loads now; eager refolds once exact halts are frequent
+    int64_t eager_switches = 0;
     int fuse_pre = 1;                 // k_pair stages the tables before its wait (KB_FUSE_PRE=0: after)
     size_t pair_lds = 0;              // k_pair's dynamic LDS: max(scan, step)
     bool gb = false;                  // B > MAXB: broker tables in memory (k_scan GT, k_step GB)
@@ -170,7 +175,6 @@ struct kb_engine {
     unsigned char* gath_buf = nullptr;
     int64_t xbuf_bytes = 0;            // summary bytes the buffers were sized for
     unsigned long long pair_wait_ticks = 200000000ull;   // k_pair's wait bound: 2 s of the 100 MHz clock
-    int pair_acq = 0;                                     // k_pair: acquire after the wait always (A/B)
     std::string last_err;
 };
 
@@ -619,7 +623,12 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
     // folds often, and each then waited for a refresh of the approximate loads): EGW extra
     // workgroups per scan launch, kept co-resident with the scan's (and its list workgroup)
     e->eager = e->rf_stream && e->B >= 2048;
-    if (const char* v = getenv("KB_EAGER")) e->eager = e->rf_stream && *v == '1';          // diagnostic
+    // (fewer brokers: lazy loads, refreshed when a decision needs them exact; a plan whose
+    // decisions keep needing them switches to eager refolds, switch_to_eager)
+    e->eager_auto = e->rf_stream && !e->eager && !e->gb;
+    if (const char* v = getenv("KB_EAGER")) { e->eager = e->rf_stream && *v == '1'; e->eager_auto = false; }  // diagnostic
+    if (const char* v = getenv("KB_EAGER_AUTO")) e->eager_auto = e->eager_auto && *v != '0';               // A/B
+    e->slots_scan = (int64_t)per_cu * ncu;
     e->nscan = std::min<int64_t>(e->ntiles, std::max<int64_t>(1, (int64_t)per_cu * ncu - (e->eager ? EGW + 1 : 0)));
     if (const char* v = getenv("KB_NSCAN")) if (atoi(v) > 0) e->nscan = std::min<int64_t>(e->ntiles, atoi(v));  // diagnostic
     e->nscan = std::min<int64_t>(e->nscan, SUM_RECS);     // (a rank summary reads one record per thread)
@@ -648,11 +657,11 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
         if (const char* v = getenv("KB_FUSE")) e->fuse = e->fuse && *v != '0';                      // A/B
         if (const char* v = getenv("KB_FUSE_PRE")) e->fuse_pre = *v != '0';                          // diagnostic
         if (const char* v = getenv("KB_PAIR_WAIT_TICKS")) e->pair_wait_ticks = strtoull(v, nullptr, 10);   // tests
-        if (const char* v = getenv("KB_PAIR_ACQ")) e->pair_acq = *v == '1';                          // A/B
         if (e->fuse) {
             e->pair_lds = std::max(e->scan_lds, (size_t)e->step_lds_bytes);
             int pst = 0;
             const int pcu = pair_blocks_per_cu(e->rc_dev, e->lds_sets, e->pair_lds, &pst);
+            e->slots_pair = (int64_t)pcu * ncu;
             if (pcu < 1 || pst + e->pair_lds > 160 * 1024) e->fuse = false;
             // (every workgroup of the grid resident at once: the scan's, the list workgroup, the
             // eager ones and the step workgroup)
@@ -667,8 +676,11 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
         if (e->fuse_sum) {
             int sst = 0;
             const int scu = scansum_blocks_per_cu(e->rc_dev, e->lds_sets, e->scan_lds, &sst);
+            e->slots_sum = (int64_t)scu * ncu;
             const int64_t cap = (int64_t)scu * ncu - (e->eager ? EGW + 1 : (e->integral ? 0 : 1)) - 1;
-            if (scu < 1 || sst + e->scan_lds > 160 * 1024 || cap < 1 || (e->fuse && cap < e->nscan)) e->fuse_sum = false;
+            // (the summary workgroup stages r in the scan's dynamic LDS)
+            if (scu < 1 || sst + e->scan_lds > 160 * 1024 || cap < 1 || (e->fuse && cap < e->nscan) ||
+                e->scan_lds < (size_t)e->B * 8) e->fuse_sum = false;
             else e->nscan = std::min<int64_t>(e->nscan, cap);
         }
     }
@@ -850,7 +862,7 @@ static void fill_step_args(kb_engine* e, StepArgs& a, const Recs& R, int use_spi
     a.nsets = (int)e->nsets; a.NP2 = e->NP2;
     a.sb_lds = e->sb_lds; a.lds_bytes = e->step_lds_bytes;
     a.gscr = e->gscr;
-    a.wait_cnt = e->pair_cnt; a.wait_n = 0; a.fuse_pre = 1; a.wait_ticks = e->pair_wait_ticks; a.pair_acq = e->pair_acq;
+    a.wait_cnt = e->pair_cnt; a.wait_n = 0; a.fuse_pre = 1; a.wait_ticks = e->pair_wait_ticks;
     a.setbits = e->setbits; a.setrec = e->setrec;
     a.order = e->order; a.posu = e->posu; a.blm = e->blm; a.posm = e->posm; a.r = e->r;
     a.load = e->load; a.lerr = e->lerr; a.eb = e->eb; a.bfl = e->bfl; a.cnt = e->cnt;
@@ -1200,6 +1212,28 @@ static int grow_spill(kb_engine* e) {
 
 // run up to max_steps Balance() calls device-resident; returns the number of
 // log entries written (changes + the terminating no-change / error)
+// Lazy loads (fewer than 2048 brokers) cost a halt, a refresh and a re-run whenever a
+// decision needs exact folds, and the approximate loads' error widens eps and with it the
+// census; on a balanced cluster without -allow-leader that is a quarter of the steps (c3nl
+// past its 300th step: 0.118 ms/step lazy, 0.051 eager).  Once the halts reach one per 16
+// steps the plan switches to eager refolds (the next launches refold the touched brokers
+// beside the scan): the grids shrink by the eager workgroups so every workgroup of a fused
+// launch stays resident.  Switched between batches, where no list edit is in flight but the
+// last step's (which the next launch's list workgroup applies, the eager workgroups having
+// no brokers yet).  The decisions do not depend on the mode.
+static void maybe_switch_to_eager(kb_engine* e, const DevCtl& c) {
+    if (!e->eager_auto || e->eager) return;
+    if (c.total_exact_halts < 4 || 16 * c.total_exact_halts < (unsigned long long)std::max(c.steps, 1)) return;
+    const int64_t lw = EGW + 1;                       // the eager workgroups and the list workgroup
+    int64_t n = std::min<int64_t>(e->nscan, std::max<int64_t>(1, e->slots_scan - lw));
+    if (e->fuse) n = std::min<int64_t>(n, std::max<int64_t>(1, e->slots_pair - lw - 1));
+    if (e->fuse_sum) n = std::min<int64_t>(n, std::max<int64_t>(1, e->slots_sum - lw - 1));
+    e->nscan = n;
+    e->eager = true;
+    e->recs_fresh = false;
+    e->eager_switches++;
+}
+
 static int run_steps(kb_engine* e, int64_t max_steps) {
     if (ensure_log(e, max_steps) != KB_OK) return KB_ERR_HIP;
     if (e->h_logcap < e->logcap) {
@@ -1313,10 +1347,12 @@ static int run_steps(kb_engine* e, int64_t max_steps) {
         if (c.halted == H_NEED_EXACT || (c.want_refresh && c.steps - steps0 < max_steps)) {
             if (const int rc = refresh(e); rc != KB_OK) return rc;
             // refresh() cleared halted; the step log position is kept
+            maybe_switch_to_eager(e, c);
             prepped = false;
             fresh = false;
             continue;
         }
+        maybe_switch_to_eager(e, c);
         prepped = c.prepped != 0;
     }
     float ms = 0;
@@ -1492,6 +1528,8 @@ extern "C" int kb_engine_stats(kb_engine* e, kb_stats* o) {
     o->relists = e->relists;
     o->fused_pairs = e->fuse && !e->incr ? 1 : 0;
     o->fused_summaries = e->fuse_sum ? 1 : 0;
+    o->eager = e->eager ? 1 : 0;
+    o->eager_switches = e->eager_switches;
     return KB_OK;
 }
 
@@ -1815,7 +1853,7 @@ extern "C" int kb_engine_set_stream(kb_engine* e, void* s) {
 static int enqueue_scan_summary(kb_engine* e, void* summary_dev) {
     SumArgs s;
     s.ctl = e->ctl; s.R = scan_recs(e->recs, (int)e->nscan); s.cont = e->cont; s.cont_cap = e->cont_cap;
-    s.r = e->r; s.out = summary_recs((unsigned char*)summary_dev, 1, e->sum_keys);
+    s.r = e->r; s.B = (int)e->B; s.out = summary_recs((unsigned char*)summary_dev, 1, e->sum_keys);
     s.spill_growable = e->cont_cap < kContMax ? 1 : 0;
     s.wait_cnt = e->pair_cnt; s.wait_n = 0; s.wait_ticks = e->pair_wait_ticks; s.log = e->log;
     if (e->fuse_sum) {

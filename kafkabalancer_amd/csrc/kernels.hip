@@ -75,29 +75,6 @@ __device__ __forceinline__ void st32_wt(uint32_t* p, uint32_t v) {
     // (global address space: a global_store sc1 even where the pointer is generic)
     __hip_atomic_store((__attribute__((address_space(1))) uint32_t*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-// ... and the matching sc1 loads (L2-served: never a stale L1 line).  k_pair's step workgroup
-// reads everything the scan workgroups of its own launch stored write-through with these,
-// so after its poll it needs no agent acquire (MI355X_MICROARCH.md, valid forms: the
-// first row -- one lane's atomic add per workgroup after every wave's drain, an sc1 poll
-// of every shard, a barrier, then only sc1 loads of those bytes)
-template <typename T>
-__device__ __forceinline__ T ldobj_wt(const T* p) {
-    static_assert(sizeof(T) % 8 == 0, "8-byte granules");
-    T v;
-    unsigned long long* dst = (unsigned long long*)&v;
-    unsigned long long* src = (unsigned long long*)p;
-#pragma unroll
-    for (int i = 0; i < (int)(sizeof(T) / 8); i++)
-        dst[i] = __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return v;
-}
-__device__ __forceinline__ uint32_t ld32_wt(const void* p) {
-    return __hip_atomic_load((uint32_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ double ldd_wt(const double* p) {
-    return __hip_atomic_load((double*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
 // reference term (utils.go:136-143): r = L/avg - 1; r>0 ? r*r : r*r/2 (exact ops)
 __device__ __forceinline__ double term_x(double L, double avg) {
     double r = L / avg - 1.0;
@@ -592,9 +569,8 @@ __device__ void do_list_op(DevCtl* ctl, Lists L, int* s_i) {
     else if (kind == 3) ok = list_insert(L, to, p, s_i);
     __syncthreads();
     if (threadIdx.x == 0) {
-        // (write-through: k_pair's step workgroup reads them with sc1 loads, no acquire)
-        if (!ok) st32_wt((uint32_t*)&ctl->list_overflow, 1u);
-        st32_wt((uint32_t*)&ctl->pending_list, 0u);
+        if (!ok) ctl->list_overflow = 1;
+        ctl->pending_list = 0;
     }
     __syncthreads();
 }
@@ -1411,11 +1387,11 @@ __device__ __forceinline__ void for_each_contender(const StepArgs& a, const doub
     const int nt = blockDim.x;
     for (int i = threadIdx.x; i < a.R.n; i += nt) {
         const RecHdr* h = a.R.h(i);
-        if (!(ldd_wt(&h->dmin[kind]) <= g + 8.0 * eps)) continue;
+        if (!(ldd(&h->dmin[kind]) <= g + 8.0 * eps)) continue;
         const Contender* keys = a.R.k(i);
-        const int nk = (int)min(ld32_wt(&h->nkeys), (uint32_t)a.R.cap);
+        const int nk = (int)min(ld32(&h->nkeys), (uint32_t)a.R.cap);
         for (int k = 0; k < nk; k++) {
-            const Contender c = ldobj_wt(keys + k);
+            const Contender c = ldobj(keys + k);
             if (c.kind != kind) continue;
             if (cont_delta_ld(s_ld, c, inv_avg) <= g + 4.0 * eps) f(c);
         }
@@ -1423,7 +1399,7 @@ __device__ __forceinline__ void for_each_contender(const StepArgs& a, const doub
     if (a.use_spill) {
         const uint32_t n = min(ncont, a.cont_cap);
         for (uint32_t i = threadIdx.x; i < n; i += nt) {
-            const Contender c = ldobj_wt(a.cont + i);
+            const Contender c = ldobj(a.cont + i);
             if (c.kind != kind) continue;
             if (cont_delta_ld(s_ld, c, inv_avg) <= g + 4.0 * eps) f(c);
         }
@@ -1583,8 +1559,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
         }
         __shared__ int s_wait_to;
         if (wid == 0) {
-            const int ph = ctl->halted;
-            if (lane == 0) s_prehalt = ph;
+            if (lane == 0) s_prehalt = ctl->halted;
             // the arrival count is sharded over PAIR_SHARDS words (a workgroup adds to the
             // shard of blockIdx % 8, the blocks that share an XCD: 32 arrivals per word instead
             // of 255 serialised on one); lanes 0..7 poll one shard each.  (A bounded wait: 2 s
@@ -1601,15 +1576,11 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
                 if (wave_sum(v) >= (uint32_t)a.wait_n) break;
                 __builtin_amdgcn_s_sleep(1);
             }
-            // the scanning workgroups and the list workgroup stored what this workgroup reads
-            // write-through and it reads them with sc1 loads (ldobj_wt, the control block
-            // below): no acquire.  The eager workgroups and an in-stream refresh write plain
-            // (loads, lists) and publish with a release: then the acquire, as every staged
-            // table they touch is read again with plain loads
-            if (a.pair_acq || ph == H_NEED_EXACT || (KB_EAGER_CODE && a.eager && ctl->eg_n > 0)) {
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // (the other XCDs' writes)
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            }
+            // (tried: every handed-off byte read with sc1 loads instead of this acquire, the
+            // producers' stores being write-through already -- c3 2 us per step slower, the
+            // record and key loads as 8-byte atomic loads)
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // (the other XCDs' writes)
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             if (!to && lane < PAIR_SHARDS)
                 __hip_atomic_store(a.wait_cnt + lane * PAIR_STRIDE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (lane == 0) s_wait_to = to;
@@ -1628,10 +1599,8 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
             return;
         }
         t_in = wall_clock64();
-        ts_b = __hip_atomic_load(&ctl->ts_beg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        ts_e = __hip_atomic_load(&ctl->ts_end, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        ts_pe = ctl->ts_prev_end;
-        if (tid < CTL_WORDS) ((uint32_t*)&C)[tid] = ld32_wt((const uint32_t*)ctl + tid);
+        ts_b = ctl->ts_beg; ts_e = ctl->ts_end; ts_pe = ctl->ts_prev_end;
+        if (tid < CTL_WORDS) ((uint32_t*)&C)[tid] = ((const uint32_t*)ctl)[tid];
         if (s_prehalt == H_NEED_EXACT || !a.fuse_pre) stage_tables();
         else if (egb >= 0 && egb < B) { s_ld[egb] = a.load[egb]; s_e[egb] = a.eb[egb]; s_fl[egb] = a.bfl[egb]; }
     } else {
@@ -1654,11 +1623,11 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
     uint32_t hflg = 0, hfm = 0, hnk0 = 0, hnk1 = 0, hnks = 0;
     if (tid < a.R.n) {
         const RecHdr* h = a.R.h(tid);
-        hd0 = ldd_wt(&h->dmin[0]); hd1 = ldd_wt(&h->dmin[1]);
-        hc0 = ldobj_wt(&h->cand[0]); hc1 = ldobj_wt(&h->cand[1]);
-        hnks = ld32_wt(&h->nkeys);
-        hflg = ld32_wt(&h->flags) & 1u; hfm = ld32_wt(&h->fmask);
-        const uint32_t nkk = ld32_wt(&h->nkk[0]);
+        hd0 = ldd(&h->dmin[0]); hd1 = ldd(&h->dmin[1]);
+        hc0 = ldobj(&h->cand[0]); hc1 = ldobj(&h->cand[1]);
+        hnks = ld32(&h->nkeys);
+        hflg = ld32(&h->flags) & 1u; hfm = ld32(&h->fmask);
+        const uint32_t nkk = ld32(&h->nkk[0]);
         hnk0 = nkk & 0xFFFFu; hnk1 = nkk >> 16;
     }
     KB_STAMP(ctl, 28);
@@ -1725,7 +1694,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
     // round trip so they are not held in registers through it
     Contender hb0, hb1;
     hb0.s = hb1.s = -1;
-    if (do_res && tid < a.R.n) { hb0 = ldobj_wt(&a.R.h(tid)->best[0]); hb1 = ldobj_wt(&a.R.h(tid)->best[1]); }
+    if (do_res && tid < a.R.n) { hb0 = ldobj(&a.R.h(tid)->best[0]); hb1 = ldobj(&a.R.h(tid)->best[1]); }
     KB_STAMP(ctl, 12);
     KB_STOP(1);
     // ---- the scan records (or the gathered rank summaries): one per thread, reduced
@@ -1745,7 +1714,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
             unsigned long long c0 = hc0, c1 = hc1;
             uint32_t flg = hflg, fm = hfm;
             for (int i = tid + STEP_THREADS; i < a.R.n; i += STEP_THREADS) {
-                const RecHdr h = ldobj_wt(a.R.h(i));
+                const RecHdr h = ldobj(a.R.h(i));
                 d0 = h.dmin[0] < d0 ? h.dmin[0] : d0;
                 d1 = h.dmin[1] < d1 ? h.dmin[1] : d1;
                 c0 += h.cand[0]; c1 += h.cand[1];
@@ -1788,10 +1757,10 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
 #pragma unroll
             for (int q = 0; q < NF; q++) f[q] = NONE32;
             for (int i = tid; i < a.R.n; i += STEP_THREADS) {
-                if (!ld32_wt(&a.R.h(i)->fmask)) continue;
+                if (!ld32(&a.R.h(i)->fmask)) continue;
                 const uint32_t* fi = a.R.f(i);
 #pragma unroll
-                for (int q = 0; q < NF; q++) f[q] = min(f[q], ld32_wt(fi + q));
+                for (int q = 0; q < NF; q++) f[q] = min(f[q], ld32(fi + q));
             }
 #pragma unroll
             for (int q = 0; q < NF; q++) {
@@ -1846,7 +1815,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
                 uint32_t nks = hnks;
                 if (i != tid) {
                     const RecHdr* h = a.R.h(i);
-                    d0 = ldd_wt(&h->dmin[0]); d1 = ldd_wt(&h->dmin[1]); nks = ld32_wt(&h->nkeys);
+                    d0 = ldd(&h->dmin[0]); d1 = ldd(&h->dmin[1]); nks = ld32(&h->nkeys);
                 }
                 const bool q0 = need0 && d0 <= g0 + 8.0 * eps;
                 const bool q1 = need1 && d1 <= g1 + 8.0 * eps;
@@ -1859,7 +1828,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
                 const int i = x / cap, k = x - i * cap;
                 const uint32_t rq = s_rq[i];
                 if (k >= (int)(rq >> 2)) continue;
-                const Contender c = ldobj_wt(a.R.k(i) + k);
+                const Contender c = ldobj(a.R.k(i) + k);
                 if (!((rq >> (c.kind ? 1 : 0)) & 1u)) continue;
                 if (cont_delta_ld(s_ld, c, inv_avg) <= (c.kind ? g1 : g0) + 4.0 * eps &&
                     dedup_insert(T, c.kind, c.s, c.t, c.w, c.iter) < 0)
@@ -1868,13 +1837,13 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
         } else {
             for (int i = tid; (need0 || need1) && i < a.R.n; i += STEP_THREADS) {
                 const RecHdr* h = a.R.h(i);
-                const bool q0 = need0 && ldd_wt(&h->dmin[0]) <= g0 + 8.0 * eps;
-                const bool q1 = need1 && ldd_wt(&h->dmin[1]) <= g1 + 8.0 * eps;
+                const bool q0 = need0 && ldd(&h->dmin[0]) <= g0 + 8.0 * eps;
+                const bool q1 = need1 && ldd(&h->dmin[1]) <= g1 + 8.0 * eps;
                 if (!q0 && !q1) continue;
                 const Contender* keys = a.R.k(i);
-                const int nk = (int)min(ld32_wt(&h->nkeys), (uint32_t)a.R.cap);
+                const int nk = (int)min(ld32(&h->nkeys), (uint32_t)a.R.cap);
                 for (int k = 0; k < nk; k++) {
-                    const Contender c = ldobj_wt(keys + k);
+                    const Contender c = ldobj(keys + k);
                     if (!(c.kind ? q1 : q0)) continue;
                     if (cont_delta_ld(s_ld, c, inv_avg) <= (c.kind ? g1 : g0) + 4.0 * eps &&
                         dedup_insert(T, c.kind, c.s, c.t, c.w, c.iter) < 0)
@@ -1890,7 +1859,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
         // raw spills of the scan (rare): every thread
         const uint32_t n = min(C.ncont, a.cont_cap);
         for (uint32_t i = tid; i < n; i += STEP_THREADS) {
-            const Contender c = ldobj_wt(a.cont + i);
+            const Contender c = ldobj(a.cont + i);
             if (cont_delta_ld(s_ld, c, inv_avg) <= s_g[c.kind] + 4.0 * eps &&
                 dedup_insert(T, c.kind, c.s, c.t, c.w, c.iter) < 0)
                 s_kfail[c.kind] = 1;
@@ -2714,9 +2683,9 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
         const bool bkeys = do_res && tid < a.R.n;
         Contender bk0, bk1, bx0, bx1;
         bk0.s = bk1.s = bx0.s = bx1.s = -1;
-        if (bkeys) { bk0 = ldobj_wt(&a.R.h(tid)->best[0]); bk1 = ldobj_wt(&a.R.h(tid)->best[1]); }
+        if (bkeys) { bk0 = ldobj(&a.R.h(tid)->best[0]); bk1 = ldobj(&a.R.h(tid)->best[1]); }
         if (bkeys && !a.use_spill) {                  // rank summaries: the second-best keys too
-            bx0 = ldobj_wt(a.R.k(tid) + (a.R.cap - 2)); bx1 = ldobj_wt(a.R.k(tid) + (a.R.cap - 1));
+            bx0 = ldobj(a.R.k(tid) + (a.R.cap - 2)); bx1 = ldobj(a.R.k(tid) + (a.R.cap - 1));
         }
         if (tid < nT) { s_fl[s_T[tid]] |= BF_TOUCHED; s_cntT[tid] = 0; }
         if (tid == 0) { s_unc = 0; s_nsub = 0; }
@@ -3273,9 +3242,9 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
     const bool bkeys = do_res && !full && tid < a.R.n;
     Contender bk0, bk1, bx0, bx1;
     bk0.s = bk1.s = bx0.s = bx1.s = -1;
-    if (bkeys) { bk0 = ldobj_wt(&a.R.h(tid)->best[0]); bk1 = ldobj_wt(&a.R.h(tid)->best[1]); }
+    if (bkeys) { bk0 = ldobj(&a.R.h(tid)->best[0]); bk1 = ldobj(&a.R.h(tid)->best[1]); }
     if (bkeys && !a.use_spill) {                      // rank summaries: the second-best keys too
-        bx0 = ldobj_wt(a.R.k(tid) + (a.R.cap - 2)); bx1 = ldobj_wt(a.R.k(tid) + (a.R.cap - 1));
+        bx0 = ldobj(a.R.k(tid) + (a.R.cap - 2)); bx1 = ldobj(a.R.k(tid) + (a.R.cap - 1));
     }
     // approximate S (exact in integral mode: integers below 2^52), total load error E
     double sS = 0.0, sE = 0.0;
@@ -3896,10 +3865,10 @@ __device__ __attribute__((noinline)) void eager_refold(const RefreshArgs* rfp, i
 // r) and a second-best key of another partition, and its near-tie keys within 4 eps of its
 // own minima.  One record per thread (R.n <= SUM_RECS; the host keeps a sharded engine's
 // scan grid within it), so every record field is loaded once; the near-tie keys are then
-// loaded one key slot per thread, all in flight at once.  Every record byte is read with sc1
-// loads (ldobj_wt): the scan workgroups store them write-through, so the fused form
-// (k_scansum: this body in the scan grid's last workgroup, after its wait) needs no acquire.
-__device__ __forceinline__ void summary_body(const SumArgs& a) {
+// loaded one key slot per thread, all in flight at once.
+// (s_r: LDS for the relative loads r, B doubles: every key is re-scored from LDS; staged:
+// the caller already copied r there -- k_scansum does it while the scan runs)
+__device__ __forceinline__ void summary_body(const SumArgs& a, double* s_r, bool staged) {
     DevCtl* ctl = a.ctl;
     RecHdr* out = a.out.h(0);
     Contender* okeys = a.out.k(0);
@@ -3942,12 +3911,14 @@ __device__ __forceinline__ void summary_body(const SumArgs& a) {
     bk[0].s = bk[1].s = -1;
     if (mine) {
         const RecHdr* h = a.R.h(tid);
-        d0 = ldd_wt(&h->dmin[0]); d1 = ldd_wt(&h->dmin[1]);
-        c0 = ldobj_wt(&h->cand[0]); c1 = ldobj_wt(&h->cand[1]);
-        nks = min(ld32_wt(&h->nkeys), (uint32_t)a.R.cap);
-        fm = ld32_wt(&h->fmask);
-        bk[0] = ldobj_wt(&h->best[0]); bk[1] = ldobj_wt(&h->best[1]);
+        d0 = ldd(&h->dmin[0]); d1 = ldd(&h->dmin[1]);
+        c0 = ldobj(&h->cand[0]); c1 = ldobj(&h->cand[1]);
+        nks = min(ld32(&h->nkeys), (uint32_t)a.R.cap);
+        fm = ld32(&h->fmask);
+        bk[0] = ldobj(&h->best[0]); bk[1] = ldobj(&h->best[1]);
     }
+    if (!staged)                                     // (the header loads above are in flight)
+        for (int b = tid; b < a.B; b += 1024) s_r[b] = a.r[b];
     if (tid < SUM_RECS) s_rk[tid] = nks;
     const uint32_t myfm = fm;
     d0 = wave_min(d0); d1 = wave_min(d1); c0 = wave_sum(c0); c1 = wave_sum(c1);
@@ -3960,7 +3931,7 @@ __device__ __forceinline__ void summary_body(const SumArgs& a) {
     if (myfm) {
         const uint32_t* fi = a.R.f(tid);
         for (int q = 0; q < NF; q++) {
-            const uint32_t v = ld32_wt(fi + q);
+            const uint32_t v = ld32(fi + q);
             if (v != NONE32) atomicMin(&s_f[q], v);
         }
     }
@@ -3977,24 +3948,26 @@ __device__ __forceinline__ void summary_body(const SumArgs& a) {
     unsigned long long me[2] = {NONE64, NONE64};
     for (int k = 0; k < 2; k++)
         if (bk[k].s >= 0) {
-            me[k] = enc(cont_delta(a.r, bk[k], inv_avg));
+            me[k] = enc(cont_delta(s_r, bk[k], inv_avg));
             atomicMin(&s_benc[k], me[k]);
         }
     __syncthreads();
     auto ins = [&](const Contender& c) {
         const double g = s_g[c.kind];
         if (!(g < HUGE_VAL)) return;               // (no census wave on this rank for the kind)
-        if (!(cont_delta(a.r, c, inv_avg) <= g + 4.0 * eps)) return;
+        if (!(cont_delta(s_r, c, inv_avg) <= g + 4.0 * eps)) return;
         if (dedup_insert(T, c.kind, c.s, c.t, c.w, c.iter) < 0) s_fail = 1;
     };
     {
+        // (tried: the first 4 key slots per thread loaded speculatively beside the headers --
+        // 130 KB through one workgroup per step at c3, the summary 2.2 us slower)
         const int kc = a.R.cap, tot = a.R.n * kc;
         for (int x = tid; x < tot; x += 1024) {
             const int i = x / kc, k = x - i * kc;
-            if (k < (int)s_rk[i]) ins(ldobj_wt(a.R.k(i) + k));
+            if (k < (int)s_rk[i]) ins(ldobj(a.R.k(i) + k));
         }
-        const uint32_t nc = min(__hip_atomic_load(&ctl->ncont, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), a.cont_cap);
-        for (uint32_t i = tid; i < nc; i += 1024) ins(ldobj_wt(a.cont + i));
+        const uint32_t nc = min(ctl->ncont, a.cont_cap);
+        for (uint32_t i = tid; i < nc; i += 1024) ins(ldobj(a.cont + i));
     }
     for (int k = 0; k < 2; k++)
         if (me[k] != NONE64 && me[k] == s_benc[k]) atomicMin(&s_brec[k], (uint32_t)tid);
@@ -4032,7 +4005,7 @@ __device__ __forceinline__ void summary_body(const SumArgs& a) {
         if (s_brec2[tid] == NONE32) okeys[capk + tid] = x;
     }
     if (tid == 0) {
-        const uint32_t ovf = __hip_atomic_load(&ctl->cont_overflow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t ovf = ctl->cont_overflow;
         out->nkeys = s_n < capk ? s_n : capk;
         out->flags = (ovf || s_fail || s_n > capk) ? 1u : 0u;
         out->flags |= 2u;
@@ -4047,7 +4020,12 @@ __device__ __forceinline__ void summary_body(const SumArgs& a) {
     }
 }
 
-__global__ __launch_bounds__(1024) void k_summary(SumArgs a) { summary_body(a); }
+__global__ __launch_bounds__(1024) void k_summary(SumArgs a) {
+    // (r in LDS up to SUM_RLDS brokers; past that, the keys are re-scored from memory)
+    extern __shared__ __align__(16) double sum_dyn[];
+    if (a.B <= SUM_RLDS) summary_body(a, sum_dyn, false);
+    else summary_body(a, const_cast<double*>(a.r), true);
+}
 
 // The scan and the rank summary in one launch (sharded engines): the scan's grid plus one
 // resident summary workgroup, the last of the grid, which waits for the others' arrivals
@@ -4059,6 +4037,11 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scansum(ScanArgs a, SumArgs sa
     if ((int)blockIdx.x == (int)gridDim.x - 1) {
         const int tid = threadIdx.x, lane = tid & 63;
         __shared__ int s_to;
+        // r does not change while the scan runs: staged into this workgroup's dynamic LDS
+        // (the scan's tables' space, at least 16 B per broker) before the wait
+        extern __shared__ __align__(16) unsigned char smem_sum[];
+        double* s_r = (double*)smem_sum;
+        for (int b = tid; b < sa.B; b += 1024) s_r[b] = sa.r[b];
         if (tid < 64) {
             const unsigned long long t0 = wall_clock64();
             int to = 0;
@@ -4069,6 +4052,8 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scansum(ScanArgs a, SumArgs sa
                 if (wave_sum(v) >= (uint32_t)sa.wait_n) break;
                 __builtin_amdgcn_s_sleep(1);
             }
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // (the other XCDs' writes)
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             if (!to && lane < PAIR_SHARDS)
                 __hip_atomic_store(sa.wait_cnt + lane * PAIR_STRIDE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (lane == 0) s_to = to;
@@ -4089,7 +4074,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scansum(ScanArgs a, SumArgs sa
             }
             return;
         }
-        summary_body(sa);
+        summary_body(sa, s_r, true);
         return;
     }
     const bool wt = (int)blockIdx.x < a.nscan && !(a.rfpass && a.ctl->halted == H_NEED_EXACT);
@@ -4284,7 +4269,7 @@ void launch_refresh(const RefreshArgs& a, hipStream_t st) {
     if (a.B > 0) hipLaunchKernelGGL(k_refresh, dim3(a.B), dim3(REFRESH_THREADS), 0, st, a);
 }
 void launch_summary(const SumArgs& a, hipStream_t st) {
-    hipLaunchKernelGGL(k_summary, dim3(1), dim3(1024), 0, st, a);
+    hipLaunchKernelGGL(k_summary, dim3(1), dim3(1024), a.B <= SUM_RLDS ? (size_t)a.B * 8 : 0, st, a);
 }
 
 template <int RC, bool LSETS, bool BK>

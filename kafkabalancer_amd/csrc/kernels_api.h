@@ -121,8 +121,6 @@ struct StepArgs {
     int wait_n;               //    grid's other workgroups), then resets it
     int fuse_pre;             // k_pair: stage the broker tables before the wait (diagnostic 0: after)
     unsigned long long wait_ticks;   // k_pair: the wait's bound (100 MHz ticks; 2 s, tests: 0)
-    int pair_acq;             // k_pair: agent acquire after the wait even when every handed-off
-                              //    byte was stored write-through (A/B; 0 = sc1 loads only)
 };
 
 
@@ -132,6 +130,7 @@ struct SumArgs {
     const Contender* cont;
     uint32_t cont_cap;
     const double* r;
+    int B;                    // brokers (r's length; k_summary stages r in LDS, B <= MAXB)
     Recs out;                 // one summary (summary_recs layout)
     int spill_growable;       // 1: this rank's spill buffer can still grow (summary flag bit 2)
     // k_scansum (the summary workgroup in the scan's grid): the arrival count it waits on

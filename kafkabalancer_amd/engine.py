@@ -65,7 +65,8 @@ class kb_stats(C.Structure):
                 ("max_replicas", C.c_int32), ("refreshes", C.c_int64), ("exact_halts", C.c_int64),
                 ("scan_workgroups", C.c_int64), ("retries", C.c_int64), ("spill_grows", C.c_int64),
                 ("blocks_scanned", C.c_int64), ("relists", C.c_int64),
-                ("fused_pairs", C.c_int64), ("fused_summaries", C.c_int64)]
+                ("fused_pairs", C.c_int64), ("fused_summaries", C.c_int64),
+                ("eager", C.c_int64), ("eager_switches", C.c_int64)]
 
 
 _lib = None

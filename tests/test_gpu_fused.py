@@ -183,3 +183,18 @@ def test_summary_timeout_poisons_engine():
     eng.close()
     got, err, st, _ = _sharded_world1(cl, cfg, 10, ("KB_FUSE_SUM", "1"))
     assert err is None and len(got) == 10 and st["fused_summaries"] == 1
+
+
+def test_sharded_summary_wide_brokers_match_plain_plan():
+    """A sharded engine past SUM_RLDS brokers (9000: broker tables in memory, k_summary
+    re-scores the keys from r in memory, no fused summary) gives the unsharded plan."""
+    cl = synth.make_cluster(30000, 9000, 3, "zipf", seed=0x5EED9000)
+    cfg = {"allow_leader": True, "rebalance_leaders": False, "min_replicas": 2, "min_unbalance": 0.0,
+           "brokers": None}
+    ref = E.Engine(cl, cfg)
+    want, err = ref.plan(24)
+    ref.close()
+    assert err is None and len(want) == 24
+    got, err, st, _ = _sharded_world1(cl, cfg, 24, ("KB_FUSE_SUM", "1"))
+    assert err is None and st["fused_summaries"] == 0
+    assert keyed(got) == keyed(want)

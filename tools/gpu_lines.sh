@@ -1,6 +1,7 @@
 #!/bin/bash
 # bench lines of a measurement session into gpurun_out/$TAG/: the default bench (c3, with
-# the CPU baseline), c2 / c4 / c5 (no CPU baseline), the drop-in costs at c3 and the
+# the CPU baseline), c2 / c4 / c5 / c3 at 1000 steps / c3nl / w16k (each with its CPU
+# baseline), the drop-in costs at c3 and the
 # rocprofv3 kernel-trace summaries of c3 and c2.  LINES overrides the list.
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 O=gpurun_out/${TAG:-lines}; mkdir -p $O
@@ -18,6 +19,9 @@ for l in ${LINES:-default c2 c4 c5 dropin prof}; do
     c2) run c2 300 --workload c2 --steps 80 --cpu-seconds 10 ;;
     c4) run c4 400 --workload c4 --steps 1000 --cpu-seconds 10 ;;
     c5) run c5 600 --workload c5 --steps 200 --cpu-seconds 10 ;;
+    c3full) run c3full 400 --steps 1000 --cpu-seconds 10 ;;
+    c3nl) run c3nl 400 --workload c3nl --steps 1000 --cpu-seconds 10 ;;
+    w16k) run w16k 400 --workload w16k --steps 200 --cpu-seconds 10 ;;
     dropin) run dropin 500 --workload c3 --drop-in --steps 200 ;;
     prof) WLS="c3 c5" tools/prof_wl.sh > $O/prof.txt 2>&1 || { cat $O/prof.txt; exit 1; }
           cat $O/prof.txt
