@@ -848,6 +848,10 @@ __device__ __forceinline__ void scan_round(const ScanArgs& a, const ScanParams& 
     const bool ub_open = ubN == HUGE_VAL || (a.allow_leader && ubL == HUGE_VAL);
     if (!run || (a.dbg & 4) || (a.ubpass && !ub_open)) return;
     const bool census_off = (a.dbg & 1) || q.ubpass;
+    // (bound keys are for the next step's census bound: none when this step's bound is
+    // -inf -- the step after a first-index stage, whose successor is almost always one too
+    // and which re-scans with the bound opened if it reaches move() after all)
+    const bool bk_on = BK && !census_off && ubN != -HUGE_VAL;
     // Lower-bound prune.  The source delta f(r_s - delta) - f(r_s) decreases and the
     // target delta f(r_t + delta) - f(r_t) increases with the relative load (f is
     // convex), so every candidate of a partition with weight w scores
@@ -1012,7 +1016,7 @@ __device__ __forceinline__ void scan_round(const ScanArgs& a, const ScanParams& 
         // windows); this key only bounds.  (The lane holding the wave minimum finds its
         // (partition, slot) again by re-scoring its two partitions, the same arithmetic, rather
         // than the scoring loop carrying an argmin in registers for every lane.)
-        if (BK && !census_off) {
+        if (bk_on) {
             const bool needL = !hasL && a.allow_leader && __ballot(lL < HUGE_VAL);
             const bool needN = !hasN && __ballot(lN < HUGE_VAL);
             const double wL = needL ? wave_min(lL) : HUGE_VAL, wN = needN ? wave_min(lN) : HUGE_VAL;
@@ -1797,7 +1801,11 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
         // table -- the summary's key list holds it; and a single key whose record
         // offered no best key is collected rather than guessed)
         const bool many = a.R.n > STEP_THREADS || (a.use_spill && C.ncont > 0) || !a.use_spill;
-        const bool need0 = many || s_kc[0] > 1 || s_sok[0] < 0, need1 = many || s_kc[1] > 1 || s_sok[1] < 0;
+        // (s_kc counts every key of the scan records in the windows, stored or spilled: a kind
+        // with none has nothing to collect -- the step after a first-index stage, census off)
+        const bool counted = a.R.n <= STEP_THREADS && a.use_spill;
+        const bool need0 = (many || s_kc[0] > 1 || s_sok[0] < 0) && !(counted && s_kc[0] == 0);
+        const bool need1 = (many || s_kc[1] > 1 || s_sok[1] < 0) && !(counted && s_kc[1] == 0);
         if (tid < 2 && !(tid ? need1 : need0) && s_kc[tid] == 1) {
             s_nd[tid] = s_sok[tid] ? 1 : 0;          // resolve takes s_single (s_li == -2)
             s_li[tid] = -2;
