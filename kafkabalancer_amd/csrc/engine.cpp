@@ -103,6 +103,9 @@ struct kb_engine {
     int64_t slots_scan = 0, slots_pair = 0, slots_sum = 0;
     bool eager_auto = false;          // lazy loads now; eager refolds once exact halts are frequent
     int64_t eager_switches = 0;
+    // the halt rate's window: the steps and exact halts at the checkpoint before last (w0)
+    // and at the last one (w1), checkpoints at least 64 steps apart
+    unsigned long long w0_steps = 0, w0_halts = 0, w1_steps = 0, w1_halts = 0;
     int fuse_pre = 1;                 // k_pair stages the tables before its wait (KB_FUSE_PRE=0: after)
     size_t pair_lds = 0;              // k_pair's dynamic LDS: max(scan, step)
     bool gb = false;                  // B > MAXB: broker tables in memory (k_scan GT, k_step GB)
@@ -1216,14 +1219,23 @@ static int grow_spill(kb_engine* e) {
 // decision needs exact folds, and the approximate loads' error widens eps and with it the
 // census; on a balanced cluster without -allow-leader that is a quarter of the steps (c3nl
 // past its 300th step: 0.118 ms/step lazy, 0.051 eager).  Once the halts reach one per 16
-// steps the plan switches to eager refolds (the next launches refold the touched brokers
+// steps over the last 64-128 steps (at least 4 of them) the plan switches to eager refolds
+// (the next launches refold the touched brokers
 // beside the scan): the grids shrink by the eager workgroups so every workgroup of a fused
 // launch stays resident.  Switched between batches, where no list edit is in flight but the
 // last step's (which the next launch's list workgroup applies, the eager workgroups having
 // no brokers yet).  The decisions do not depend on the mode.
 static void maybe_switch_to_eager(kb_engine* e, const DevCtl& c) {
     if (!e->eager_auto || e->eager) return;
-    if (c.total_exact_halts < 4 || 16 * c.total_exact_halts < (unsigned long long)std::max(c.steps, 1)) return;
+    const unsigned long long st = (unsigned long long)std::max(c.steps, 0), h = c.total_exact_halts;
+    const unsigned long long ds = st - std::min(st, e->w0_steps), dh = h - std::min(h, e->w0_halts);
+    if (dh < 4 || 16 * dh < ds) {
+        if (st >= e->w1_steps + 64) {
+            e->w0_steps = e->w1_steps; e->w0_halts = e->w1_halts;
+            e->w1_steps = st; e->w1_halts = h;
+        }
+        return;
+    }
     const int64_t lw = EGW + 1;                       // the eager workgroups and the list workgroup
     int64_t n = std::min<int64_t>(e->nscan, std::max<int64_t>(1, e->slots_scan - lw));
     if (e->fuse) n = std::min<int64_t>(n, std::max<int64_t>(1, e->slots_pair - lw - 1));
