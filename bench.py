@@ -72,7 +72,7 @@ def _move_sample(cl, cfg, seconds):
     assert r["status"] == 0, r["err"]
     P = cl.n
     leaders = bool(cfg.get("allow_leader"))
-    k = 16
+    k = 1                          # (w16k: one partition's move() is ~1 s of 16384-term folds)
     while True:
         t0 = time.perf_counter()
         n, _ = O.move_sample(opl, cfg, leaders, k)
@@ -317,6 +317,15 @@ def kernel_times(eng, steps, mode):
     return {k: (1e3 * v[0] / max(v[1], 1), v[1]) for k, v in tk.items()}
 
 
+_T0 = time.perf_counter()
+
+
+def progress(msg):
+    """A line on stderr per phase (long runs -- c5, w16k, the CPU baselines -- print nothing
+    else before their JSON line)."""
+    print("bench %.1fs: %s" % (time.perf_counter() - _T0, msg), file=sys.stderr, flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -398,11 +407,13 @@ def main():
     from kafkabalancer_amd import synth
     torch.cuda.set_device(0)
     cl, cfg, desc = synth.config(args.workload, scale=args.scale)
+    progress("%s: %d partitions built" % (args.workload, cl.n))
     incr = args.mode == "incremental"
     eng = E.Engine(cl, cfg, device=0, time_kernels=False, incremental=incr)
     if args.warmup:
         _, err = eng.plan(args.warmup)
         assert err is None, err
+    progress("engine created, %d warm-up steps" % args.warmup)
     st0 = eng.stats()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -411,6 +422,7 @@ def main():
     wall = time.perf_counter() - t0
     changes, err = eng.changes(*raw)            # (Python dicts, outside the timed region)
     assert err is None, err
+    progress("timed plan: %d steps in %.3f s" % (len(changes), wall))
     st1 = eng.stats()
     if args.plan_out:
         with open(args.plan_out, "w") as f:
@@ -461,7 +473,9 @@ def main():
         return kt, s0, s1, iso
 
     kdc, stk0, stk1, scan_iso_us = replay(1)
+    progress("kernel timing replay (device clock) done")
     kev, _, _, _ = replay(2)
+    progress("kernel timing replay (events) done")
     scan_us, scan_n = kdc["scan"]
     if not scan_n:                      # (no back-to-back launch: the inner interval)
         scan_us, scan_n = kdc["scan_inner"]
@@ -565,7 +579,9 @@ def main():
         "engine_events": {k: st1[k] - st0[k] for k in ("retries", "refreshes", "exact_halts", "exact_folds")},
     }
     if not args.no_cpu_baseline:
+        progress("CPU baseline (%.0f s sample)" % args.cpu_seconds)
         out["cpu_baseline"] = cpu_baseline(cl, cfg, desc, cand / max(steps, 1), args.cpu_seconds)
+        progress("CPU baseline done")
         cb = out["cpu_baseline"]
         if cb.get("unit") == "candidates/s" and cb.get("value"):
             out["speedup_vs_cpu"] = out["value"] / cb["value"]
