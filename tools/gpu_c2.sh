@@ -1,7 +1,6 @@
 #!/bin/bash
-# Step-body session: bench lines of c2 / c3 / c3nl / c5 at their headline step counts, c3
-# with the post-wait acquire forced back on (KB_PAIR_ACQ=1, A/B on the same box), the
-# KB_STAMPS phase breakdown of c2 and c3, then the GPU suite.
+# Step-body session: bench lines of c2 / c3 / c3nl / c5 at their headline step counts, the
+# sharded world-1 line with and without the fused summary, the KB_STAMPS phase breakdown of c2 and c3, then the GPU suite.
 # Usage: gpurun -- 'bash tools/gpu_c2.sh <tag> [suite]'
 set -u
 T=${1:-x}
@@ -9,7 +8,6 @@ O=gpurun_out/$T
 mkdir -p $O
 timeout -k 10 300 python bench.py --workload c2 --steps 100 --no-cpu-baseline > $O/c2.json 2> $O/c2.err &&
 timeout -k 10 300 python bench.py --steps 1000 --no-cpu-baseline > $O/c3.json 2> $O/c3.err &&
-KB_PAIR_ACQ=1 timeout -k 10 300 python bench.py --steps 1000 --no-cpu-baseline > $O/c3_acq.json 2> $O/c3_acq.err &&
 timeout -k 10 300 python bench.py --steps 1000 --no-cpu-baseline > $O/c3b.json 2> $O/c3b.err &&
 timeout -k 10 300 python bench.py --workload c3nl --steps 1000 --no-cpu-baseline > $O/c3nl.json 2> $O/c3nl.err &&
 timeout -k 10 300 python bench.py --workload c5 --steps 200 --no-cpu-baseline > $O/c5.json 2> $O/c5.err &&
