@@ -117,23 +117,42 @@ def test_control_transfer_modes_match(mode):
     ref.close()
 
 
+class _DevBuf:
+    """A zeroed device buffer from the HIP runtime the engine uses (no torch: only the
+    engine's own stream touches it)."""
+    _hip = None
+
+    def __init__(self, nbytes):
+        import ctypes
+        if _DevBuf._hip is None:
+            _DevBuf._hip = ctypes.CDLL("libamdhip64.so")
+        self.p = ctypes.c_void_p()
+        assert _DevBuf._hip.hipMalloc(ctypes.byref(self.p), ctypes.c_size_t(nbytes)) == 0
+        assert _DevBuf._hip.hipMemset(self.p, 0, ctypes.c_size_t(nbytes)) == 0
+        assert _DevBuf._hip.hipDeviceSynchronize() == 0
+
+    def ptr(self):
+        return self.p.value
+
+    def free(self):
+        _DevBuf._hip.hipFree(self.p)
+
+
 def _sharded_world1(cl, cfg, steps, env):
     """The batched sharded protocol at world size 1 (the summary is its own gathered
     buffer), with the given environment at engine creation; (changes, error, stats, loads)."""
-    import torch
     eng = _with_env(*env, lambda: E.Engine(cl, cfg, shard=(0, cl.n)))
-    got, err = [], None
+    got, err, bufs = [], None, []
     try:
         done = False
         while not done and len(got) < steps:
-            nb = eng.summary_bytes()
-            summ = torch.zeros(nb, dtype=torch.uint8, device="cuda")
-            torch.cuda.synchronize()
+            summ = _DevBuf(eng.summary_bytes())
+            bufs.append(summ)
             batch = min(16, steps - len(got))
             eng.sharded_reset(batch)
             for _ in range(batch):
-                eng.sharded_scan(summ.data_ptr())
-                eng.sharded_resolve(summ.data_ptr(), 1)
+                eng.sharded_scan(summ.ptr())
+                eng.sharded_resolve(summ.ptr(), 1)
             st, ch = eng.sharded_collect(batch + 1)
             got.extend(ch)
             done = st == "done"
@@ -142,6 +161,8 @@ def _sharded_world1(cl, cfg, steps, env):
     st = eng.stats()
     loads = eng.loads() if err is None else None
     eng.close()
+    for b in bufs:
+        b.free()
     return got, err, st, loads
 
 
@@ -164,16 +185,14 @@ def test_summary_timeout_poisons_engine():
     """k_scansum's summary workgroup gives up waiting for its grid (a zero wait bound): the
     batch ends with the explicit error, the arrival count is reset, and the engine refuses
     further sharded work."""
-    import torch
     cl, cfg, _ = synth.config("c3", scale=0.25)
     eng = _with_env("KB_PAIR_WAIT_TICKS", "0", lambda: E.Engine(cl, cfg, shard=(0, cl.n)))
     assert eng.stats()["fused_summaries"] == 1
-    summ = torch.zeros(eng.summary_bytes(), dtype=torch.uint8, device="cuda")
-    torch.cuda.synchronize()
+    summ = _DevBuf(eng.summary_bytes())
     eng.sharded_reset(4)
     for _ in range(4):
-        eng.sharded_scan(summ.data_ptr())
-        eng.sharded_resolve(summ.data_ptr(), 1)
+        eng.sharded_scan(summ.ptr())
+        eng.sharded_resolve(summ.ptr(), 1)
     with pytest.raises(E.EngineError) as ei:
         eng.sharded_collect(5)
     assert "timed out" in str(ei.value)
@@ -181,6 +200,7 @@ def test_summary_timeout_poisons_engine():
         eng.sharded_reset(1)
     assert "unusable" in str(ei.value)
     eng.close()
+    summ.free()
     got, err, st, _ = _sharded_world1(cl, cfg, 10, ("KB_FUSE_SUM", "1"))
     assert err is None and len(got) == 10 and st["fused_summaries"] == 1
 
