@@ -856,6 +856,7 @@ static void fill_scan_args(kb_engine* e, ScanArgs& s) {
     s.eager = e->eager && e->nscan > 0 ? EGW : 0;
     s.gt = e->gb ? 1 : 0;
     s.done = e->pair_cnt;
+    s.pred = 0;                       // (enqueue_pair sets it for k_pair)
     s.dyn_lds = (int)e->scan_lds;
 }
 
@@ -966,6 +967,7 @@ static void enqueue_pair(kb_engine* e, bool rf = false, bool rf_scan = false) {
         ScanArgs s;
         fill_scan_args(e, s);
         s.rfpass = rf && rf_scan && e->rf_stream;
+        s.pred = 1;
         StepArgs a;
         fill_step_args(e, a, scan_recs(e->recs, (int)e->nscan), 1);
         a.rf_final = rf && e->rf_stream;

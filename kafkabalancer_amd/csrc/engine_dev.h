@@ -41,6 +41,12 @@ constexpr int TMAX = 2 * MAXR + 4;  // brokers touched by one applied change (bo
 constexpr int EGW = 4;              // eager refold workgroups per scan launch (touched brokers)
 constexpr int PAIR_SHARDS = 8;      // k_pair's arrival count: one word per XCD group of blocks,
 constexpr int PAIR_STRIDE = 32;     // each on a 128-B line of its own
+// k_pair's scan workgroups also fold their record's minima, candidate counts and predicate
+// mask into their arrival line (u32 word offsets; the u64 words 8-byte aligned): the step
+// workgroup reads the grid's reduction from the 8 lines instead of reducing every record
+// after its wait.  Zero is every word's identity: the minima are stored as ~enc(d) and
+// combined with max.
+constexpr int PRED_M0 = 2, PRED_M1 = 4, PRED_C0 = 6, PRED_C1 = 8, PRED_FM = 10;
 constexpr int RF_CHUNK = 2048;       // in-stream refresh: contributions per fold chunk (two buffers)
 constexpr int RF_LDS_BYTES = 2 * RF_CHUNK * 8;
 constexpr int BLK = 128;            // partitions of one wave in a scan tile = one block of

@@ -1235,6 +1235,17 @@ __device__ __forceinline__ void scan_round(const ScanArgs& a, const ScanParams& 
             else { r.best[k].s = r.best[k].t = -1; r.best[k].w = 0.0; r.best[k].iter = NONE64; r.best[k].kind = k; r.best[k].pad = 0; }
         }
         stobj_wt(hdr, r);
+        if (a.pred) {
+            // k_pair: the record's minima, counts and predicate mask folded into this
+            // workgroup's arrival line (performed at L2 before the arrival add: the step
+            // workgroup reads the grid's reduction there after its wait)
+            uint32_t* sh = a.done + (wg % PAIR_SHARDS) * PAIR_STRIDE;
+            __hip_atomic_fetch_max((unsigned long long*)(sh + PRED_M0), ~enc(wgL), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_max((unsigned long long*)(sh + PRED_M1), ~enc(wgN), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (cL) __hip_atomic_fetch_add((unsigned long long*)(sh + PRED_C0), cL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (cN) __hip_atomic_fetch_add((unsigned long long*)(sh + PRED_C1), cN, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (fm) __hip_atomic_fetch_or(sh + PRED_FM, fm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
         if (fm) {
             uint32_t* fo = a.R.f(wg);
 #pragma unroll
@@ -1585,9 +1596,38 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
             // record and key loads as 8-byte atomic loads)
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // (the other XCDs' writes)
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (!to && lane < PAIR_SHARDS)
-                __hip_atomic_store(a.wait_cnt + lane * PAIR_STRIDE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (lane == 0) s_wait_to = to;
+            // the grid's record reduction (ScanArgs.pred: every scanning workgroup folded its
+            // record's minima, counts and predicate mask into its arrival line before counting
+            // in), read once the count is complete, then every word of the line reset
+            unsigned long long m0 = 0, m1 = 0, c0 = 0, c1 = 0;
+            uint32_t fm = 0;
+            if (!to && lane < PAIR_SHARDS) {
+                uint32_t* sh = a.wait_cnt + lane * PAIR_STRIDE;
+                m0 = __hip_atomic_load((unsigned long long*)(sh + PRED_M0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                m1 = __hip_atomic_load((unsigned long long*)(sh + PRED_M1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                c0 = __hip_atomic_load((unsigned long long*)(sh + PRED_C0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                c1 = __hip_atomic_load((unsigned long long*)(sh + PRED_C1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                fm = __hip_atomic_load(sh + PRED_FM, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            m0 = wave_red_max(m0); m1 = wave_red_max(m1);
+            c0 = wave_sum(c0); c1 = wave_sum(c1);
+            fm = wave_red_or(fm);
+            if (!to && lane < PAIR_SHARDS) {
+                // (after the loads: the reductions above consumed them)
+                uint32_t* sh = a.wait_cnt + lane * PAIR_STRIDE;
+                __hip_atomic_store(sh, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store((unsigned long long*)(sh + PRED_M0), 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store((unsigned long long*)(sh + PRED_M1), 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store((unsigned long long*)(sh + PRED_C0), 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store((unsigned long long*)(sh + PRED_C1), 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(sh + PRED_FM, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            if (lane == 0) {
+                s_wait_to = to;
+                s_g[0] = m0 ? dec(~m0) : HUGE_VAL; s_g[1] = m1 ? dec(~m1) : HUGE_VAL;
+                s_cand[0] = c0; s_cand[1] = c1;
+                s_fm = fm;
+            }
         }
         __syncthreads();
         if (s_wait_to) {
@@ -1713,6 +1753,19 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
         __shared__ double s_pd[2][NW];
         __shared__ unsigned long long s_pc[2][NW];
         __shared__ uint32_t s_pf[2][NW];
+        if constexpr (FUSED) {
+            // k_pair: the scanning workgroups reduced their records into the arrival lines
+            // (s_g / s_cand / s_fm are set from them after the wait); scan records carry no
+            // overflow flag (flags == 0), only the raw spill buffer can have overflowed
+            if (tid == 0) {
+                if (a.incr) {
+                    if (C.incr_ok) { s_cand[0] = C.cand_cache[0]; s_cand[1] = C.cand_cache[1]; }
+                    else { C.cand_cache[0] = s_cand[0]; C.cand_cache[1] = s_cand[1]; }
+                }
+                s_flags = a.use_spill && C.cont_overflow ? 1u : 0u;
+                C.last_fm = s_fm;
+            }
+        } else {
         if (wid < nrw) {
             double d0 = hd0, d1 = hd1;
             unsigned long long c0 = hc0, c1 = hc1;
@@ -1751,6 +1804,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
                 s_fm = fm;
                 C.last_fm = fm;
             }
+        }
         }
         __syncthreads();
         const double g0 = s_g[0], g1 = s_g[1];

@@ -32,7 +32,7 @@ def main():
         print(wl, "ms/step %.4f dev %.4f launch %.1f us frac %.3f scan %.1f" % (
             x["ms_per_step"], x["config"]["device_ms_per_step"], r["avg_launch_us"], r["frac"], r.get("scan_phase_us") or 0),
             {k: round(v, 1) for k, v in x["kernels_us_per_launch"].items()}, x["engine_events"])
-    for wl in ("c2", "c3"):
+    for wl in ("c2", "c3", "c3nl", "c5"):
         x = last_json(os.path.join(d, wl + "_stamps.json"))
         if x:
             st = {k: round(v, 2) for k, v in x["stamps_us_per_step"].items() if v >= 0.3}
