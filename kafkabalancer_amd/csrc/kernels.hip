@@ -1455,7 +1455,7 @@ __device__ double incr_wskip(double rlo, double rhi, double thr, double avg, dou
 }
 
 #ifndef KB_SET_G
-#define KB_SET_G 4   // records a wave rebuilds at once in the fused prep (A/B)
+#define KB_SET_G 2   // records a wave rebuilds at once in the fused prep (A/B: 2 beat 4 and 1 at c3)
 #endif
 
 #ifndef KB_CLIST
