@@ -138,6 +138,8 @@ struct kb_engine {
     bool eager = false;            // eager refolds of the touched brokers (ScanArgs.eager)
     RefreshArgs* rf_dev = nullptr; // the refresh's arguments in device memory (ScanArgs.rf)
     int dbg_scan = 0;
+    unsigned long long* wgt = nullptr;     // diagnostic (KB_WGT=path): scan workgroup timeline
+    std::string wgt_path;
     int incr = 0;                  // incremental mode (kb_engine_set_incremental)
     BlockDesc* bdesc = nullptr;    // partition blocks of the shard by wmax descending
     BlockDesc* ubdesc = nullptr;   // the bound pass's blocks (last best keys + heaviest)
@@ -689,6 +691,11 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
     }
     HIPCHK(hipStreamCreateWithFlags(&e->st, hipStreamNonBlocking));
     e->own_st = true;
+    if (const char* v = getenv("KB_WGT")) {                 // diagnostic: scan workgroup timeline
+        e->wgt_path = v;
+        HIPCHK(dalloc(&e->wgt, 3 * (size_t)std::max<int64_t>(e->nscan, 1)));
+        HIPCHK(hipMemset(e->wgt, 0, 3 * (size_t)std::max<int64_t>(e->nscan, 1) * 8));
+    }
     HIPCHK(dalloc(&e->w, e->Ppad));
     HIPCHK(dalloc(&e->meta, e->Ppad));
     HIPCHK(dalloc(&e->rep, (size_t)e->rc_dev * e->Ppad));
@@ -856,6 +863,7 @@ static void fill_scan_args(kb_engine* e, ScanArgs& s) {
     s.eager = e->eager && e->nscan > 0 ? EGW : 0;
     s.gt = e->gb ? 1 : 0;
     s.done = e->pair_cnt;
+    s.wgt = e->wgt;
     s.pred = 0;                       // (enqueue_pair sets it for k_pair)
     s.dyn_lds = (int)e->scan_lds;
 }
@@ -1785,6 +1793,20 @@ extern "C" int kb_engine_last_error(kb_engine* e, char* buf, size_t n) {
 
 extern "C" void kb_engine_destroy(kb_engine* e) {
     if (!e) return;
+    if (e->wgt) {
+        // diagnostic (KB_WGT=path): the last scan launch's {start, scored, record written}
+        // per workgroup (100 MHz device clock), appended as one JSON line
+        std::vector<unsigned long long> h(3 * (size_t)std::max<int64_t>(e->nscan, 1));
+        hipStreamSynchronize(e->st);
+        hipMemcpy(h.data(), e->wgt, h.size() * 8, hipMemcpyDeviceToHost);
+        if (FILE* f = fopen(e->wgt_path.c_str(), "a")) {
+            fprintf(f, "{\"nscan\": %lld, \"wg\": [", (long long)e->nscan);
+            for (size_t i = 0; i < h.size(); i++) fprintf(f, "%s%llu", i ? ", " : "", h[i]);
+            fprintf(f, "]}\n");
+            fclose(f);
+        }
+        hipFree(e->wgt);
+    }
     void* ptrs[] = {e->w, e->rep, e->meta, e->pset, e->nc, e->load, e->lerr, e->eb, e->bfl, e->cnt,
                     e->setbits, e->setrec, e->order, e->posu, e->blm, e->posm, e->r,
                     e->bset_off, e->bset_ids, e->gscr, e->pair_cnt, e->recs, e->cont, e->ctl, e->log, e->bdesc, e->ubdesc,

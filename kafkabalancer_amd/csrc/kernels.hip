@@ -1169,6 +1169,7 @@ __device__ __forceinline__ void scan_round(const ScanArgs& a, const ScanParams& 
         for (int f = 0; f < NF; f++) s_f[f][wid] = fst[f];
     }
     __syncthreads();   // also orders every census insert before the flush
+    const unsigned long long t_sc = a.wgt ? wall_clock64() : 0ull;
     // the wave partials, combined lane-parallel by the waves that use them (the key
     // flush below: waves 0..3, one per SIMD)
     if (wid < DEDUP_SCAN / 64) {
@@ -1215,6 +1216,18 @@ __device__ __forceinline__ void scan_round(const ScanArgs& a, const ScanParams& 
                 }
             }
         }
+        // each kind's best key outside the census (BK plans): the first wave holding the
+        // smallest, found lane-parallel (one lane per wave) rather than by lane 0 alone
+        int bkw[2] = {-1, -1};
+        if constexpr (BK) {
+#pragma unroll
+            for (int k = 0; k < 2; k++) {
+                const unsigned long long e = lane < NW ? s_bke[k][lane] : NONE64;
+                const unsigned long long m = wave_min(e);
+                const unsigned long long bb = __ballot(lane < NW && e == m && m != NONE64);
+                bkw[k] = bb ? __ffsll((long long)bb) - 1 : -1;
+            }
+        }
       if (lane == 0) {
         RecHdr r;
         r.dmin[0] = wgL; r.dmin[1] = wgN;
@@ -1227,14 +1240,14 @@ __device__ __forceinline__ void scan_round(const ScanArgs& a, const ScanParams& 
 #pragma unroll
         for (int k = 0; k < 2; k++) {
             if (s_bslot[k] != NONE32) { r.best[k] = dedup_entry(T, (int)s_bslot[k]); continue; }
-            // no census key: the best key of the waves outside the census (or none)
-            int bw = -1;
-            unsigned long long be = NONE64;
-            for (int x = 0; x < NW; x++) if (s_bke[k][x] < be) { be = s_bke[k][x]; bw = x; }
+            // no census key: the best key of the waves outside the census (or none; plans
+            // with -allow-leader keep no such keys)
+            const int bw = bkw[k];
             if (bw >= 0) r.best[k] = s_bkc[k][bw];
             else { r.best[k].s = r.best[k].t = -1; r.best[k].w = 0.0; r.best[k].iter = NONE64; r.best[k].kind = k; r.best[k].pad = 0; }
         }
         stobj_wt(hdr, r);
+        if (a.wgt) { a.wgt[3 * wg] = t_in; a.wgt[3 * wg + 1] = t_sc; a.wgt[3 * wg + 2] = wall_clock64(); }
         if (a.pred) {
             // k_pair: the record's minima, counts and predicate mask folded into this
             // workgroup's arrival line (performed at L2 before the arrival add: the step

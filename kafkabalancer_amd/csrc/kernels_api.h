@@ -71,6 +71,7 @@ struct ScanArgs {
                               //    last applied step's touched brokers (DevCtl.eg_*)
     int gt;                   // 1: the broker tables are read from memory (B > MAXB; k_scan<.., GT>)
     uint32_t* done;           // k_pair: every non-step workgroup counts itself in here when done
+    unsigned long long* wgt;  // diagnostic (KB_WGT): per scan workgroup {start, scored, record written}
     int pred;                 // 1 (k_pair only): scanning workgroups fold their record's minima,
                               //    counts and predicate mask into their arrival line (PRED_*)
     int dyn_lds;              // the launch's dynamic LDS bytes (the eager refolds' buffer)
