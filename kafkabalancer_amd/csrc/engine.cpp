@@ -693,8 +693,8 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
     e->own_st = true;
     if (const char* v = getenv("KB_WGT")) {                 // diagnostic: scan workgroup timeline
         e->wgt_path = v;
-        HIPCHK(dalloc(&e->wgt, 3 * (size_t)std::max<int64_t>(e->nscan, 1)));
-        HIPCHK(hipMemset(e->wgt, 0, 3 * (size_t)std::max<int64_t>(e->nscan, 1) * 8));
+        HIPCHK(dalloc(&e->wgt, 6 * (size_t)std::max<int64_t>(e->nscan, 1)));
+        HIPCHK(hipMemset(e->wgt, 0, 6 * (size_t)std::max<int64_t>(e->nscan, 1) * 8));
     }
     HIPCHK(dalloc(&e->w, e->Ppad));
     HIPCHK(dalloc(&e->meta, e->Ppad));
@@ -1796,7 +1796,7 @@ extern "C" void kb_engine_destroy(kb_engine* e) {
     if (e->wgt) {
         // diagnostic (KB_WGT=path): the last scan launch's {start, scored, record written}
         // per workgroup (100 MHz device clock), appended as one JSON line
-        std::vector<unsigned long long> h(3 * (size_t)std::max<int64_t>(e->nscan, 1));
+        std::vector<unsigned long long> h(6 * (size_t)std::max<int64_t>(e->nscan, 1));
         hipStreamSynchronize(e->st);
         hipMemcpy(h.data(), e->wgt, h.size() * 8, hipMemcpyDeviceToHost);
         if (FILE* f = fopen(e->wgt_path.c_str(), "a")) {

@@ -670,18 +670,37 @@ __device__ void walk_targets(const ScanArgs& a, const Dedup& T, RF s_rf, PS s_po
         if (d > g + 8.0 * eps) return;
     }
     if (nl < KR || last < 0) return;              // the set is exhausted
-    const uint64_t* sb = a.setbits + (size_t)set * a.W64;
-    for (int k = s_pos[last] + 1; k < nblm; k++) {   // rare: more than KR near-tied targets
-        KB_COUNT_WALK(a.ctl, 27, 1);
-        const int b = s_blm[k];
-        if (!setbit(sb, b)) continue;
-        bool isrep = false;
+    // rare: more than KR near-tied targets -- the walk goes on in bl order through the set's
+    // membership words in memory, LA positions per round trip (their broker ids, then their
+    // words, all in flight together): a set of 64 in 1000 brokers has a member every ~16
+    // positions, and one position per dependent load made the few census workgroups that get
+    // here the scan's last by ~2.5 us at c3
+    // (32-bit halves of the words: the walk is inlined in the scoring loop, whose registers
+    // it shares -- four positions of 64-bit words made every scan workgroup slower)
+    const uint32_t* sb = (const uint32_t*)(a.setbits + (size_t)set * a.W64);
+    constexpr int LA = 4;
+    for (int k0 = s_pos[last] + 1; k0 < nblm; k0 += LA) {
+        int bq[LA];
+        uint32_t wq[LA];
 #pragma unroll
-        for (int q = 0; q < RC; q++) isrep |= (q < nrep) && ((int)reps[q] == b);
-        if (isrep) continue;
-        const double d = ds + dtgt_f(s_rf[b], delta);
-        if (d <= g + 4.0 * eps) emit(a, T, kind, src, b, w, ib | (unsigned long long)k);
-        if (d > g + 8.0 * eps) return;
+        for (int q = 0; q < LA; q++) bq[q] = s_blm[k0 + q < nblm ? k0 + q : k0];
+#pragma unroll
+        for (int q = 0; q < LA; q++) wq[q] = sb[bq[q] >> 5];
+#pragma unroll
+        for (int q = 0; q < LA; q++) {
+            const int k = k0 + q;
+            if (k >= nblm) return;
+            KB_COUNT_WALK(a.ctl, 27, 1);
+            const int b = bq[q];
+            if (!((wq[q] >> (b & 31)) & 1u)) continue;
+            bool isrep = false;
+#pragma unroll
+            for (int x = 0; x < RC; x++) isrep |= (x < nrep) && ((int)reps[x] == b);
+            if (isrep) continue;
+            const double d = ds + dtgt_f(s_rf[b], delta);
+            if (d <= g + 4.0 * eps) emit(a, T, kind, src, b, w, ib | (unsigned long long)k);
+            if (d > g + 8.0 * eps) return;
+        }
     }
 }
 
@@ -839,6 +858,8 @@ __device__ __forceinline__ void scan_round(const ScanArgs& a, const ScanParams& 
     if (tid == 0) s_nk = 0;
     if (tid < 2) { s_benc[tid] = NONE64; s_bslot[tid] = NONE32; s_nkk[tid] = 0; }
     if (tid < 2 * NW) (&s_bke[0][0])[tid] = NONE64;
+    __shared__ unsigned long long s_cz[3];           // diagnostic (a.wgt): census clocks, waves, walk clocks
+    if (tid < 3) s_cz[tid] = 0;
     const bool run = q.run != 0;
     const double inv_avg = q.inv_avg, eps = q.eps;
     const double ubL = q.ubL, ubN = q.ubN;
@@ -966,6 +987,9 @@ __device__ __forceinline__ void scan_round(const ScanArgs& a, const ScanParams& 
         }
         // branch-free: every lane scores both partitions; invalid ones are masked
         const uint32_t bmax = (uint32_t)(a.B - 1);
+        // (BK plans: the lane's argmin per kind, (target << 8) | (j << 4) | slot, for the wave's
+        // bound key below -- two registers, in the BK instantiation only)
+        uint32_t amL = 0, amN = 0;
 #pragma unroll
         for (int j = 0; j < PER_LANE; j++) {
             const uint32_t m = P.mt(j);
@@ -982,13 +1006,17 @@ __device__ __forceinline__ void scan_round(const ScanArgs& a, const ScanParams& 
             const uint32_t r0 = min(reps[0], bmax);   // table index even where the slot is unused
             if (a.allow_leader) {
                 const double d = dsrc_f(s_rf[r0], delta) + dt;
-                lL = ok && d < lL ? d : lL;
+                const bool bt = ok && d < lL;
+                lL = bt ? d : lL;
+                if constexpr (BK) amL = bt ? (((uint32_t)tb0 << 8) | ((uint32_t)j << 4)) : amL;
                 cl += ne;
             }
 #pragma unroll
             for (int k = 1; k < RC; k++) {
                 const double d = dsrc_f(s_rf[k < nrep ? reps[k] : r0], delta) + dt;
-                lN = ok && k < nrep && d < lN ? d : lN;
+                const bool bt = ok && k < nrep && d < lN;
+                lN = bt ? d : lN;
+                if constexpr (BK) amN = bt ? (((uint32_t)tb0 << 8) | ((uint32_t)j << 4) | (uint32_t)k) : amN;
             }
             cn += ne * (uint32_t)(nrep - 1);
         }
@@ -1013,9 +1041,9 @@ __device__ __forceinline__ void scan_round(const ScanArgs& a, const ScanParams& 
         // step's minimum, most often just the winning move -- no key survived the move and
         // the bound went open on every step (c3nl: 4000 of 5400 waves walked their targets,
         // 0.47 ms/step).  The record's minimum and key list stay the census waves' (k_step's
-        // windows); this key only bounds.  (The lane holding the wave minimum finds its
-        // (partition, slot) again by re-scoring its two partitions, the same arithmetic, rather
-        // than the scoring loop carrying an argmin in registers for every lane.)
+        // windows); this key only bounds.  (The scoring loop carries each lane's argmin in two
+        // registers, in this instantiation only; re-scoring the lane's two partitions to find
+        // it again cost every scored wave of a c3nl scan ~1 us per unit.)
         if (bk_on) {
             const bool needL = !hasL && a.allow_leader && __ballot(lL < HUGE_VAL);
             const bool needN = !hasN && __ballot(lN < HUGE_VAL);
@@ -1023,28 +1051,28 @@ __device__ __forceinline__ void scan_round(const ScanArgs& a, const ScanParams& 
             const unsigned long long bl = needL ? __ballot(lL == wL) : 0ull, bn = needN ? __ballot(lN == wN) : 0ull;
             const bool myL = bl && lane == __ffsll((long long)bl) - 1, myN = bn && lane == __ffsll((long long)bn) - 1;
             if ((myL && enc(wL) < s_bke[0][wid]) || (myN && enc(wN) < s_bke[1][wid])) {
-                for (int j = 0; j < PER_LANE; j++) {
-                    const uint32_t m = P.mt(j);
-                    const int nrep = (int)meta_nrep(m);
-                    uint32_t reps[RC];
-                    for (int k = 0; k < RC; k++) reps[k] = P.rp(k, j);
-                    int nelig;
-                    const int tb0 = first_target<RC, LSETS>(a, s_set, set_of<RC, LSETS>(P, j), reps, nrep, &nelig);
-                    if (!(base + j < a.shard_end && meta_elig(m) && nrep > 0 && tb0 >= 0)) continue;
-                    const double delta = P.wt(j) * inv_avg;
-                    const double dt = dtgt_f(s_rf[tb0], delta);
-                    for (int k = 0; k < nrep && k < RC; k++) {
-                        const int kind = k ? 1 : 0;
-                        if (!(kind ? myN : myL)) continue;
-                        const double d = dsrc_f(s_rf[reps[k]], delta) + dt;
-                        const unsigned long long e = enc(d);
-                        if (d != (kind ? wN : wL) || !(e < s_bke[kind][wid])) continue;
-                        Contender c;
-                        c.s = (int)reps[k]; c.t = tb0; c.w = P.wt(j); c.kind = kind; c.pad = 0;
-                        c.iter = ((unsigned long long)(base + j) << 21) | ((unsigned long long)k << 16) |
-                                 (unsigned long long)s_pos[tb0];
-                        s_bke[kind][wid] = e; s_bkc[kind][wid] = c;
+                // (the lane's argmin from the scoring loop: the first (partition, slot) in
+                // scoring order with the wave minimum, as a re-scoring would find it)
+#pragma unroll
+                for (int kind = 0; kind < 2; kind++) {
+                    if (!(kind ? myN : myL)) continue;
+                    const unsigned long long e = enc(kind ? wN : wL);
+                    if (!(e < s_bke[kind][wid])) continue;
+                    const uint32_t am = kind ? amN : amL;
+                    const int tb = (int)(am >> 8), jm = (int)((am >> 4) & 15u), km = (int)(am & 15u);
+                    uint32_t src = 0;
+                    double wj = 0.0;
+#pragma unroll
+                    for (int jj = 0; jj < PER_LANE; jj++) {
+                        if (jj == jm) wj = P.wt(jj);
+#pragma unroll
+                        for (int kk = 0; kk < RC; kk++) if (jj == jm && kk == km) src = P.rp(kk, jj);
                     }
+                    Contender c;
+                    c.s = (int)src; c.t = tb; c.w = wj; c.kind = kind; c.pad = 0;
+                    c.iter = ((unsigned long long)(base + jm) << 21) | ((unsigned long long)km << 16) |
+                             (unsigned long long)s_pos[tb];
+                    s_bke[kind][wid] = e; s_bkc[kind][wid] = c;
                 }
             }
         }
@@ -1055,6 +1083,7 @@ __device__ __forceinline__ void scan_round(const ScanArgs& a, const ScanParams& 
         }
 #endif
         if (!census_off && ((hasL && lL <= tL + 8.0 * eps) || (hasN && lN <= tN + 8.0 * eps))) {
+            const unsigned long long cz0 = a.wgt ? clock64() : 0ull;
             // the (partition, slot) pairs within 8*eps of the wave minimum, as bits j*16 + slot
             uint32_t todo = 0;
 #pragma unroll
@@ -1077,6 +1106,7 @@ __device__ __forceinline__ void scan_round(const ScanArgs& a, const ScanParams& 
                     if (hasN && k < nrep && dsrc_f(s_rf[reps[k]], delta) + dt <= tN + 8.0 * eps)
                         todo |= 1u << (j * 16 + k);
             }
+            const unsigned long long cz1 = a.wgt ? clock64() : 0ull;
             // one walk call site (a compact, rarely executed code path)
             while (todo) {
                 const int bit = __ffs(todo) - 1;
@@ -1096,6 +1126,10 @@ __device__ __forceinline__ void scan_round(const ScanArgs& a, const ScanParams& 
                 const double ds = dsrc_f(s_rf[src], w * inv_avg);
                 walk_targets<RC>(a, T, s_rf, s_pos, s_blm, R, k ? 1 : 0, base + j, k, (int)src, reps, nrep,
                                       set, w, ds, k ? tN : tL, eps, inv_avg, nblm);
+            }
+            if (a.wgt && lane == __ffsll((long long)__ballot(1)) - 1) {   // (the census lanes' first)
+                const unsigned long long cz2 = clock64();
+                atomicAdd(&s_cz[0], cz2 - cz0); atomicAdd(&s_cz[1], 1ull); atomicAdd(&s_cz[2], cz2 - cz1);
             }
         }
         wgL = tL < wgL ? tL : wgL;
@@ -1247,7 +1281,10 @@ __device__ __forceinline__ void scan_round(const ScanArgs& a, const ScanParams& 
             else { r.best[k].s = r.best[k].t = -1; r.best[k].w = 0.0; r.best[k].iter = NONE64; r.best[k].kind = k; r.best[k].pad = 0; }
         }
         stobj_wt(hdr, r);
-        if (a.wgt) { a.wgt[3 * wg] = t_in; a.wgt[3 * wg + 1] = t_sc; a.wgt[3 * wg + 2] = wall_clock64(); }
+        if (a.wgt) {
+            unsigned long long* o = a.wgt + 6 * wg;
+            o[0] = t_in; o[1] = t_sc; o[2] = wall_clock64(); o[3] = s_cz[0]; o[4] = s_cz[1]; o[5] = s_cz[2];
+        }
         if (a.pred) {
             // k_pair: the record's minima, counts and predicate mask folded into this
             // workgroup's arrival line (performed at L2 before the arrival add: the step

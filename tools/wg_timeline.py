@@ -32,8 +32,9 @@ def main():
     assert err is None, err
     eng.close()
     x = [json.loads(ln) for ln in open(path)][-1]
-    t = np.array(x["wg"], dtype=np.int64).reshape(-1, 3)
-    t = t[t[:, 0] > 0]
+    t6 = np.array(x["wg"], dtype=np.int64).reshape(-1, 6)
+    t6 = t6[t6[:, 0] > 0]
+    t = t6[:, :3]
     t0 = t[:, 0].min()
     us = (t - t0) / 100.0
     q = lambda v: [round(float(np.percentile(v, p)), 2) for p in (0, 10, 50, 90, 100)]
@@ -42,6 +43,14 @@ def main():
            "scored_us": q(us[:, 1]), "end_us": q(us[:, 2]),
            "dur_start_to_scored_us": q(us[:, 1] - us[:, 0]),
            "dur_scored_to_end_us": q(us[:, 2] - us[:, 1])}
+    idx = np.nonzero(np.array(x["wg"], dtype=np.int64).reshape(-1, 6)[:, 0] > 0)[0]
+    slow = np.argsort(-(us[:, 1] - us[:, 0]))[:6]
+    out["slowest"] = [[int(idx[i]), round(float(us[i, 0]), 2), round(float(us[i, 1]), 2), round(float(us[i, 2]), 2),
+                       int(t6[i, 3]), int(t6[i, 4]), int(t6[i, 5])] for i in slow]
+    out["slowest_def"] = "[wg, start, scored, end (us), census shader clocks summed over its waves, census waves, walk clocks]"
+    out["census_wgs"] = int((t6[:, 4] > 0).sum())
+    late = np.argsort(-us[:, 2])[:6]
+    out["latest_end"] = [[int(idx[i]), round(float(us[i, 0]), 2), round(float(us[i, 1]), 2), round(float(us[i, 2]), 2)] for i in late]
     print(json.dumps(out))
 
 
