@@ -148,6 +148,7 @@ struct kb_engine {
     int batch = 64;                // (scan, step) pairs per enqueued batch (adaptive, run_steps)
     int sum_keys = SUMMARY_KEYS;   // near-tie keys per rank summary (grown on overflow)
     bool ub_mode = false;          // a step re-scanned: enqueue the conditional bound pass per scan
+    bool ub_sticky = true;         // (diagnostic KB_UB_STICKY=0: a retry does not turn ub_mode on)
     uint32_t list_slack = 1024;        // free entries per broker list (doubled on every re-layout)
     int64_t relists = 0;
     const void* gath = nullptr;        // the last gathered rank summaries (device) and their count
@@ -817,10 +818,15 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
     HIPCHK(hipEventCreate(&e->ev0));
     HIPCHK(hipEventCreate(&e->ev1));
     e->scan_bytes = (e->shard_end - e->shard_begin) * (int64_t)(8 + 4 + 2 * e->rc_dev);
-    // thousands of brokers: a move rarely leaves a best key whose brokers it did not
-    // touch, so the next step's census bound is open; the conditional bound pass runs
-    // from the first step (else the second step's census spills once, ~1 s at c5)
-    e->ub_mode = e->B >= 2048;
+    // thousands of brokers with -allow-leader: a move rarely leaves a best key whose brokers
+    // it did not touch, so the next step's census bound is open; the conditional bound pass
+    // runs from the first step (else the second step's census spills once, ~1 s at c5 in
+    // round 2).  Plans without -allow-leader carry every scored wave's bound key (BK), which
+    // keeps the bound closed: there the pass waits for a first retry (c5: none in 200 steps,
+    // 0.1006 -> 0.0962 ms/step without the pass's two launches per step)
+    e->ub_mode = e->B >= 2048 && e->allow_leader;
+    if (const char* v = getenv("KB_UB_MODE")) e->ub_mode = *v == '1';                      // diagnostic
+    if (const char* v = getenv("KB_UB_STICKY")) e->ub_sticky = *v != '0';                   // diagnostic
     *out = e;
     return KB_OK;
 }
@@ -1350,7 +1356,7 @@ static int run_steps(kb_engine* e, int64_t max_steps) {
         reuse = false;
         harvest(e);
         const DevCtl& c = *e->h_ctl;
-        if (c.total_retries > 0) e->ub_mode = true;
+        if (c.total_retries > 0 && e->ub_sticky) e->ub_mode = true;
         // adaptive batch: the pairs enqueued behind a halted step run as no-ops (a launch
         // each), so after a halt the next batch is about twice the steps that ran before
         // it; full batches double it again, up to kStepBatch
