@@ -37,6 +37,14 @@
 #include "kernels_api.h"
 #include "wave_ops.h"
 
+// The file builds as several translation units compiled in parallel (Makefile: -DKB_TU=0..10,
+// each instantiating one group of kernels and their launch helpers); without KB_TU it is
+// one unit holding everything.
+#ifndef KB_TU
+#define KB_TU (-1)
+#endif
+#define KB_IN_TU(n) (KB_TU < 0 || KB_TU == (n))
+
 namespace kbe {
 
 // --------------------------------------------------------------- helpers
@@ -3704,10 +3712,12 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_pair(ScanArgs a, StepArgs sa) 
 
 // ------------------------------------------------------------- k_listop
 
+#if KB_IN_TU(0)
 __global__ __launch_bounds__(1024) void k_listop(DevCtl* ctl, Lists L) {
     __shared__ int s_i;
     do_list_op(ctl, L, &s_i);
 }
+#endif
 
 // ------------------------------------------------------------ k_refresh
 // exact partition-ordered refold (getBrokerLoad, utils.go:92-105) of every
@@ -3715,7 +3725,7 @@ __global__ __launch_bounds__(1024) void k_listop(DevCtl* ctl, Lists L) {
 // folded sequentially by one lane.
 
 constexpr int REFRESH_THREADS = 256;
-constexpr int REFRESH_CHUNK = 1024;
+[[maybe_unused]] constexpr int REFRESH_CHUNK = 1024;
 // The exact getBrokerLoad fold (utils.go:92-105) of broker b's contributions in partition
 // order by one workgroup of NT threads (every thread calls; the result is wave 0's).
 // Double-buffered: while wave 0 folds chunk j (a broadcast-LDS add chain), waves 1..
@@ -3785,12 +3795,14 @@ __device__ __forceinline__ double refold_broker(const RefreshArgs& a, int b, dou
 }
 
 // One workgroup per dirty broker (the host's refresh after a batch halted for exact loads)
+#if KB_IN_TU(0)
 __global__ __launch_bounds__(REFRESH_THREADS) void k_refresh(RefreshArgs a) {
     const int b = blockIdx.x;
     if (b >= a.B || !(a.bfl[b] & BF_DIRTY)) return;
     __shared__ __align__(16) double s_c[2 * REFRESH_CHUNK];
     refold_broker<REFRESH_THREADS, REFRESH_CHUNK>(a, b, s_c);
 }
+#endif
 
 // The same refresh inside the stream: the first scan launch of the pair after a k_step
 // that halted for exact loads (ScanArgs.rfpass) refolds the dirty brokers instead of
@@ -4132,12 +4144,14 @@ __device__ __forceinline__ void summary_body(const SumArgs& a, double* s_r, bool
     }
 }
 
+#if KB_IN_TU(0)
 __global__ __launch_bounds__(1024) void k_summary(SumArgs a) {
     // (r in LDS up to SUM_RLDS brokers; past that, the keys are re-scored from memory)
     extern __shared__ __align__(16) double sum_dyn[];
     if (a.B <= SUM_RLDS) summary_body(a, sum_dyn, false);
     else summary_body(a, const_cast<double*>(a.r), true);
 }
+#endif
 
 // The scan and the rank summary in one launch (sharded engines): the scan's grid plus one
 // resident summary workgroup, the last of the grid, which waits for the others' arrivals
@@ -4203,55 +4217,77 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scansum(ScanArgs a, SumArgs sa
 }
 
 // ------------------------------------------------------- launch helpers
+// (compiled as several translation units, KB_TU = 0..10, in parallel: Makefile)
 
-template <int RC>
-static void launch_scan_rc(const ScanArgs& a, bool lds_sets, size_t lds, hipStream_t st) {
-    const int grid = a.nscan + (a.listwg ? 1 : 0) + a.eager;
-    // (incremental mode: with the set records in LDS only; engine.cpp gates it.  Broker
-    // tables in memory (a.gt, B > MAXB): set records in memory too)
-    if (a.gt) hipLaunchKernelGGL((k_scan<RC, false, false, true>), dim3(grid), dim3(SCAN_THREADS), lds, st, a);
-    else if (lds_sets && a.incr) hipLaunchKernelGGL((k_scan<RC, true, true>), dim3(grid), dim3(SCAN_THREADS), lds, st, a);
-    else if (lds_sets) hipLaunchKernelGGL((k_scan<RC, true, false>), dim3(grid), dim3(SCAN_THREADS), lds, st, a);
-    else hipLaunchKernelGGL((k_scan<RC, false, false>), dim3(grid), dim3(SCAN_THREADS), lds, st, a);
-}
+// (the scan's instantiations per slot count spread over TUs 1, 8, 9, 10)
+#define KB_SCAN_TU(RC)                                                                                    \
+    void launch_scan_##RC(const ScanArgs& a, bool lds_sets, size_t lds, hipStream_t st) {                \
+        const int grid = a.nscan + (a.listwg ? 1 : 0) + a.eager;                                         \
+        /* (incremental mode: with the set records in LDS only; engine.cpp gates it.  Broker           \
+           tables in memory (a.gt, B > MAXB): set records in memory too) */                              \
+        if (a.gt) hipLaunchKernelGGL((k_scan<RC, false, false, true>), dim3(grid), dim3(SCAN_THREADS), lds, st, a); \
+        else if (lds_sets && a.incr) hipLaunchKernelGGL((k_scan<RC, true, true>), dim3(grid), dim3(SCAN_THREADS), lds, st, a); \
+        else if (lds_sets) hipLaunchKernelGGL((k_scan<RC, true, false>), dim3(grid), dim3(SCAN_THREADS), lds, st, a); \
+        else hipLaunchKernelGGL((k_scan<RC, false, false>), dim3(grid), dim3(SCAN_THREADS), lds, st, a);  \
+    }                                                                                                     \
+    int scan_occ_##RC(bool lds_sets, bool gt, size_t lds) {                                              \
+        int n = 0, m = 0;                                                                                 \
+        if (gt) hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_scan<RC, false, false, true>, SCAN_THREADS, lds); \
+        else if (lds_sets) {                                                                              \
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_scan<RC, true, false>, SCAN_THREADS, lds); \
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&m, k_scan<RC, true, true>, SCAN_THREADS, lds);  \
+            n = n < m ? n : m;                                                                            \
+        } else hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_scan<RC, false, false>, SCAN_THREADS, lds); \
+        return n;                                                                                         \
+    }
+#if KB_IN_TU(1)
+KB_SCAN_TU(1) KB_SCAN_TU(2) KB_SCAN_TU(3)
+#endif
+#if KB_IN_TU(8)
+KB_SCAN_TU(4) KB_SCAN_TU(6)
+#endif
+#if KB_IN_TU(9)
+KB_SCAN_TU(8) KB_SCAN_TU(12)
+#endif
+#if KB_IN_TU(10)
+KB_SCAN_TU(16)
+#endif
+#undef KB_SCAN_TU
 
+#if KB_IN_TU(0)
+#define KB_SCAN_DECL(RC)                                                                                  \
+    void launch_scan_##RC(const ScanArgs& a, bool lds_sets, size_t lds, hipStream_t st);                \
+    int scan_occ_##RC(bool lds_sets, bool gt, size_t lds);
+KB_SCAN_DECL(1) KB_SCAN_DECL(2) KB_SCAN_DECL(3) KB_SCAN_DECL(4) KB_SCAN_DECL(6) KB_SCAN_DECL(8)
+KB_SCAN_DECL(12) KB_SCAN_DECL(16)
+#undef KB_SCAN_DECL
 void launch_scan(const ScanArgs& a, int rc, bool lds_sets, size_t lds, hipStream_t st) {
     switch (rc) {
-        case 1: launch_scan_rc<1>(a, lds_sets, lds, st); break;
-        case 2: launch_scan_rc<2>(a, lds_sets, lds, st); break;
-        case 3: launch_scan_rc<3>(a, lds_sets, lds, st); break;
-        case 4: launch_scan_rc<4>(a, lds_sets, lds, st); break;
-        case 6: launch_scan_rc<6>(a, lds_sets, lds, st); break;
-        case 8: launch_scan_rc<8>(a, lds_sets, lds, st); break;
-        case 12: launch_scan_rc<12>(a, lds_sets, lds, st); break;
-        default: launch_scan_rc<16>(a, lds_sets, lds, st); break;
+        case 1: launch_scan_1(a, lds_sets, lds, st); break;
+        case 2: launch_scan_2(a, lds_sets, lds, st); break;
+        case 3: launch_scan_3(a, lds_sets, lds, st); break;
+        case 4: launch_scan_4(a, lds_sets, lds, st); break;
+        case 6: launch_scan_6(a, lds_sets, lds, st); break;
+        case 8: launch_scan_8(a, lds_sets, lds, st); break;
+        case 12: launch_scan_12(a, lds_sets, lds, st); break;
+        default: launch_scan_16(a, lds_sets, lds, st); break;
     }
 }
-template <int RC>
-static int scan_occ_rc(bool lds_sets, bool gt, size_t lds) {
-    int n = 0;
-    int m = 0;
-    if (gt) hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_scan<RC, false, false, true>, SCAN_THREADS, lds);
-    else if (lds_sets) {
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_scan<RC, true, false>, SCAN_THREADS, lds);
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&m, k_scan<RC, true, true>, SCAN_THREADS, lds);
-        n = n < m ? n : m;
-    } else hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_scan<RC, false, false>, SCAN_THREADS, lds);
-    return n;
-}
-
 int scan_blocks_per_cu(int rc, bool lds_sets, bool gt, size_t lds) {
     switch (rc) {
-        case 1: return scan_occ_rc<1>(lds_sets, gt, lds);
-        case 2: return scan_occ_rc<2>(lds_sets, gt, lds);
-        case 3: return scan_occ_rc<3>(lds_sets, gt, lds);
-        case 4: return scan_occ_rc<4>(lds_sets, gt, lds);
-        case 6: return scan_occ_rc<6>(lds_sets, gt, lds);
-        case 8: return scan_occ_rc<8>(lds_sets, gt, lds);
-        case 12: return scan_occ_rc<12>(lds_sets, gt, lds);
-        default: return scan_occ_rc<16>(lds_sets, gt, lds);
+        case 1: return scan_occ_1(lds_sets, gt, lds);
+        case 2: return scan_occ_2(lds_sets, gt, lds);
+        case 3: return scan_occ_3(lds_sets, gt, lds);
+        case 4: return scan_occ_4(lds_sets, gt, lds);
+        case 6: return scan_occ_6(lds_sets, gt, lds);
+        case 8: return scan_occ_8(lds_sets, gt, lds);
+        case 12: return scan_occ_12(lds_sets, gt, lds);
+        default: return scan_occ_16(lds_sets, gt, lds);
     }
 }
+#endif
+
+#if KB_IN_TU(0)
 
 __global__ __launch_bounds__(1024) void k_touch(double* r, int B, int32_t* blm, int32_t* posm, uint4* setrec, int nrec) {
     for (int i = threadIdx.x; i < B; i += 1024) {
@@ -4307,6 +4343,9 @@ void launch_ubinit(DevCtl* ctl, const Recs& R, int allow_leader, hipStream_t st)
 void launch_touch(double* r, int B, int32_t* blm, int32_t* posm, uint4* setrec, int nrec, hipStream_t st) {
     hipLaunchKernelGGL(k_touch, dim3(1), dim3(1024), 0, st, r, B, blm, posm, setrec, nrec);
 }
+#endif
+
+#if KB_IN_TU(2)
 
 int step_static_lds(bool gb) {
     hipFuncAttributes fa, fb;
@@ -4326,52 +4365,64 @@ void launch_step(const StepArgs& a, hipStream_t st) {
     else
         hipLaunchKernelGGL(k_step<false>, dim3(1), dim3(STEP_THREADS), a.lds_bytes, st, a);
 }
-// the fused pair (k_pair) for the device slot counts of the common replication factors
-bool pair_supported(int rc) { return rc == 3 || rc == 4; }
+#endif
 
-template <int RC, bool BK>
-static int pair_attr1(bool lds_sets, size_t lds, int* static_lds) {
-    hipFuncAttributes fa;
-    const void* f = lds_sets ? (const void*)k_pair<RC, true, BK> : (const void*)k_pair<RC, false, BK>;
-    if (hipFuncGetAttributes(&fa, f) != hipSuccess) return -1;
-    *static_lds = (int)fa.sharedSizeBytes;
-    int n = 0;
-    if (lds_sets) hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_pair<RC, true, BK>, SCAN_THREADS, lds);
-    else hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_pair<RC, false, BK>, SCAN_THREADS, lds);
-    return n;
-}
+// the fused pair (k_pair) for the device slot counts of the common replication factors
+// (one translation unit per (slot count, bound keys): TUs 3 / 6 for RC = 3 without / with
+// bound keys, 4 / 7 for RC = 4)
+#define KB_PAIR_TU(R, BKV, NAME)                                                                      \
+    int pair_attr_##NAME(bool lds_sets, size_t lds, int* static_lds) {                               \
+        hipFuncAttributes fa;                                                                          \
+        const void* f = lds_sets ? (const void*)k_pair<R, true, BKV> : (const void*)k_pair<R, false, BKV>; \
+        if (hipFuncGetAttributes(&fa, f) != hipSuccess) return -1;                                   \
+        *static_lds = (int)fa.sharedSizeBytes;                                                         \
+        int n = 0;                                                                                     \
+        if (lds_sets) hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_pair<R, true, BKV>, SCAN_THREADS, lds);  \
+        else hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_pair<R, false, BKV>, SCAN_THREADS, lds);          \
+        return n;                                                                                      \
+    }                                                                                                  \
+    void launch_pair_##NAME(const ScanArgs& a, const StepArgs& sa, bool lds_sets, size_t lds, hipStream_t st) { \
+        const int grid = a.nscan + (a.listwg ? 1 : 0) + a.eager + 1;                                 \
+        if (lds_sets) hipLaunchKernelGGL((k_pair<R, true, BKV>), dim3(grid), dim3(SCAN_THREADS), lds, st, a, sa); \
+        else hipLaunchKernelGGL((k_pair<R, false, BKV>), dim3(grid), dim3(SCAN_THREADS), lds, st, a, sa);         \
+    }
+#if KB_IN_TU(3)
+KB_PAIR_TU(3, false, 3n)
+#endif
+#if KB_IN_TU(6)
+KB_PAIR_TU(3, true, 3b)
+#endif
+#if KB_IN_TU(4)
+KB_PAIR_TU(4, false, 4n)
+#endif
+#if KB_IN_TU(7)
+KB_PAIR_TU(4, true, 4b)
+#endif
+#undef KB_PAIR_TU
+
+#if KB_IN_TU(0)
+#define KB_PAIR_DECL(NAME)                                                                             \
+    int pair_attr_##NAME(bool lds_sets, size_t lds, int* static_lds);                                \
+    void launch_pair_##NAME(const ScanArgs& a, const StepArgs& sa, bool lds_sets, size_t lds, hipStream_t st);
+KB_PAIR_DECL(3n) KB_PAIR_DECL(3b) KB_PAIR_DECL(4n) KB_PAIR_DECL(4b)
+#undef KB_PAIR_DECL
+bool pair_supported(int rc) { return rc == 3 || rc == 4; }
 // (both instantiations: the grid is sized so every workgroup is resident in either)
-template <int RC>
-static int pair_attr(bool lds_sets, size_t lds, int* static_lds) {
+int pair_blocks_per_cu(int rc, bool lds_sets, size_t lds, int* static_lds) {
+    if (rc != 3 && rc != 4) return -1;
     int s0 = 0, s1 = 0;
-    const int n0 = pair_attr1<RC, false>(lds_sets, lds, &s0), n1 = pair_attr1<RC, true>(lds_sets, lds, &s1);
+    const int n0 = rc == 3 ? pair_attr_3n(lds_sets, lds, &s0) : pair_attr_4n(lds_sets, lds, &s0);
+    const int n1 = rc == 3 ? pair_attr_3b(lds_sets, lds, &s1) : pair_attr_4b(lds_sets, lds, &s1);
     *static_lds = s0 > s1 ? s0 : s1;
     return n0 < n1 ? n0 : n1;
 }
-
-int pair_blocks_per_cu(int rc, bool lds_sets, size_t lds, int* static_lds) {
-    if (rc == 3) return pair_attr<3>(lds_sets, lds, static_lds);
-    if (rc == 4) return pair_attr<4>(lds_sets, lds, static_lds);
-    return -1;
-}
-
 void launch_pair(const ScanArgs& a, const StepArgs& sa, int rc, bool lds_sets, size_t lds, hipStream_t st) {
-    const int grid = a.nscan + (a.listwg ? 1 : 0) + a.eager + 1;
     // bound keys for plans without -allow-leader: there every step moves another partition
     // and the census waves' keys rarely outlive it (the -allow-leader headline keeps the
     // instantiation without them: its kernel is unchanged)
     const bool bk = !a.allow_leader;
-#define KB_PAIR_LAUNCH(R, L)                                                                          \
-    do {                                                                                              \
-        if (bk) hipLaunchKernelGGL((k_pair<R, L, true>), dim3(grid), dim3(SCAN_THREADS), lds, st, a, sa);  \
-        else hipLaunchKernelGGL((k_pair<R, L, false>), dim3(grid), dim3(SCAN_THREADS), lds, st, a, sa);    \
-    } while (0)
-    if (rc == 3) {
-        if (lds_sets) KB_PAIR_LAUNCH(3, true); else KB_PAIR_LAUNCH(3, false);
-    } else {
-        if (lds_sets) KB_PAIR_LAUNCH(4, true); else KB_PAIR_LAUNCH(4, false);
-    }
-#undef KB_PAIR_LAUNCH
+    if (rc == 3) { if (bk) launch_pair_3b(a, sa, lds_sets, lds, st); else launch_pair_3n(a, sa, lds_sets, lds, st); }
+    else { if (bk) launch_pair_4b(a, sa, lds_sets, lds, st); else launch_pair_4n(a, sa, lds_sets, lds, st); }
 }
 
 void launch_listop(DevCtl* ctl, const Lists& L, hipStream_t st) {
@@ -4383,6 +4434,9 @@ void launch_refresh(const RefreshArgs& a, hipStream_t st) {
 void launch_summary(const SumArgs& a, hipStream_t st) {
     hipLaunchKernelGGL(k_summary, dim3(1), dim3(1024), a.B <= SUM_RLDS ? (size_t)a.B * 8 : 0, st, a);
 }
+#endif
+
+#if KB_IN_TU(5)
 
 template <int RC, bool LSETS, bool BK>
 static int scansum_attr1(size_t lds, int* static_lds) {
@@ -4420,6 +4474,9 @@ void launch_scansum(const ScanArgs& a, const SumArgs& sa, int rc, bool lds_sets,
     }
 #undef KB_SCANSUM_LAUNCH
 }
+#endif
+
+#if KB_IN_TU(0)
 
 // Control-block / step-log transfers between the device and the host's pinned
 // (fine-grained, mapped) mirror as one small kernel on the engine's stream instead of
@@ -4442,5 +4499,6 @@ __global__ void __launch_bounds__(256) k_xfer(XferArgs a) {
 void launch_xfer(const XferArgs& a, hipStream_t st) {
     hipLaunchKernelGGL(k_xfer, dim3(1), dim3(256), 0, st, a);
 }
+#endif
 
 }  // namespace kbe
