@@ -9,7 +9,8 @@ over the timed steps, per wall second.
 
 Roofline: the dominant kernel is the launch that streams the partitions --
 k_pair (the scan's grid and the step workgroup in one launch per step) where the engine
-fuses the pair, else k_scan; `achieved` = the scan's algorithmic bytes per launch / that
+fuses the pair, else k_scan; `achieved` = SURVEY 8(d)'s algorithmic bytes of a step (26.0 MB
+at c3; the engine's own 18-B-per-partition layout is a side figure) / that
 launch's average in-plan duration, measured live on the engine's stream with the device
 clock: each launch's span from the end of the launch before it to its own end (dispatch
 included: the interval rocprofv3 --kernel-trace reports, so the committed
@@ -20,9 +21,14 @@ workgroup start to last end) and the whole-step fraction
 `frac_step` (SURVEY 8(d) bytes per step / ms_per_step / 8 TB/s) are reported beside it.  `traffic` is the rocprofv3 PMC figure for the same workload
 (profiles/pmc_traffic.json, keyed by workload, stamped with the git head it ran on).
 
+c3 lines carry a `secondary` entry: c3nl (the same cluster without -allow-leader, whose plan
+moves a different partition almost every step, unlike c3's leader 2-cycle), same steps,
+warm-up and timing method, no CPU leg (--no-secondary leaves it out).
+
 Multi-GPU: under torch.distributed.run (WORLD_SIZE set) kafkabalancer_amd.dist.bench_main;
-`--gpus N` without a launcher starts N ranks itself (spawn_ranks).  c5: a fixed 10M
-partitions sharded N ways, strong scaling; other workloads weak by default.
+`--gpus N` without a launcher starts N ranks itself (spawn_ranks).  Strong scaling by
+default: the workload's one cluster (c3: 1M x 1000) sharded N ways, so every N runs the same
+plan; --scaling weak gives every rank a full cluster.
 """
 import argparse
 import json
@@ -161,9 +167,16 @@ def cpu_baseline(cl, cfg, desc, plan_cand_per_step, seconds=12.0):
                 break
             steps += 1
         dt = time.perf_counter() - t0
-        out["optimised_cpu"] = {"value": (ce.candidates() - c0) / dt, "unit": "candidates/s",
+        val = (ce.candidates() - c0) / dt
+        out["optimised_cpu"] = {"value": val, "unit": "candidates/s",
                                 "ms_per_step": 1e3 * dt / max(steps, 1), "cores": threads, "steps": steps,
                                 "cores_available": avail,
+                                # (the GPU pool's boxes give a job OMP_NUM_THREADS = 16 of the host's
+                                # cores and ask that pools stay within it: the all-cores figure is the
+                                # linear extrapolation, an upper bound, not a measurement)
+                                "all_cores_value_extrapolated": val * max(avail, threads) / threads,
+                                "all_cores_ms_per_step_extrapolated": 1e3 * dt / max(steps, 1) * threads / max(avail, threads),
+                                "all_cores_def": "value x cores_available / cores (linear scaling: an upper bound)",
                                 "cores_source": "OMP_NUM_THREADS" if os.environ.get("OMP_NUM_THREADS") else "affinity",
                                 "kind": "engine algorithm on the host (tools/cpu_engine, OpenMP)"}
         ce.close()
@@ -334,12 +347,14 @@ def main():
     ap.add_argument("--workload", default="c3")
     ap.add_argument("--scale", type=float, default=1.0)
     ap.add_argument("--scaling", default=None, choices=[None, "weak", "strong"],
-                    help="multi-GPU: weak (every rank adds a full cluster) or strong (one cluster "
-                         "sharded N ways; default for c5)")
+                    help="multi-GPU: strong (the default: one cluster sharded N ways) or weak (every "
+                         "rank adds a full cluster)")
     ap.add_argument("--mode", default="full", choices=["full", "incremental"],
                     help="incremental: SURVEY 8(f3) rescoring mode (scans read only the blocks a "
                          "lower-bound certificate keeps); a separate line, not the full-scan roofline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-secondary", action="store_true",
+                    help="c3: leave out the secondary c3nl line (c3's cluster without -allow-leader)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--isolated-scan", action="store_true",
                     help="also time 200 back-to-back k_scan launches on the final state (kept out of "
@@ -352,6 +367,9 @@ def main():
                     help="what a drop-in user pays: kb_engine_balance per call and the CLI end to end "
                          "(decode / create / plan / encode) on the workload's JSON; a separate line")
     ap.add_argument("--cli-reassign", type=int, default=1000)
+    ap.add_argument("--dist-world1", action="store_true",
+                    help="test: the multi-GPU bench path (dist.bench_main, RCCL unless KB_DIST_BACKEND) "
+                         "under a one-rank torch.distributed.run launch")
     ap.add_argument("--sharded", action="store_true",
                     help="one GPU: the sharded protocol (RCCL all-gather per step, plan driven from C) at "
                          "world size 1 against the plain plan over the same steps; a separate line")
@@ -395,7 +413,7 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    if world > 1 or args.dist_world1:
         from kafkabalancer_amd import dist
         return dist.bench_main(args, world, rank, local, cpu_baseline=cpu_baseline)
     if args.sharded:
@@ -403,11 +421,34 @@ def main():
         return dist.bench_world1(args)
 
     import torch
+    torch.cuda.set_device(0)
+    out = measure(args, args.workload, with_cpu=not args.no_cpu_baseline)
+    if out is None:
+        return
+    # the plan that is not a 2-cycle: c3's cluster without -allow-leader, whose
+    # 1000-step plan moves a different partition almost every step, measured the same way
+    # (same steps and warm-up, no CPU leg) beside the headline
+    if args.workload == "c3" and args.mode == "full" and not args.no_secondary and not args.stamps:
+        sec = measure(args, "c3nl", with_cpu=False)
+        r = sec["roofline"]
+        out["secondary"] = {
+            "workload": "c3nl", "config": sec["config"], "steps": sec["steps"], "warmup": sec["warmup"],
+            "ms_per_step": sec["ms_per_step"], "device_ms_per_step": sec["config"]["device_ms_per_step"],
+            "value": sec["value"], "unit": sec["unit"],
+            "roofline": {k: r[k] for k in ("achieved", "peak", "unit", "frac", "avg_launch_us", "bytes_per_launch",
+                                           "frac_engine_bytes", "scan_phase_us", "frac_step", "traffic")},
+            "kernels_us_per_launch": sec["kernels_us_per_launch"], "engine_events": sec["engine_events"]}
+    print(json.dumps(out))
+
+
+def measure(args, workload, with_cpu):
+    """One single-GPU bench line of `workload` (the timed plan, then the kernel-timing
+    replays): the line's dict, or None for the diagnostic --stamps run (printed here)."""
+    import torch
     from kafkabalancer_amd import engine as E
     from kafkabalancer_amd import synth
-    torch.cuda.set_device(0)
-    cl, cfg, desc = synth.config(args.workload, scale=args.scale)
-    progress("%s: %d partitions built" % (args.workload, cl.n))
+    cl, cfg, desc = synth.config(workload, scale=args.scale)
+    progress("%s: %d partitions built" % (workload, cl.n))
     incr = args.mode == "incremental"
     eng = E.Engine(cl, cfg, device=0, time_kernels=False, incremental=incr)
     if args.warmup:
@@ -446,7 +487,7 @@ def main():
                           "stamps_us_per_step": {k: st[i] / mhz / n for i, k in enumerate(names) if k},
                           "counts_per_step": {k: st[i] / n for k, i in counts.items()},
                           "stats": eng.stats()}))
-        return
+        return None
     eng.close()
     # per-kernel durations, outside the headline timing, over the SAME steps of the plan as
     # the headline: a fresh engine replays the warm-up and the timed steps (the plan is
@@ -513,15 +554,27 @@ def main():
             scan_us = kdc["pair"][0]
             pair_timing = "first workgroup start .. step end"
         achieved = bytes_scan / (scan_us * 1e-6) / 1e9
-    traffic, traffic_git = (None, None) if incr else pmc_traffic(args.workload, kname)
+    traffic, traffic_git = (None, None) if incr else pmc_traffic(workload, kname)
+    # achieved = SURVEY.md 8(d)'s algorithmic bytes of a step (P * (8 w + 4 Rmax rep + 1 nrep +
+    # 1 want + 4 aset) + 12 B + the allowed-set words; early-exit stages to their hit) / the
+    # launch's duration; the engine's own layout (18 B per partition at RF 3) beside it.
+    # (incremental mode: the blocks its scans read, engine layout -- never the full-scan figure)
+    bytes_alg = bytes_scan if incr else b8d / max(steps, 1)
+    achieved = bytes_alg / (scan_us * 1e-6) / 1e9
+    achieved_eng = bytes_scan / (scan_us * 1e-6) / 1e9
     roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
             "kernel": kname + (" (one launch per step: the scan's grid and the step workgroup)" if fused else ""),
-            "bytes_per_launch": bytes_scan,
-            "bytes_per_launch_def": ("engine layout: per partition 8 w + 4 meta + 2*%d rep" % rmax) +
-                                    (" x the blocks the incremental scans read (+16 B per block "
-                                     "descriptor); the full scan reads %d" % st1["scan_bytes"]
-                                     if incr else ""),
+            "bytes_per_launch": bytes_alg,
+            "bytes_per_launch_def": ("SURVEY.md 8(d) algorithmic bytes per step (one launch per step): "
+                                     "P*(8 w + 4*%d rep + 1 nrep + 1 want + 4 aset) + 12 B + nsets*ceil(B/64)*8"
+                                     % rmax) if not incr else
+                                    ("engine layout: per partition 8 w + 4 meta + 2*%d rep x the blocks the "
+                                     "incremental scans read (+16 B per block descriptor); the full scan reads %d"
+                                     % (rmax, st1["scan_bytes"])),
+            "achieved_engine_bytes": achieved_eng, "frac_engine_bytes": achieved_eng / HBM_PEAK_GBS,
+            "engine_bytes_per_launch": bytes_scan,
+            "engine_bytes_def": "the engine's layout: per partition 8 w + 4 meta + 2*%d rep" % rmax,
             "avg_launch_us": scan_us,
             "timing": (("device clock (100 MHz), in-plan launches back to back: the previous launch's end "
                         "to the step workgroup's end (dispatch included, the interval rocprofv3 "
@@ -533,9 +586,9 @@ def main():
                        "--kernel-trace reports), %d launches" % scan_n),
             "avg_launch_us_device_clock": scan_clock_us,
             "device_clock_def": "first scan workgroup start .. last end (no dispatch)",
-            "frac_device_clock": bytes_scan / (scan_clock_us * 1e-6) / 1e9 / HBM_PEAK_GBS,
+            "frac_device_clock": bytes_alg / (scan_clock_us * 1e-6) / 1e9 / HBM_PEAK_GBS,
             "scan_phase_us": scan_phase_us,
-            "scan_phase_frac": bytes_scan / (scan_phase_us * 1e-6) / 1e9 / HBM_PEAK_GBS,
+            "scan_phase_frac": bytes_alg / (scan_phase_us * 1e-6) / 1e9 / HBM_PEAK_GBS,
             "scan_phase_def": "the scan's span alone: the previous step's end to the last scan workgroup's "
                               "end (device clock)",
             "avg_launch_us_events": kev["scan"][0],
@@ -546,11 +599,11 @@ def main():
                                 "GB/s informational)" if early_exit else ""),
             "bytes_8d_per_step": b8d / max(steps, 1),
             "traffic_source": "profiles/pmc_traffic.json[%s] (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE per "
-                              "launch, separate passes)" % args.workload,
+                              "launch, separate passes)" % workload,
             "traffic_git_head": traffic_git}
     if scan_iso_us is not None:
         roof.update(avg_launch_us_isolated=scan_iso_us,
-                    frac_isolated=bytes_scan / (scan_iso_us * 1e-6) / 1e9 / HBM_PEAK_GBS,
+                    frac_isolated=bytes_alg / (scan_iso_us * 1e-6) / 1e9 / HBM_PEAK_GBS,
                     isolated_timing="HIP events around 200 back-to-back k_scan launches on the final state")
     out = {
         "metric": "candidate moves scored/sec (+ ms per reassignment step)",
@@ -564,7 +617,7 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic (numpy PCG64 seed %#x), %s" % (synth.SEEDS[args.workload], weights),
+        "data": "synthetic (numpy PCG64 seed %#x), %s" % (synth.SEEDS[workload], weights),
         "config": dict(desc, parallelism="single-gpu", device_ms_per_step=1e3 * dev_s / max(steps, 1),
                        mode=args.mode, fused_pairs=fused),
         "roofline": roof,
@@ -578,7 +631,7 @@ def main():
                              "HIP events); every kernel figure describes the timed steps" % kt_steps,
         "engine_events": {k: st1[k] - st0[k] for k in ("retries", "refreshes", "exact_halts", "exact_folds")},
     }
-    if not args.no_cpu_baseline:
+    if with_cpu:
         progress("CPU baseline (%.0f s sample)" % args.cpu_seconds)
         out["cpu_baseline"] = cpu_baseline(cl, cfg, desc, cand / max(steps, 1), args.cpu_seconds)
         progress("CPU baseline done")
@@ -587,7 +640,7 @@ def main():
             out["speedup_vs_cpu"] = out["value"] / cb["value"]
         elif cb.get("unit") == "ms/step":
             out["speedup_vs_cpu"] = cb["value"] / ms_per_step
-    print(json.dumps(out))
+    return out
 
 
 if __name__ == "__main__":

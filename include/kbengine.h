@@ -5,7 +5,7 @@
  * (balancer.go:34-65).  The reference seam is the step signature
  *     func(*PartitionList, RebalanceConfig) (*PartitionList, error)
  * dispatched by Balance() (balancer.go:49-65).  A host (the cgo shim shown in
- * INTEGRATION.md, the C++ host library in kafkabalancer_amd/csrc/host, or the
+ * INTEGRATION.md, the C++ host library in kafkabalancer_amd/host, or the
  * Python mirror) marshals a PartitionList into kb_cluster once, then asks the
  * engine for one Balance() step at a time (kb_engine_balance) or for a whole
  * -max-reassign plan that stays resident on the GPU (kb_engine_plan).
@@ -158,6 +158,14 @@ typedef struct kb_engine kb_engine;
 
 /* ABI version of the loaded library (== KB_ABI_VERSION) */
 int kb_abi_version(void);
+
+/* Diagnostics opt-in (process-wide, default off).  Only after kb_set_diagnostics(1) does the
+ * library read its A/B and diagnostic switches from the environment at kb_engine_create
+ * (KB_FUSE, KB_EAGER, KB_PAIR_WAIT_TICKS, ...: the list is in INTEGRATION.md); a drop-in host
+ * never calls it, so an inherited environment cannot change the engine's kernel paths.  The
+ * test suite and the bench scripts opt in (kafkabalancer_amd/engine.py: KB_DIAGNOSTICS=1). */
+void kb_set_diagnostics(int on);
+int kb_diagnostics_enabled(void);
 
 /* Validates + fills defaults like ValidateWeights/ValidateReplicas/FillDefaults
  * (steps.go:7-66) and uploads the SoA state.  A validation error does not fail

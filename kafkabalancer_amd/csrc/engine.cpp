@@ -52,6 +52,15 @@ static const char* kStepNames[9] = {
 
 enum { TK_STEP = 0, TK_SCAN = 1, TK_REFRESH = 2, TK_BOUND = 3, TK_N = 4 };
 
+// Diagnostic / A-B switches (KB_FUSE, KB_EAGER, KB_PAIR_WAIT_TICKS, ... -- INTEGRATION.md lists
+// them) are read from the environment only after kb_set_diagnostics(1): a drop-in host never
+// calls it, so an inherited environment cannot change the product library's kernel paths.
+// The test suite and the bench scripts opt in (kafkabalancer_amd/engine.py, KB_DIAGNOSTICS=1).
+static int g_diag = 0;
+static const char* diag_getenv(const char* name) { return g_diag ? getenv(name) : nullptr; }
+extern "C" void kb_set_diagnostics(int on) { g_diag = on ? 1 : 0; }
+extern "C" int kb_diagnostics_enabled(void) { return g_diag; }
+
 struct kb_engine {
     int dev = 0;
     hipStream_t st = nullptr;
@@ -609,7 +618,7 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
     e->scan_lds = (e->gb ? 0 : rbytes + 2 * pbytes) + (e->lds_sets ? setbytes : 0) + dedup;
     // (room for the in-stream refresh's two fold buffers: ScanArgs.rfpass)
     e->rf_stream = !e->integral;
-    if (const char* v = getenv("KB_RF_STREAM")) if (*v == '0') e->rf_stream = false;   // diagnostic
+    if (const char* v = diag_getenv("KB_RF_STREAM")) if (*v == '0') e->rf_stream = false;   // diagnostic
     if (e->rf_stream) e->scan_lds = std::max(e->scan_lds, (size_t)RF_LDS_BYTES);
     // one wave of resident workgroups; each loops over its tiles
     int per_cu = scan_blocks_per_cu(e->rc_dev, e->lds_sets, e->gb, e->scan_lds);
@@ -622,7 +631,7 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
         const int64_t nblk = (e->shard_end - e->shard_begin + BLK - 1) / BLK;
         const int64_t slots = (int64_t)per_cu * ncu;
         e->twaves = (int)std::max<int64_t>(1, std::min<int64_t>(SCAN_THREADS / 64, nblk / std::max<int64_t>(slots, 1)));
-        if (const char* v = getenv("KB_TWAVES")) if (atoi(v) > 0) e->twaves = std::min(atoi(v), SCAN_THREADS / 64);  // diagnostic
+        if (const char* v = diag_getenv("KB_TWAVES")) if (atoi(v) > 0) e->twaves = std::min(atoi(v), SCAN_THREADS / 64);  // diagnostic
         e->ntiles = (nblk + e->twaves - 1) / e->twaves;
     }
     // eager refolds (thousands of brokers, non-integral loads: the decisions there need exact
@@ -632,13 +641,13 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
     // (fewer brokers: lazy loads, refreshed when a decision needs them exact; a plan whose
     // decisions keep needing them switches to eager refolds, switch_to_eager)
     e->eager_auto = e->rf_stream && !e->eager && !e->gb;
-    if (const char* v = getenv("KB_EAGER")) { e->eager = e->rf_stream && *v == '1'; e->eager_auto = false; }  // diagnostic
-    if (const char* v = getenv("KB_EAGER_AUTO")) e->eager_auto = e->eager_auto && *v != '0';               // A/B
+    if (const char* v = diag_getenv("KB_EAGER")) { e->eager = e->rf_stream && *v == '1'; e->eager_auto = false; }  // diagnostic
+    if (const char* v = diag_getenv("KB_EAGER_AUTO")) e->eager_auto = e->eager_auto && *v != '0';               // A/B
     e->slots_scan = (int64_t)per_cu * ncu;
     e->nscan = std::min<int64_t>(e->ntiles, std::max<int64_t>(1, (int64_t)per_cu * ncu - (e->eager ? EGW + 1 : 0)));
-    if (const char* v = getenv("KB_NSCAN")) if (atoi(v) > 0) e->nscan = std::min<int64_t>(e->ntiles, atoi(v));  // diagnostic
+    if (const char* v = diag_getenv("KB_NSCAN")) if (atoi(v) > 0) e->nscan = std::min<int64_t>(e->ntiles, atoi(v));  // diagnostic
     e->nscan = std::min<int64_t>(e->nscan, SUM_RECS);     // (a rank summary reads one record per thread)
-    if (const char* v = getenv("KB_DEBUG_SCAN")) e->dbg_scan = atoi(v);                                   // diagnostic
+    if (const char* v = diag_getenv("KB_DEBUG_SCAN")) e->dbg_scan = atoi(v);                                   // diagnostic
     {
         // k_step's LDS: static tables + per-broker arrays (+ every set's words when they fit)
         const int st_lds = step_static_lds(e->gb);
@@ -646,7 +655,7 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
         const int lim = 160 * 1024;
         const int sbw = (int)e->nsets * e->W64;
         e->sb_lds = (!e->gb && sbw * 8 <= STEP_SB_MAX && st_lds + step_lds((int)e->B, e->NP2, sbw).total <= lim) ? 1 : 0;
-        if (const char* v = getenv("KB_STEP_SB")) if (*v == '0') e->sb_lds = 0;                           // diagnostic
+        if (const char* v = diag_getenv("KB_STEP_SB")) if (*v == '0') e->sb_lds = 0;                           // diagnostic
         e->step_lds_bytes = e->gb ? 0 : step_lds((int)e->B, e->NP2, e->sb_lds ? sbw : 0).total;
         if (st_lds + e->step_lds_bytes > lim) { e->last_err = "too many brokers for k_step's LDS"; *out = e; return KB_ERR_UNSUPPORTED; }
     }
@@ -660,9 +669,9 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
         // 0.0427 vs 0.0389 ms/step at c2, profiles/r04_c)
         e->fuse = !e->gb && pair_supported(e->rc_dev) && e->nsets <= (int64_t)MAX_SETS &&
                   full_shard && e->nscan > 1 && e->twaves == SCAN_THREADS / 64;
-        if (const char* v = getenv("KB_FUSE")) e->fuse = e->fuse && *v != '0';                      // A/B
-        if (const char* v = getenv("KB_FUSE_PRE")) e->fuse_pre = *v != '0';                          // diagnostic
-        if (const char* v = getenv("KB_PAIR_WAIT_TICKS")) e->pair_wait_ticks = strtoull(v, nullptr, 10);   // tests
+        if (const char* v = diag_getenv("KB_FUSE")) e->fuse = e->fuse && *v != '0';                      // A/B
+        if (const char* v = diag_getenv("KB_FUSE_PRE")) e->fuse_pre = *v != '0';                          // diagnostic
+        if (const char* v = diag_getenv("KB_PAIR_WAIT_TICKS")) e->pair_wait_ticks = strtoull(v, nullptr, 10);   // tests
         if (e->fuse) {
             e->pair_lds = std::max(e->scan_lds, (size_t)e->step_lds_bytes);
             int pst = 0;
@@ -678,21 +687,25 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
         // grid plus one resident summary workgroup; every workgroup resident at once, as in
         // k_pair (an engine whose k_pair grid would have to shrink for it keeps two launches)
         e->fuse_sum = !e->gb && pair_supported(e->rc_dev) && e->nsets <= (int64_t)MAX_SETS && e->nscan > 1;
-        if (const char* v = getenv("KB_FUSE_SUM")) e->fuse_sum = e->fuse_sum && *v != '0';          // A/B
+        if (const char* v = diag_getenv("KB_FUSE_SUM")) e->fuse_sum = e->fuse_sum && *v != '0';          // A/B
         if (e->fuse_sum) {
             int sst = 0;
             const int scu = scansum_blocks_per_cu(e->rc_dev, e->lds_sets, e->scan_lds, &sst);
             e->slots_sum = (int64_t)scu * ncu;
             const int64_t cap = (int64_t)scu * ncu - (e->eager ? EGW + 1 : (e->integral ? 0 : 1)) - 1;
             // (the summary workgroup stages r in the scan's dynamic LDS)
-            if (scu < 1 || sst + e->scan_lds > 160 * 1024 || cap < 1 || (e->fuse && cap < e->nscan) ||
+            // (a full-shard engine -- one GPU, or the world-1 protocol line -- never shrinks its
+            // scan grid for the summary workgroup: it keeps two launches for the summary instead)
+            if (scu < 1 || sst + e->scan_lds > 160 * 1024 || cap < 1 || ((e->fuse || full_shard) && cap < e->nscan) ||
                 e->scan_lds < (size_t)e->B * 8) e->fuse_sum = false;
             else e->nscan = std::min<int64_t>(e->nscan, cap);
         }
+        // (after every grid sizing above: a rank summary reads one record per thread)
+        e->nscan = std::min<int64_t>(e->nscan, SUM_RECS);
     }
     HIPCHK(hipStreamCreateWithFlags(&e->st, hipStreamNonBlocking));
     e->own_st = true;
-    if (const char* v = getenv("KB_WGT")) {                 // diagnostic: scan workgroup timeline
+    if (const char* v = diag_getenv("KB_WGT")) {                 // diagnostic: scan workgroup timeline
         e->wgt_path = v;
         HIPCHK(dalloc(&e->wgt, 6 * (size_t)std::max<int64_t>(e->nscan, 1)));
         HIPCHK(hipMemset(e->wgt, 0, 6 * (size_t)std::max<int64_t>(e->nscan, 1) * 8));
@@ -720,7 +733,7 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
     HIPCHK(dalloc(&e->bset_off, e->B + 1));
     HIPCHK(dalloc(&e->bset_ids, hbi.size()));
     HIPCHK(dalloc(&e->recs, (size_t)std::max<int64_t>(e->nscan, 1) * WGREC_BYTES));
-    if (const char* v = getenv("KB_CONT_CAP")) e->cont_cap = (uint32_t)std::max(1, atoi(v));   // tests: growth path
+    if (const char* v = diag_getenv("KB_CONT_CAP")) e->cont_cap = (uint32_t)std::max(1, atoi(v));   // tests: growth path
     HIPCHK(dalloc(&e->cont, e->cont_cap));
     HIPCHK(dalloc(&e->ctl, 1));
     HIPCHK(dalloc(&e->bdesc, std::max<size_t>(hbd.size(), 1)));
@@ -750,7 +763,7 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
     HIPCHK(hipHostMalloc((void**)&e->h_flag, 64, hipHostMallocCoherent | hipHostMallocMapped));
     HIPCHK(hipHostGetDevicePointer((void**)&e->h_flag_d, e->h_flag, 0));
     *e->h_flag = 0;
-    if (const char* v = getenv("KB_XFER")) e->xfer = std::min(2, std::max(0, atoi(v)));      // A/B
+    if (const char* v = diag_getenv("KB_XFER")) e->xfer = std::min(2, std::max(0, atoi(v)));      // A/B
     HIPCHK(hipMemcpy(e->w, hw.data(), hw.size() * 8, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(e->meta, hm.data(), hm.size() * 4, hipMemcpyHostToDevice));
     if (!e->lds_sets) {
@@ -825,8 +838,8 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
     // keeps the bound closed: there the pass waits for a first retry (c5: none in 200 steps,
     // 0.1006 -> 0.0962 ms/step without the pass's two launches per step)
     e->ub_mode = e->B >= 2048 && e->allow_leader;
-    if (const char* v = getenv("KB_UB_MODE")) e->ub_mode = *v == '1';                      // diagnostic
-    if (const char* v = getenv("KB_UB_STICKY")) e->ub_sticky = *v != '0';                   // diagnostic
+    if (const char* v = diag_getenv("KB_UB_MODE")) e->ub_mode = *v == '1';                      // diagnostic
+    if (const char* v = diag_getenv("KB_UB_STICKY")) e->ub_sticky = *v != '0';                   // diagnostic
     *out = e;
     return KB_OK;
 }
@@ -1697,7 +1710,7 @@ extern "C" int kb_engine_bench_scan(kb_engine* e, int iters, double* avg_us) {
     // scans, 2 = one that rewrites the scan's tables (as k_step does); each scan is
     // then timed on its own
     int il = 0;
-    if (const char* v = getenv("KB_PROBE_INTERLEAVE")) il = atoi(v);
+    if (const char* v = diag_getenv("KB_PROBE_INTERLEAVE")) il = atoi(v);
     float ms = 0;
     if (il) {
         hipEvent_t c, d;
@@ -2052,6 +2065,12 @@ extern "C" int kb_engine_comm_init(kb_engine* e, int32_t n_ranks, int32_t rank, 
     }
     e->nranks = n_ranks;
     e->rank = rank;
+    // (a new communicator may change the world size or this rank's slot: the exchange
+    // buffers are sized and offset for the old one, so the next plan reallocates them)
+    HIPCHK(hipStreamSynchronize(e->st));
+    if (e->gath_buf) hipFree(e->gath_buf);
+    e->gath_buf = e->sum_buf = nullptr;
+    e->xbuf_bytes = 0;
     return KB_OK;
 }
 

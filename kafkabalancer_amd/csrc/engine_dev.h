@@ -34,6 +34,7 @@ constexpr int SUMMARY_KEYS = 56;    // key slots per rank summary to start with 
                                     // the near-tie keys overflow
 constexpr int SUMMARY_KEYS_MAX = 2048;
 constexpr int SUM_RECS = 1024;      // scan records one rank summary reads (one per thread)
+constexpr uint32_t SUM_POISON = 8u;  // rank summary flag: its summary workgroup timed out (every rank halts)
 constexpr int SUM_RLDS = 8192;      // k_summary keeps r in LDS up to this many brokers
 constexpr int DEDUP_STEP = 2048;    // LDS key table of k_step / k_summary
 constexpr int DEDUP_SCAN = 256;     // LDS key table of one k_scan workgroup

@@ -1723,17 +1723,36 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
     double hd0 = HUGE_VAL, hd1 = HUGE_VAL;
     unsigned long long hc0 = 0, hc1 = 0;
     uint32_t hflg = 0, hfm = 0, hnk0 = 0, hnk1 = 0, hnks = 0;
+    bool hpoison = false;
     if (tid < a.R.n) {
         const RecHdr* h = a.R.h(tid);
         hd0 = ldd(&h->dmin[0]); hd1 = ldd(&h->dmin[1]);
         hc0 = ldobj(&h->cand[0]); hc1 = ldobj(&h->cand[1]);
         hnks = ld32(&h->nkeys);
-        hflg = ld32(&h->flags) & 1u; hfm = ld32(&h->fmask);
+        hflg = ld32(&h->flags);
+        hfm = ld32(&h->fmask);
+        hpoison = !a.use_spill && (hflg & SUM_POISON);   // (a rank summary that timed out)
+        hflg &= 1u;
         const uint32_t nkk = ld32(&h->nkk[0]);
         hnk0 = nkk & 0xFFFFu; hnk1 = nkk >> 16;
     }
     KB_STAMP(ctl, 28);
     dedup_clear(T);
+    if (!a.use_spill && __syncthreads_or(hpoison)) {
+        // some rank's summary workgroup timed out in its wait (k_scansum): its summary is not
+        // this round's; every rank reads the same gathered summaries and stops here alike
+        // (the rank that timed out logged the error in k_scansum and halted already)
+        if (tid == 0 && ctl->halted == H_RUN) {
+            ChangeDev ch;
+            ch.status = -1; ch.step = -1; ch.kind = 0; ch.slot = -1; ch.part = -1; ch.from = ch.to = -1;
+            ch.su = ch.cu = 0.0; ch.exact = 0; ch.err_code = E_PAIR_TIMEOUT; ch.err_broker = -1; ch.pad = 0;
+            const int lp = ctl->logpos;
+            if (lp < ctl->logcap) a.log[lp] = ch;
+            ctl->logpos = lp + 1;
+            ctl->halted = H_DONE;
+        }
+        return;
+    }
     if (tid < 2) { s_nd[tid] = 0; s_li[tid] = -1; s_kfail[tid] = 0; }
     __syncthreads();                               // the control block copy
     {
@@ -3724,7 +3743,7 @@ __global__ __launch_bounds__(1024) void k_listop(DevCtl* ctl, Lists L) {
 // dirty broker: one workgroup per broker; contributions staged in LDS chunks,
 // folded sequentially by one lane.
 
-constexpr int REFRESH_THREADS = 256;
+[[maybe_unused]] constexpr int REFRESH_THREADS = 256;
 [[maybe_unused]] constexpr int REFRESH_CHUNK = 1024;
 // The exact getBrokerLoad fold (utils.go:92-105) of broker b's contributions in partition
 // order by one workgroup of NT threads (every thread calls; the result is wave 0's).
@@ -4187,8 +4206,14 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scansum(ScanArgs a, SumArgs sa
         __syncthreads();
         if (s_to) {
             // (as k_pair's step workgroup: an explicit error in the step log, the plan halts;
-            // the host resets the count and refuses further work)
+            // the host resets the count and refuses further work.)  This rank's summary slot
+            // carries SUM_POISON, so every rank's resolve of this round reads it from the
+            // gathered summaries and halts with the same error: no rank applies a change the
+            // others do not, and no rank stays behind in a later collective.
             if (tid == 0) {
+                RecHdr* out = sa.out.h(0);
+                __hip_atomic_store(&out->flags, SUM_POISON, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_store(&out->nkeys, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 DevCtl* ctl = sa.ctl;
                 ChangeDev ch;
                 ch.status = -1; ch.step = -1; ch.kind = 0; ch.slot = -1; ch.part = -1; ch.from = ch.to = -1;

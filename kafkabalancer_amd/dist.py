@@ -183,21 +183,21 @@ def bench_main(args, world, rank, local, cpu_baseline=None):
     local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dist.init_process_group(backend)
-    # strong scaling (c5 default, BASELINE configs[4]): one cluster of the configured size
-    # sharded N ways; weak: every rank adds a full cluster's worth of partitions
-    scaling = getattr(args, "scaling", None) or ("strong" if args.workload == "c5" else "weak")
+    # strong scaling (the default): the workload's one cluster (c3: BASELINE's 1M x 1000)
+    # sharded N ways, so the N-GPU line is the same plan as the 1-GPU line; weak: every rank
+    # adds a full cluster's worth of partitions (--scaling weak)
+    scaling = getattr(args, "scaling", None) or "strong"
     cl, cfg, desc = synth.config(args.workload, scale=args.scale * (world if scaling == "weak" else 1))
     shard = shard_bounds(cl.n, world, rank)
     rccl = backend == "nccl"
-    uid = None
-    if rccl:
-        box = [E.comm_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(box, src=0)
-        uid = box[0]
 
     def make():
         if rccl:
-            e = _rccl_engine(E, cl, cfg, local, shard, world, rank, uid)
+            # a fresh RCCL unique id per communicator: the bootstrap root behind an id serves
+            # one ncclCommInitRank round (the kernel-timing replay below builds a second one)
+            box = [E.comm_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(box, src=0)
+            e = _rccl_engine(E, cl, cfg, local, shard, world, rank, box[0])
             return e, (lambda n: _plan_or_raise(e.sharded_plan, n))
         e = E.Engine(cl, cfg, device=local, shard=shard)
         e.set_stream(torch.cuda.current_stream().cuda_stream)
@@ -221,6 +221,7 @@ def bench_main(args, world, rank, local, cpu_baseline=None):
     st1 = eng.stats()
     steps = max(1, len(changes))
     cand = st1["candidates"] - st0["candidates"]       # merged counts: the whole job
+    dev_ms = st1["device_ms"] if rccl else None        # (the timed plan call's device time)
     eng.close()
     # per-kernel device-clock durations over the same steps (a fresh engine replays the
     # warm-up and the timed steps): the scan launch's span, as on one GPU -- the end of
@@ -239,9 +240,16 @@ def bench_main(args, world, rank, local, cpu_baseline=None):
         timing = "device clock: earliest scan workgroup start to latest end"
     scan_us = 1e3 * scan_ms / max(scan_n, 1)
     shard_bytes = st1["scan_bytes"]
-    achieved = shard_bytes / (scan_us * 1e-6) / 1e9 if scan_us > 0 else 0.0
+    scan_achieved = shard_bytes / (scan_us * 1e-6) / 1e9 if scan_us > 0 else 0.0
+    # the same pricing as the 1-GPU line: SURVEY 8(d)'s algorithmic bytes of a step over the
+    # step's device time -- here one round (scan + rank summary, the all-gather, the resolve)
+    # of the whole cluster on N GPUs, against N x the HBM peak (dev_ms: the timed call's
+    # device time on rank 0; every rank runs the same rounds)
+    b8d = cl.n * (8 + 4 * st1["max_replicas"] + 1 + 1 + 4) + 12 * st1["n_brokers"] + \
+        st1["n_sets"] * ((st1["n_brokers"] + 63) // 64) * 8
+    round_us = 1e3 * (dev_ms if dev_ms else wall * 1e3) / steps
+    achieved = b8d / (round_us * 1e-6) / 1e9
     if rank == 0:
-        b8d = cl.n * (8 + 4 * st1["max_replicas"] + 1 + 1 + 4) + 12 * st1["n_brokers"]
         out = {
             "metric": "candidate moves scored/sec (+ ms per reassignment step)",
             "value": cand / wall,
@@ -260,10 +268,21 @@ def bench_main(args, world, rank, local, cpu_baseline=None):
             "config": dict(desc, parallelism="partition-sharded x%d, replicated broker state, "
                                               "1 all-gather per step (%s)" % (world, "RCCL, plan driven from C"
                                                                               if rccl else "gloo, host-staged")),
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": 8000.0, "unit": "GB/s",
-                         "frac": achieved / 8000.0, "traffic": None, "kernel": "k_scan (rank 0 shard)",
-                         "bytes_per_launch": shard_bytes, "avg_launch_us": scan_us, "timing": timing,
-                         "launches": scan_n,
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": 8000.0 * world, "unit": "GB/s",
+                         "frac": achieved / (8000.0 * world),
+                         # (PMC passes are 1-GPU runs: profiles/pmc_traffic.json carries the world-1
+                         # sharded protocol's per-launch traffic where one was taken)
+                         "traffic": None,
+                         "kernel": "one sharded round: k_scansum (scan + rank summary) + ncclAllGather + k_step "
+                                   "(resolve), whole cluster on %d GPUs" % world,
+                         "bytes_per_launch": b8d,
+                         "bytes_per_launch_def": "SURVEY.md 8(d) algorithmic bytes of one step of the whole cluster",
+                         "avg_launch_us": round_us,
+                         "timing": "device time of the timed plan call (rank 0) / steps" if dev_ms else
+                                   "wall time / steps (no device time on this path)",
+                         "scan_span_us": scan_us, "scan_timing": timing, "scan_launches": scan_n,
+                         "scan_bytes_per_rank": shard_bytes,
+                         "scan_achieved_per_rank": scan_achieved, "scan_frac_per_rank": scan_achieved / 8000.0,
                          "frac_step": b8d / (wall / steps) / 8e12,
                          "frac_step_def": "SURVEY.md 8(d) bytes of the whole cluster per step / ms_per_step / 8 TB/s"},
             "kernels_us_per_launch": {k: 1e3 * v[0] / max(v[1], 1) for k, v in tk.items() if v[1]},

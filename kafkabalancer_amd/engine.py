@@ -29,7 +29,8 @@ EXPORTS = ["kb_abi_version", "kb_engine_create", "kb_engine_balance", "kb_engine
            "kb_engine_step_begin", "kb_engine_step_finish", "kb_engine_set_stream",
            "kb_engine_sharded_reset", "kb_engine_sharded_scan", "kb_engine_sharded_resolve",
            "kb_engine_sharded_collect", "kb_engine_set_incremental", "kb_engine_step",
-           "kb_engine_host_timings", "kb_comm_unique_id", "kb_engine_comm_init", "kb_engine_sharded_plan"]
+           "kb_engine_host_timings", "kb_comm_unique_id", "kb_engine_comm_init", "kb_engine_sharded_plan",
+           "kb_set_diagnostics", "kb_diagnostics_enabled"]
 
 P64 = C.POINTER(C.c_int64)
 PD = C.POINTER(C.c_double)
@@ -150,6 +151,12 @@ def lib():
             L.kb_engine_set_incremental.restype = C.c_int
         if L.kb_abi_version() != 10 and not any_abi:
             raise ImportError("libkbengine.so ABI mismatch")
+        # the library's A/B and diagnostic switches (KB_FUSE, KB_EAGER, ...) are read from the
+        # environment only after this opt-in (include/kbengine.h); the tests and the bench
+        # scripts set KB_DIAGNOSTICS=1, a plain import leaves them off
+        if hasattr(L, "kb_set_diagnostics"):
+            L.kb_set_diagnostics.argtypes = [C.c_int]
+            L.kb_set_diagnostics(1 if os.environ.get("KB_DIAGNOSTICS") == "1" else 0)
         _lib = L
     return _lib
 

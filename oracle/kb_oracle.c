@@ -575,6 +575,11 @@ static int move_chunk(const or_plist *pl, const or_config *cfg, int leaders, blo
  * in iteration order.  tests/test_oracle.py checks it against the literal loop. */
 static int g_window = 0;
 void or_set_window(int on) { g_window = on ? 1 : 0; }
+/* target walks the early stop below ended (n >= 64), summed over move_window calls: the
+   tests check that the walk's branch is exercised (tests/test_oracle.py) */
+static int64_t g_walk_stops = 0;
+int64_t or_walk_stops(void) { return g_walk_stops; }
+void or_reset_walk_stops(void) { g_walk_stops = 0; }
 
 typedef struct { double ua; int64_t i, s, k, ridx; } wcand;
 typedef struct { wcand *v; int64_t n, cap; double best; } wlist;
@@ -656,6 +661,7 @@ static int move_window(const or_plist *pl, const or_config *cfg, int leaders, bl
     if (T > np) T = np > 0 ? (int)np : 1;
     wlist *TL = (wlist *)calloc((size_t)T, sizeof(wlist));
     int64_t *tcnt = (int64_t *)calloc((size_t)T, sizeof(int64_t));
+    int64_t *tstop = (int64_t *)calloc((size_t)T, sizeof(int64_t));
     int *terr = (int *)calloc((size_t)T, sizeof(int));
 #pragma omp parallel for num_threads(T) schedule(static, 1)
     for (int t = 0; t < T; t++) {
@@ -701,6 +707,7 @@ static int move_window(const or_plist *pl, const or_config *cfg, int leaders, bl
                             if (ua < L->best) L->best = ua;
                         } else if (walk && ua > L->best + 3 * eps) {
                             stop = 1;          /* every later target scores above the window */
+                            tstop[t]++;
                             break;
                         }
                     }
@@ -710,6 +717,8 @@ static int move_window(const or_plist *pl, const or_config *cfg, int leaders, bl
     }
     int err = 0;
     double best = HUGE_VAL;
+    for (int t = 0; t < T; t++) g_walk_stops += tstop[t];
+    free(tstop);
     for (int t = 0; t < T && !err; t++) {
         *cnt_out += tcnt[t];
         if (terr[t]) { err = terr[t]; break; }          /* the first panic in order */

@@ -103,6 +103,8 @@ void or_set_threads(int n);
  * reference's choice -- the same result as the literal loop (kb_oracle.c: move_window;
  * tests/test_oracle.py checks it).  Default off. */
 void or_set_window(int on);
+int64_t or_walk_stops(void);
+void or_reset_walk_stops(void);
 
 /* Build a partition list from flat arrays.  Brokers lists are deduplicated
  * into sets; partitions with the same set_idx share one slice (as FillDefaults

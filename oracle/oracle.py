@@ -86,6 +86,10 @@ def lib():
         L.or_set_threads.restype = None
         L.or_set_window.argtypes = [C.c_int]
         L.or_set_window.restype = None
+        L.or_walk_stops.argtypes = []
+        L.or_walk_stops.restype = C.c_int64
+        L.or_reset_walk_stops.argtypes = []
+        L.or_reset_walk_stops.restype = None
         _lib = L
     return _lib
 
@@ -274,6 +278,15 @@ def move_sample(opl, cfg, leaders, max_parts):
 def set_threads(n):
     """Worker threads of the oracle's move() (identical results for any n)."""
     lib().or_set_threads(int(n))
+
+
+def walk_stops(reset=False):
+    """Target walks the windowed search's early stop ended since the last reset (its n >= 64
+    branch, kb_oracle.c move_window)."""
+    n = int(lib().or_walk_stops())
+    if reset:
+        lib().or_reset_walk_stops()
+    return n
 
 
 def set_window(on):

@@ -598,3 +598,39 @@ def test_bench_gpus2_spawns_two_ranks(tmp_path):
     key = lambda c: (c["step"], c["pidx"], c["kind"], c["from_"], c["to"], c["slot"])
     assert [key(c) for c in got] == [key(c) for c in want[5:35]]
     eng.close()
+
+
+@pytest.mark.gpu
+def test_bench_main_rccl_world1(tmp_path):
+    """The multi-GPU bench path with RCCL (its default backend) under a one-rank
+    torch.distributed.run launch: both engines it builds (the timed plan and the kernel-timing
+    replay) get communicators of their own unique ids, the line is printed, and the plan
+    equals one engine's plan of the same steps."""
+    import socket
+    from kafkabalancer_amd import engine as E
+    from kafkabalancer_amd import synth
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = tmp_path / "plan.json"
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    env = dict(os.environ)
+    env.pop("KB_DIST_BACKEND", None)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port),
+                        os.path.join(root, "bench.py"), "--dist-world1", "--workload", "c3", "--scale", "0.02",
+                        "--steps", "30", "--warmup", "5", "--no-cpu-baseline", "--plan-out", str(out)],
+                       cwd=root, env=env, capture_output=True, text=True, timeout=400)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["n_gpus"] == 1 and line["exchange"] == "rccl" and line["scaling"] == "strong", line
+    assert line["roofline"]["avg_launch_us"] > 0 and 0 < line["roofline"]["frac"] < 1, line["roofline"]
+    got = json.load(open(out))
+    cl, cfg, _ = synth.config("c3", scale=0.02)
+    eng = E.Engine(cl, cfg)
+    want, err = eng.plan(35)
+    assert err is None
+    key = lambda c: (c["step"], c["pidx"], c["kind"], c["from_"], c["to"], c["slot"])
+    assert [key(c) for c in got] == [key(c) for c in want[5:35]]
+    eng.close()

@@ -56,3 +56,22 @@ def test_broker_universe_limit():
     with pytest.raises(E.EngineError) as ei:
         E.Engine(cl, cfg)
     assert ei.value.code == -3 and "16384 distinct brokers" in str(ei.value)   # KB_ERR_UNSUPPORTED
+
+
+def test_diagnostic_switches_need_the_opt_in():
+    """The library reads its KB_* A/B and diagnostic switches only after kb_set_diagnostics(1)
+    (a drop-in host never calls it): loaded without KB_DIAGNOSTICS the opt-in is off, with it
+    the Python binding turns it on."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = ("import sys; sys.path.insert(0, %r); from kafkabalancer_amd import engine as E; "
+            "print(E.lib().kb_diagnostics_enabled())" % root)
+    for val, want in ((None, "0"), ("1", "1")):
+        env = dict(os.environ, KB_FUSE="0")
+        env.pop("KB_DIAGNOSTICS", None)
+        if val:
+            env["KB_DIAGNOSTICS"] = val
+        r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, r.stderr[-2000:]
+        assert r.stdout.strip().splitlines()[-1] == want, r.stdout

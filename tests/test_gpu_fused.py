@@ -218,3 +218,47 @@ def test_sharded_summary_wide_brokers_match_plain_plan():
     got, err, st, _ = _sharded_world1(cl, cfg, 24, ("KB_FUSE_SUM", "1"))
     assert err is None and st["fused_summaries"] == 0
     assert keyed(got) == keyed(want)
+
+
+def test_torch_hip_init_after_engine_sharded():
+    """A host that initialises HIP through torch only after kb_engine_create (the pattern
+    commit 43f2c44 moved the world-1 sharded tests away from): torch's first CUDA tensor
+    comes after the engine's HIP state, and the batched sharded protocol then runs over that
+    torch buffer.  The plan must equal the one over a hipMalloc'd buffer, which the tests
+    above use.  (Run in a child process so that torch's CUDA state starts uninitialised.)"""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = r'''
+import json, sys
+sys.path.insert(0, %r); sys.path.insert(0, %r)
+import torch
+from kafkabalancer_amd import engine as E
+from kafkabalancer_amd import synth
+import test_gpu_fused as T
+cl, cfg, _ = synth.config("c3", scale=0.05)
+eng = E.Engine(cl, cfg, shard=(0, cl.n))           # engine HIP state first
+assert not torch.cuda.is_initialized()
+summ = torch.zeros(eng.summary_bytes(), dtype=torch.uint8, device="cuda")   # then torch's
+torch.cuda.synchronize()
+got = []
+while len(got) < 30:
+    eng.sharded_reset(10)
+    for _ in range(10):
+        eng.sharded_scan(summ.data_ptr())
+        eng.sharded_resolve(summ.data_ptr(), 1)
+    st, ch = eng.sharded_collect(11)
+    got.extend(ch)
+    if st == "done":
+        break
+eng.close()
+ref, err, _, _ = T._sharded_world1(cl, cfg, 30, ("KB_FUSE_SUM", "1"))
+key = lambda c: (c["step"], c["pidx"], c["kind"], c["from_"], c["to"], c["slot"])
+print(json.dumps({"n": len(got), "equal": [key(c) for c in got[:30]] == [key(c) for c in ref[:30]],
+                  "err": None if err is None else str(err)}))
+''' % (root, os.path.join(root, "tests"))
+    r = subprocess.run([sys.executable, "-c", code], cwd=root, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, (r.returncode, r.stderr[-3000:])
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    assert res["err"] is None and res["n"] >= 30 and res["equal"], res

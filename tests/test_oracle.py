@@ -277,7 +277,53 @@ def test_windowed_oracle_matches_literal(seed):
     assert run(0, 1) == run(1, 3)
 
 
-@pytest.mark.parametrize("name", ["b4096_zipf", "c3s_nonleader", "c3s_leader"])
+# the early-stop target walk of the windowed search runs only with n >= 64 brokers
+# (kb_oracle.c move_window); these plans exercise it against the literal loop: 64-200 brokers,
+# every weight mode, with and without allowed lists, leader moves on and off
+WALK_CASES = [(b, w, s, al) for b in (64, 97, 150, 200) for w in ("uniform", "int", "zipf")
+              for s, al in (("none", False), ("all", True), ("some", False), ("all", False))]
+
+
+@pytest.mark.parametrize("B,weights,sets,allow_leader", WALK_CASES)
+def test_windowed_oracle_walk_matches_literal(B, weights, sets, allow_leader):
+    """or_set_window(1) with the early-stop walk (n >= 64) equals the literal move() loop on
+    the whole plan: every change, su / cu bit and the final state; the walk's stop branch
+    is taken (its counter), so the n >= 64 path is what was compared."""
+    rng = random.Random(hash((B, weights, sets, allow_leader)) & 0xFFFFFFFF)
+    pl = random_plist(rng, rng.choice([300, 600]), B, weights, sets, False, rng.random() < 0.3)
+    for p in pl["partitions"]:
+        # (allowed lists that hold the partition's replicas: the plan reaches move() at once
+        # instead of spending its steps in MoveDisallowedReplicas)
+        if "brokers" in p:
+            p["brokers"] = sorted(set(p["brokers"]) | set(p["replicas"]))
+    cfg = default_cfg(allow_leader=allow_leader, min_unbalance=0.0)
+
+    def run(window, threads):
+        O.set_threads(threads)
+        O.set_window(window)
+        try:
+            o = O.OraclePL(pl)
+            out = []
+            for _ in range(12):
+                r = O.balance(o, cfg, O.SEM_APPLIED)
+                out.append((r["status"], r["step"], r.get("pidx"), r.get("kind"), r.get("from_"), r.get("to"),
+                            r.get("slot"), r.get("su"), r.get("cu"), r["err"]))
+                if r["status"] != 1:
+                    break
+            return out, o.state()
+        finally:
+            O.set_threads(1)
+            O.set_window(0)
+
+    want = run(0, 1)
+    O.walk_stops(reset=True)
+    got = run(1, 3)
+    stops = O.walk_stops(reset=True)
+    assert got == want
+    assert stops > 0, "the early-stop walk never ran"
+
+
+@pytest.mark.parametrize("name", ["b4096_zipf", "b4096_uniform", "c3s_nonleader", "c3s_leader", "b6000_zipf"])
 def test_windowed_oracle_reproduces_scale_goldens(name):
     """The windowed search regenerates the committed large goldens the literal loop made
     (4096 brokers; 20k partitions x 1000 brokers with 256 allowed sets, leader and
@@ -293,13 +339,19 @@ def test_windowed_oracle_reproduces_scale_goldens(name):
     cfg = gs.case_cfg(name)
     O.set_threads(min(8, os.cpu_count() or 1))
     O.set_window(1)
+    O.walk_stops(reset=True)
+    # (b4096_uniform: the exact-tie worst case, and b6000_zipf: past the LDS broker tables;
+    # their first 12 steps)
+    nmax = 12 if name in ("b4096_uniform", "b6000_zipf") else 60
     try:
         o = gs.oracle_pl(cl)
-        for k, want in enumerate(g["changes"][:60]):
+        for k, want in enumerate(g["changes"][:nmax]):
             r = O.balance(o, cfg, O.SEM_APPLIED)
             assert r["status"] == 1, (k, r["err"])
             assert [r["step"], r["pidx"], r["kind"], r["from_"], r["to"], r["slot"]] == want, k
             assert r["su"] == g["su"][k] and r["cu"] == g["cu"][k], k
+        # (n >= 64 brokers everywhere here: the early-stop walk ran)
+        assert O.walk_stops(reset=True) > 0
     finally:
         O.set_threads(1)
         O.set_window(0)

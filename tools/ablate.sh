@@ -1,4 +1,5 @@
 #!/bin/bash
+export KB_DIAGNOSTICS=1   # (the engine reads its KB_* switches only with this opt-in)
 # Diagnostic: k_step time with phases ablated (kafkabalancer_amd/csrc `make abl ABL=n`
 # builds; their plans are wrong by construction, only the timing is of interest).
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1

@@ -1,4 +1,5 @@
 #!/bin/bash
+export KB_DIAGNOSTICS=1   # (the engine reads its KB_* switches only with this opt-in)
 # Diagnostic: build libkbengine.so of a git revision as kafkabalancer_amd/lib/libkbengine_<name>.so
 # (A/B timing against the working tree in one GPU call: tools/exp_step.sh new=- old=libkbengine_<name>.so)
 REV=${1:-HEAD}; NAME=${2:-prev}

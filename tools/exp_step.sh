@@ -1,4 +1,5 @@
 #!/bin/bash
+export KB_DIAGNOSTICS=1   # (the engine reads its KB_* switches only with this opt-in)
 # Diagnostic A/B of k_step variants on the c3 bench: each argument is NAME=LIB[:ENV=VAL,...]
 # (LIB relative to kafkabalancer_amd/lib; "-" = the production build).  Prints ms/step and
 # the per-step kernel times of each variant.  Plans of ablation builds are wrong by design.

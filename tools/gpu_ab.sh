@@ -1,4 +1,5 @@
 #!/bin/bash
+export KB_DIAGNOSTICS=1   # (the engine reads its KB_* switches only with this opt-in)
 # Same-box A/B of the current build against other builds in lib/ (libkbengine_<v>.so):
 # c3 bench lines alternated so box drift shows.  Usage: gpurun -- 'bash tools/gpu_ab.sh <tag> v1 v2 ...'
 set -u

@@ -1,4 +1,5 @@
 #!/bin/bash
+export KB_DIAGNOSTICS=1   # (the engine reads its KB_* switches only with this opt-in)
 # Same-box A/B of the current build against lib/libkbengine_prev.so on one workload:
 # usage: gpurun -- 'bash tools/gpu_ab_wl.sh <tag> <workload> <steps>'
 set -u

@@ -1,4 +1,5 @@
 #!/bin/bash
+export KB_DIAGNOSTICS=1   # (the engine reads its KB_* switches only with this opt-in)
 # Step-body session: bench lines of c2 / c3 / c3nl / c5 at their headline step counts, the
 # sharded world-1 line with and without the fused summary, the KB_STAMPS phase breakdown of c2 and c3, then the GPU suite.
 # Usage: gpurun -- 'bash tools/gpu_c2.sh <tag> [suite]'

@@ -1,4 +1,5 @@
 #!/bin/bash
+export KB_DIAGNOSTICS=1   # (the engine reads its KB_* switches only with this opt-in)
 # A/B of the fused pair (k_pair) against the two-launch pair on the default bench, then the
 # parity tests that run plans through it.  Every GPU step has its own time limit.
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1

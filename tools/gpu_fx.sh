@@ -1,4 +1,5 @@
 #!/bin/bash
+export KB_DIAGNOSTICS=1   # (the engine reads its KB_* switches only with this opt-in)
 # the whole -m gpu suite on the default (fused) path, then the exact-fold tests on the
 # two-launch path (KB_FUSE=0); each step under its own time limit
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1

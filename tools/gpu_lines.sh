@@ -1,4 +1,5 @@
 #!/bin/bash
+export KB_DIAGNOSTICS=1   # (the engine reads its KB_* switches only with this opt-in)
 # bench lines of a measurement session into gpurun_out/$TAG/: the default bench (c3, with
 # the CPU baseline), c2 / c4 / c5 / c3 at 1000 steps / c3nl / w16k (each with its CPU
 # baseline), the drop-in costs at c3 and the

@@ -1,4 +1,5 @@
 #!/bin/bash
+export KB_DIAGNOSTICS=1   # (the engine reads its KB_* switches only with this opt-in)
 # Quick check of a build on one box: bench lines (200 steps, no CPU baseline) of the
 # workloads in $WLS, then the GPU tests in $TESTS (default: the fused-pair, full-size pin,
 # parity and per-step files; TESTS=all runs the whole -m gpu suite).

@@ -1,4 +1,5 @@
 #!/bin/bash
+export KB_DIAGNOSTICS=1   # (the engine reads its KB_* switches only with this opt-in)
 # Round-4 GPU session: the whole -m gpu suite (no -x: every failure is listed), then --
 # only if it ended normally -- the default bench line and a rocprofv3 kernel trace of the
 # same command.  Every GPU step has its own time limit; the chain stops at the first

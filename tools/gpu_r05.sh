@@ -1,4 +1,5 @@
 #!/bin/bash
+export KB_DIAGNOSTICS=1   # (the engine reads its KB_* switches only with this opt-in)
 # Round-5 GPU session (run through gpurun from the repo root): the bench lines of the
 # headline and the c2 / c3nl / c5 / sharded workloads, then the GPU suite.
 # Usage: gpurun -- 'bash tools/gpu_r05.sh <tag> [steps]'

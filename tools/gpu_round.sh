@@ -1,4 +1,5 @@
 #!/bin/bash
+export KB_DIAGNOSTICS=1   # (the engine reads its KB_* switches only with this opt-in)
 # One GPU session: parity tests, then (only if the tests ended normally) the
 # bench, then (optionally) a rocprofv3 kernel-trace of the bench and PMC passes.
 # Usage: tools/gpu_round.sh TAG [--prof] [--pmc] [--notest] [pytest-args...]

@@ -1,4 +1,5 @@
 #!/bin/bash
+export KB_DIAGNOSTICS=1   # (the engine reads its KB_* switches only with this opt-in)
 # k_step phase stamps (libkbengine_stamps.so, -DKB_STAMPS) of several workloads on one box,
 # then the production build's bench line of each (same box).
 # Usage: gpurun -- 'bash tools/gpu_stamps.sh <tag> [workloads...]'   (default: c3 c5 c2)

@@ -1,4 +1,5 @@
 #!/bin/bash
+export KB_DIAGNOSTICS=1   # (the engine reads its KB_* switches only with this opt-in)
 # per-phase k_step stamps (-DKB_STAMPS build) of the fused and the two-launch pair on one
 # workload ($WL, default c2): which phase the fused step pays for
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1

@@ -10,6 +10,7 @@ import json
 import os
 import sys
 import time
+os.environ.setdefault("KB_DIAGNOSTICS", "1")   # (the engine reads its KB_* switches only with this opt-in)
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)

@@ -1,4 +1,5 @@
 #!/bin/bash
+export KB_DIAGNOSTICS=1   # (the engine reads its KB_* switches only with this opt-in)
 # PMC passes over a short bench run (one counter group per rocprofv3 run, kernel
 # trace only): FETCH_SIZE and WRITE_SIZE per dispatch of every kernel.
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out

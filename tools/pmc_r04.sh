@@ -1,4 +1,5 @@
 #!/bin/bash
+export KB_DIAGNOSTICS=1   # (the engine reads its KB_* switches only with this opt-in)
 # PMC passes for the roofline's `traffic` (MI355X_MICROARCH.md HBM section): per workload
 # one rocprofv3 run per counter (FETCH_SIZE, then WRITE_SIZE; kernel trace only, never
 # with a runtime / sys trace), each under its own hard time limit.

@@ -1,4 +1,5 @@
 #!/bin/bash
+export KB_DIAGNOSTICS=1   # (the engine reads its KB_* switches only with this opt-in)
 # SQ counter passes over a short bench run (k_step / k_scan instruction mix and waits).
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out
 TAG=${1:-pmcs}

@@ -1,4 +1,5 @@
 #!/bin/bash
+export KB_DIAGNOSTICS=1   # (the engine reads its KB_* switches only with this opt-in)
 # rocprofv3 kernel-trace summary of the bench on each workload in $WLS (default c3 c2):
 # gpurun_out/prof/<wl>/ holds the trace; prints each kernel's calls and average duration.
 # STEPS_<wl> overrides the step count (default 200, the default bench's; c2 80, its plan's length).

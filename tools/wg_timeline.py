@@ -9,6 +9,7 @@ import os
 import sys
 
 import numpy as np
+os.environ.setdefault("KB_DIAGNOSTICS", "1")   # (the engine reads its KB_* switches only with this opt-in)
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
