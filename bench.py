@@ -476,9 +476,14 @@ def measure(args, workload, with_cpu):
         st = eng.stamps()
         n = max(1, eng.stats()["steps"])       # every step since the engine was created
         # (stamp ids as placed in kernels.hip; 6..20 name the fused incremental prep's phases)
-        names = ["prep.S+r+ubloop", "step.loads", "res.reduce", "res.pred", "res.move", "res.apply(tail)", "prep.P1", None,
-                 "prep.P2", "prep.P3", "prep.end", "res.move->apply", "loads.bro+ctl", "loads.rec_reduce", "loads.keys", None, "prep.P4",
-                 "eps.sync1", "eps.wave0red", "prep.positions", "prep.sets", "apply.loads", "apply.update"]
+        # (the fast prep, round 6, reuses the ids of the full prep's phases it replaces: 9 FP1 counts,
+        # 16 FP1 marks, 19 FP1 frozen totals, 20 FP1 upper bound, 6 FP1 barrier, 0 FP2 merge,
+        # 8 FP2 barrier, 10 the commit)
+        names = ["prep.S+r+ubloop|fp2.merge", "step.loads", "res.reduce", "res.pred", "res.move", "res.apply(tail)",
+                 "prep.P1|fp1.barrier", "pre.staged",
+                 "prep.P2|fp2.barrier", "prep.P3|fp1.counts", "prep.end|fp.commit", "res.move->apply", "loads.bro+ctl",
+                 "loads.rec_reduce", "loads.keys", "pre.dprep", "prep.P4|fp1.marks",
+                 "eps.sync1", "eps.wave0red", "prep.positions|fp1.totals", "prep.sets|fp1.ub", "apply.loads", "apply.update"]
         counts = {"waves_scored": 7, "waves_gated_in": 15, "emits": 31, "spills": 30, "walks": 29, "walk_steps": 28, "walk_global": 27}
         mhz = 100.0 * st[25] / max(st[24], 1)           # shader clock (the phase stamps' unit)
         names = names + ["loads.broker", None, None, "stamp.overhead", "loads.setbits", "loads.hdr"]

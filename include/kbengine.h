@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define KB_ABI_VERSION 10
+#define KB_ABI_VERSION 11
 
 /* step indices == position in the reference's steps table (balancer.go:34-44) */
 enum kb_step {
@@ -152,6 +152,8 @@ typedef struct {
     int64_t eager;                  /* 1: touched brokers are refolded beside the next scan
                                        (eager refolds; ABI 10) */
     int64_t eager_switches;         /* plans switched from lazy loads to eager refolds (ABI 10) */
+    int64_t fast_preps;             /* steps whose order / positions / set records were left to the
+                                       next launch (the deferred prep, ABI 11) */
 } kb_stats;
 
 typedef struct kb_engine kb_engine;

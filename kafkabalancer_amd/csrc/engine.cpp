@@ -112,6 +112,8 @@ struct kb_engine {
     int64_t slots_scan = 0, slots_pair = 0, slots_sum = 0;
     bool eager_auto = false;          // lazy loads now; eager refolds once exact halts are frequent
     int64_t eager_switches = 0;
+    int fp_lds = 0;                 // deferred prep: byte offset of its region in k_step's LDS (0: none)
+    int fp_bk = 0;                  // ... which also holds the records' best keys
     // the halt rate's window: the steps and exact halts at the checkpoint before last (w0)
     // and at the last one (w1), checkpoints at least 64 steps apart
     unsigned long long w0_steps = 0, w0_halts = 0, w1_steps = 0, w1_halts = 0;
@@ -657,6 +659,23 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
         e->sb_lds = (!e->gb && sbw * 8 <= STEP_SB_MAX && st_lds + step_lds((int)e->B, e->NP2, sbw).total <= lim) ? 1 : 0;
         if (const char* v = diag_getenv("KB_STEP_SB")) if (*v == '0') e->sb_lds = 0;                           // diagnostic
         e->step_lds_bytes = e->gb ? 0 : step_lds((int)e->B, e->NP2, e->sb_lds ? sbw : 0).total;
+        // the deferred prep's region (bl positions, one 16-B record per set; DESIGN.md "Deferred
+        // prep"): set words resident, one-unit records, at most 1024 sets (its set list lives in
+        // the step's mark words)
+        e->fp_lds = 0;
+        e->fp_bk = 0;
+        const int fpb = (((int)e->B * 4 + 15) & ~15) + (int)e->nsets * 16;
+        const int fpk = (int)std::min<int64_t>(e->nscan, STEP_THREADS) * 2 * (int)sizeof(Contender);
+        bool fp = !e->gb && e->sb_lds && e->units == 1 && e->nsets <= 1024 &&
+                  st_lds + e->step_lds_bytes + fpb <= lim;
+        if (const char* v = diag_getenv("KB_FP")) fp = fp && *v != '0';                           // A/B
+        if (fp) {
+            e->fp_lds = e->step_lds_bytes;
+            e->step_lds_bytes += fpb;
+            // (the records' best keys too, for the fast prep's upper bound: it then defers only
+            // with at most STEP_THREADS records)
+            if (e->nscan <= STEP_THREADS && st_lds + e->step_lds_bytes + fpk <= lim) { e->fp_bk = 1; e->step_lds_bytes += fpk; }
+        }
         if (st_lds + e->step_lds_bytes > lim) { e->last_err = "too many brokers for k_step's LDS"; *out = e; return KB_ERR_UNSUPPORTED; }
     }
     {
@@ -694,9 +713,9 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
             e->slots_sum = (int64_t)scu * ncu;
             const int64_t cap = (int64_t)scu * ncu - (e->eager ? EGW + 1 : (e->integral ? 0 : 1)) - 1;
             // (the summary workgroup stages r in the scan's dynamic LDS)
-            // (a full-shard engine -- one GPU, or the world-1 protocol line -- never shrinks its
-            // scan grid for the summary workgroup: it keeps two launches for the summary instead)
-            if (scu < 1 || sst + e->scan_lds > 160 * 1024 || cap < 1 || ((e->fuse || full_shard) && cap < e->nscan) ||
+            // (a fused engine never shrinks its scan grid for the summary workgroup; an unfused
+            // one -- small shards, whose grids are far below the cap -- may)
+            if (scu < 1 || sst + e->scan_lds > 160 * 1024 || cap < 1 || (e->fuse && cap < e->nscan) ||
                 e->scan_lds < (size_t)e->B * 8) e->fuse_sum = false;
             else e->nscan = std::min<int64_t>(e->nscan, cap);
         }
@@ -910,6 +929,11 @@ static void fill_step_args(kb_engine* e, StepArgs& a, const Recs& R, int use_spi
     a.pset = e->pset;
     a.rf_final = 0;
     a.eager = e->eager && e->nscan > 0 ? 1 : 0;
+    // deferred prep (DevCtl.fp): its LDS region whenever the engine has one (a pending one is
+    // finished by whichever step runs next); a step may defer only in the fused single-GPU path
+    a.fp_lds = e->fp_lds;
+    a.fp_bk = e->fp_bk && R.n <= STEP_THREADS ? 1 : 0;
+    a.fp_ok = e->fp_lds && e->fuse && use_spill && !a.incr && !a.eager && !e->rebalance ? 1 : 0;
 }
 
 static const int kStepBatch = 64;
@@ -1094,6 +1118,7 @@ static int refresh(kb_engine* e) {
     if (c.halted == H_NEED_EXACT) c.halted = H_RUN;
     c.prepped = 0; c.full_prep = 1; c.ndirty = 0; c.want_refresh = 0;
     c.eg_n = 0;
+    c.fp = 0;                                        // (the full prep rebuilds what a deferred one would)
     HIPCHK(hipMemcpyAsync(e->ctl, &c, sizeof c, hipMemcpyHostToDevice, e->st));
     HIPCHK(hipStreamSynchronize(e->st));
     e->refreshes++;
@@ -1111,6 +1136,7 @@ static int reset_ctl(kb_engine* e, int64_t budget_steps) {
         if (const int rc = refresh(e); rc != KB_OK) return rc;
         c = *e->h_ctl;
         c.halted = H_RUN; c.prepped = 0; c.full_prep = 1; c.ndirty = 0; c.want_refresh = 0;
+        c.fp = 0;
     }
     c.halted = H_RUN;
     c.logpos = 0;
@@ -1571,6 +1597,7 @@ extern "C" int kb_engine_stats(kb_engine* e, kb_stats* o) {
     o->fused_summaries = e->fuse_sum ? 1 : 0;
     o->eager = e->eager ? 1 : 0;
     o->eager_switches = e->eager_switches;
+    o->fast_preps = (int64_t)e->h_ctl->total_fp;
     return KB_OK;
 }
 

@@ -248,6 +248,17 @@ struct DevCtl {
     // workgroups of the next scan launch, so the next resolve finds every load exact
     int32_t eg_n, eg_pad;
     int32_t eg_b[8];
+    // deferred prep (round 6): after a plain move() replace (frozen average, bl_move unchanged,
+    // at most two touched brokers) the step workgroup writes only what the next scan cannot
+    // derive -- r[] of the touched brokers, eps / ub, the records of the sets holding them --
+    // and leaves the broker order, the bl positions and the full set-record rebuild to the next
+    // launch's step workgroup, which does them before its wait (beside the scan).  The scan's
+    // workgroups patch the bl positions (posm / blm hold the state before the move) with this
+    // descriptor: fp = 1 pending; fp_t the touched brokers (-1 none); fp_o their bl positions
+    // before the move (INT_MAX none); fp_n after; fp_u = fp_n - (touched brokers before it)
+    int32_t fp, fp_pad;
+    int32_t fp_t[2], fp_o[2], fp_n[2], fp_u[2];
+    unsigned long long total_fp;    // steps that took the fast prep
     // diagnostic phase stamps (builds with -DKB_STAMPS): accumulated
     // shader-clock ticks (clock64) per phase of k_step; [24]/[25] the wall-clock
     // (100 MHz) and shader-clock length of k_step; [26] one stamp's own cost

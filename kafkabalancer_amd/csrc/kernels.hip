@@ -659,7 +659,6 @@ __device__ void walk_targets(const ScanArgs& a, const Dedup& T, RF s_rf, PS s_po
                              BL s_blm, const uint4 (&R)[sr_units(RC)], int kind, long long p,
                              int slot, int src, const uint32_t (&reps)[RC], int nrep, int set, double w, double ds,
                              double g, double eps, double inv_avg, int nblm) {
-    constexpr int KR = sr_kr(RC);
     const unsigned long long ib = ((unsigned long long)p << 21) | ((unsigned long long)slot << 16);
     const double delta = w * inv_avg;
     const int nl = (int)rec_u16(R, 1);
@@ -677,7 +676,9 @@ __device__ void walk_targets(const ScanArgs& a, const Dedup& T, RF s_rf, PS s_po
         if (d <= g + 4.0 * eps) emit(a, T, kind, src, b, w, ib | (unsigned long long)s_pos[b]);
         if (d > g + 8.0 * eps) return;
     }
-    if (nl < KR || last < 0) return;              // the set is exhausted
+    // (the record lists the whole set, or the walk continues past its last member: a record
+    // the fast prep merged may list fewer than KR members of a larger set)
+    if (nl >= (int)rec_u16(R, 0) || last < 0) return;
     // rare: more than KR near-tied targets -- the walk goes on in bl order through the set's
     // membership words in memory, LA positions per round trip (their broker ids, then their
     // words, all in flight together): a set of 64 in 1000 brokers has a member every ~16
@@ -760,6 +761,18 @@ struct ScanParams {
     int incr;                       // incremental round: only the blocks with wmax >= wskip
     double wskip;
     double rlo, rhi;                // range of r[] (prune bound)
+    // deferred prep pending (DevCtl.fp): posm holds the bl positions before the last move;
+    // its touched brokers t move to n, every other bl_move broker follows (fixpos)
+    int fp, fp_t0, fp_t1, fp_o0, fp_o1, fp_u0, fp_u1, fp_n0, fp_n1;
+    // the bl position after the last move of broker b at position p before it (p < 0: not in
+    // bl_move): drop the touched brokers, then count those now before the untouched rank
+    __device__ __forceinline__ int fixpos(int b, int p) const {
+        if (!fp || p < 0) return p;
+        if (b == fp_t0) return fp_n0;
+        if (b == fp_t1) return fp_n1;
+        const int pc = p - (fp_o0 < p ? 1 : 0) - (fp_o1 < p ? 1 : 0);
+        return pc + (fp_u0 <= pc ? 1 : 0) + (fp_u1 <= pc ? 1 : 0);
+    }
 };
 
 // the lookup tables as loaded by one thread (issued with the control block, before the
@@ -769,7 +782,7 @@ struct ScanParams {
 struct TabRaw {
     bool pre;
     double r;
-    int32_t pos, blm;
+    int32_t pos;
     uint4 set;
 };
 
@@ -832,29 +845,32 @@ __device__ __forceinline__ void scan_round(const ScanArgs& a, const ScanParams& 
     } else if (TR.pre) {
         if (tid < a.B) {
             TB.rf[tid] = make_double2(TR.r, fsq(TR.r));
-            TB.pos[tid] = (int16_t)TR.pos;
-            TB.blm[tid] = (uint16_t)TR.blm;
+            // (bl order as the inverse of the positions: one table load fewer, and the
+            // deferred prep's patch applies to both)
+            const int p = q.fixpos(tid, TR.pos);
+            TB.pos[tid] = (int16_t)p;
+            if (p >= 0) TB.blm[p] = (uint16_t)tid;
         }
     } else {
         // (more brokers: every load first -- at most MAXB / SCAN_THREADS per thread --
         // then the LDS writes: one round trip, not one per loop iteration)
         constexpr int TQ = (MAXB + SCAN_THREADS - 1) / SCAN_THREADS;
         double rr[TQ];
-        int32_t pp[TQ], bb[TQ];
+        int32_t pp[TQ];
 #pragma unroll
         for (int k = 0; k < TQ; k++) {
             const int i = min(k * SCAN_THREADS + tid, a.B - 1);
             rr[k] = ldd(a.r + i);
             pp[k] = (int32_t)ld32(a.posm + i);
-            bb[k] = (int32_t)ld32(a.blm + i);
         }
 #pragma unroll
         for (int k = 0; k < TQ; k++) {
             const int i = k * SCAN_THREADS + tid;
             if (i < a.B) {
                 TB.rf[i] = make_double2(rr[k], fsq(rr[k]));
-                TB.pos[i] = (int16_t)pp[k];
-                TB.blm[i] = (uint16_t)bb[k];
+                const int p = q.fixpos(i, pp[k]);
+                TB.pos[i] = (int16_t)p;
+                if (p >= 0) TB.blm[p] = (uint16_t)i;
             }
         }
     }
@@ -1380,6 +1396,11 @@ __device__ __forceinline__ void scan_kernel_body(const ScanArgs& a) {
     q.tk_on = cc->tk_on;
     q.rlo = cc->rlo; q.rhi = cc->rhi;
     const int c_incr_ok = cc->incr_ok, c_ub_sub = cc->ub_sub;
+    q.fp = cc->fp;
+    q.fp_t0 = cc->fp_t[0]; q.fp_t1 = cc->fp_t[1];
+    q.fp_o0 = cc->fp_o[0]; q.fp_o1 = cc->fp_o[1];
+    q.fp_u0 = cc->fp_u[0]; q.fp_u1 = cc->fp_u[1];
+    q.fp_n0 = cc->fp_n[0]; q.fp_n1 = cc->fp_n[1];
     const double c_wskip = cc->wskip;
     TabRaw TR;
     const int nu = LSETS ? a.nsets * sr_units(RC) : 0;
@@ -1388,7 +1409,6 @@ __device__ __forceinline__ void scan_kernel_body(const ScanArgs& a) {
         const int i = min((int)threadIdx.x, a.B - 1);
         TR.r = ldd(a.r + i);
         TR.pos = (int32_t)ld32(a.posm + i);
-        TR.blm = (int32_t)ld32(a.blm + i);
         if (LSETS) TR.set = ldobj(a.setrec + ((int)threadIdx.x < nu ? (int)threadIdx.x : 0));
     }
     PartRaw<RC> A;
@@ -1512,6 +1532,9 @@ __device__ double incr_wskip(double rlo, double rhi, double thr, double avg, dou
     return ws * iav <= best ? ws : 0.0;
 }
 
+// the frozen average is folded again from scratch every FRZ_MAX steps (k_step's prep)
+constexpr int FRZ_MAX = 1024;
+
 #ifndef KB_SET_G
 #define KB_SET_G 2   // records a wave rebuilds at once in the fused prep (A/B: 2 beat 4 and 1 at c3)
 #endif
@@ -1594,6 +1617,9 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
     __shared__ uint64_t s_blmb[MB / 64], s_presb[MB / 64];
     __shared__ uint32_t s_smark[MAX_SETS / 32];
     __shared__ int s_nd[2], s_li[2], s_kfail[2];
+    __shared__ int s_fpfail, s_fpnsub;
+    __shared__ unsigned long long s_fpub[2];
+    __shared__ double s_fpz[6];
     Dedup T{s_key, s_wb, s_it, DEDUP_STEP, s_nd, s_li};
     const int B = a.B;
 
@@ -1609,6 +1635,203 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
             s_ord[b] = a.order[b];
         }
     };
+    // ---- deferred prep (DevCtl.fp, round 6).  The last step applied a plain move() replace
+    // and left the order work of its prep to this launch: the universe order after the move
+    // (its touched brokers re-sorted, getBL's (load, id) order, utils.go:107-117), the bl_move
+    // positions, the order certification, and the full records of the sets holding a touched
+    // broker (the last step wrote their certain prefix).  In k_pair it runs before the wait,
+    // beside the scan (whose workgroups patch the positions from the descriptor); the results
+    // stay in LDS (s_pm, s_rec, s_ord) and go to memory after the wait (flush_deferred: the
+    // scan reads posm / setrec while it runs).  The same phases as the prep below (P1-P5).
+    int32_t* s_pm = (int32_t*)(dsm + (a.fp_lds ? a.fp_lds : 0));          // bl position per broker
+    uint4* s_rec = (uint4*)(dsm + (a.fp_lds ? a.fp_lds + ((B * 4 + 15) & ~15) : 0));   // set records
+    Contender* s_bk = (Contender*)(s_rec + (a.fp_lds ? a.nsets : 0));   // the records' best keys (fp_bk)
+    int* s_dlist = (int*)s_smark;                    // sets rebuilt (free until the resolve's exact folds)
+    __shared__ int s_dp, s_dn, s_dpunc, s_dlight, s_dheavy, s_dwc[NW];
+    auto stage_fp = [&]() {                          // (fp_lds: the positions and the set records)
+        for (int b = tid; b < B; b += STEP_THREADS) s_pm[b] = (int32_t)ld32(a.posm + b);
+        for (int i = tid; i < a.nsets * a.units; i += STEP_THREADS) s_rec[i] = ldobj(a.setrec + i);
+    };
+    auto deferred_prep = [&](int t0, int t1) {
+        const int dnT = t1 >= 0 ? 2 : 1;
+        if (tid == 0) { s_T[0] = t0; s_T[1] = t1; s_dn = 0; s_dpunc = 0; s_cntT[0] = 0; s_cntT[1] = 0; }
+        __syncthreads();
+        // DP1: the touched brokers' old universe positions, the sets holding one (their records
+        // are rebuilt below), the bl_move bits by broker id
+        if (tid < dnT) s_fl[s_T[tid]] |= BF_TOUCHED;
+        for (int i = tid; i < B; i += STEP_THREADS) {
+            const int b = s_ord[i];
+            if (b == t0) s_posT[0] = i;
+            if (b == t1) s_posT[1] = i;
+        }
+        for (int set = tid; set < a.nsets; set += STEP_THREADS) {
+            const uint64_t* sb = s_sb + (size_t)set * a.W64;
+            bool hit = (sb[t0 >> 6] >> (t0 & 63)) & 1ull;
+            if (t1 >= 0) hit |= (sb[t1 >> 6] >> (t1 & 63)) & 1ull;
+            if (hit) s_dlist[atomicAdd(&s_dn, 1)] = set;     // (fp_lds: nsets <= 1024 words)
+        }
+        for (int b0 = wid * 64; b0 < B; b0 += STEP_THREADS) {
+            const int b = b0 + lane;
+            const bool in = b < B && (s_fl[b] & (BF_PRESENT | BF_INCFG));
+            const unsigned long long m = __ballot(in);
+            if (lane == 0) s_blmb[b0 >> 6] = m;
+        }
+        __syncthreads();
+        // DP2: per untouched element, new position = old - (touched before it) + (touched
+        // below it); for each touched broker the untouched ones below it
+        constexpr int NQD = (MB + STEP_THREADS - 1) / STEP_THREADS;
+        int nb[NQD], np[NQD];
+#pragma unroll
+        for (int q = 0; q < NQD; q++) {
+            nb[q] = -1; np[q] = 0;
+            if (q * STEP_THREADS >= B) continue;         // uniform
+            const int i = q * STEP_THREADS + tid;
+            const bool in = i < B;
+            const int b = in ? s_ord[i] : 0;
+            const bool untouched = in && !(s_fl[b] & BF_TOUCHED);
+            const double Lb = s_ld[b];
+            int below = 0, before = 0;
+            for (int x = 0; x < dnT; x++) {
+                const int t = s_T[x];
+                const double Lt = s_ld[t];
+                below += ((Lt < Lb) || (Lt == Lb && t < b)) ? 1 : 0;
+                before += s_posT[x] < i ? 1 : 0;
+                const bool b_lt_t = untouched && ((Lb < Lt) || (Lb == Lt && b < t));
+                const unsigned long long bal = __ballot(b_lt_t);
+                if (lane == 0 && bal) atomicAdd(&s_cntT[x], (int)__popcll(bal));
+            }
+            nb[q] = untouched ? b : -1;
+            np[q] = i - before + below;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < NQD; q++)
+            if (q * STEP_THREADS < B && nb[q] >= 0) s_ord[np[q]] = nb[q];
+        if (tid < dnT) {
+            const int t = s_T[tid];
+            const double Lt = s_ld[t];
+            int rank = 0;
+            for (int x = 0; x < dnT; x++) {
+                const int t2 = s_T[x];
+                const double L2 = s_ld[t2];
+                rank += ((L2 < Lt) || (L2 == Lt && t2 < t)) ? 1 : 0;
+            }
+            s_ord[s_cntT[tid] + rank] = t;
+        }
+        __syncthreads();
+        // DP3: bl_move positions along the new order (contiguous universe positions per
+        // thread, a workgroup prefix of the bl_move counts), the order certification (with
+        // approximate loads neighbours must be separated by more than their bounds), the
+        // lightest / heaviest bl_move brokers
+        {
+            constexpr int FQ = MB / STEP_THREADS;
+            int c = 0;
+            const int base = tid * FQ;
+            bool unc = false;
+#pragma unroll
+            for (int q = 0; q < FQ; q++) {
+                const int i = base + q;
+                if (i < B) {
+                    const int b = s_ord[i];
+                    c += (s_fl[b] & (BF_PRESENT | BF_INCFG)) ? 1 : 0;
+                    if (i + 1 < B) {
+                        const int b2 = s_ord[i + 1];
+                        const double e = s_e[b] + s_e[b2];
+                        unc |= e > 0.0 && !(s_ld[b2] - s_ld[b] > e);
+                    }
+                }
+            }
+            if (unc) s_dpunc = 1;
+            const int incl = wave_incl_scan(c);
+            if (lane == 63) s_dwc[wid] = incl;
+            __syncthreads();
+            const int wc = lane < NW ? s_dwc[lane] : 0;
+            const int woff = wave_sum(lane < wid ? wc : 0), total = wave_sum(wc);
+            int pos = woff + incl - c;
+#pragma unroll
+            for (int q = 0; q < FQ; q++) {
+                const int i = base + q;
+                if (i < B) {
+                    const int b = s_ord[i];
+                    if (s_fl[b] & (BF_PRESENT | BF_INCFG)) {
+                        if (pos == 0) s_dlight = b;
+                        if (pos == total - 1) s_dheavy = b;
+                        s_pm[b] = pos++;
+                    } else s_pm[b] = -1;
+                }
+            }
+        }
+        // DP4: the marked sets' records (the first KR brokers of set ∩ bl_move in the new bl
+        // order, steps.go:192-201 targets), two per wave so their LDS chains overlap
+        {
+            constexpr int G = KB_SET_G;
+            const int W64 = a.W64, KR = a.KR, U = a.units;
+            const unsigned long long lt = (1ull << lane) - 1ull;
+            const int mn = s_dn;
+            for (int g = wid * G; g < mn; g += NW * G) {
+                const int ng = mn - g < G ? mn - g : G;
+                const uint64_t* sb[G];
+                uint16_t* rec16[G];
+                int found[G];
+#pragma unroll
+                for (int j = 0; j < G; j++) {
+                    const int set = s_dlist[g + (j < ng ? j : 0)];
+                    sb[j] = s_sb + (size_t)set * W64;
+                    rec16[j] = (uint16_t*)(s_rec + (size_t)set * U);
+                    found[j] = j < ng ? 0 : KR;
+                }
+                for (int base = 0; base < B; base += 64) {
+                    bool need = false;
+#pragma unroll
+                    for (int j = 0; j < G; j++) need |= found[j] < KR;
+                    if (!need) break;
+                    const int k = base + lane;
+                    const int b = s_ord[k < B ? k : 0];
+                    const bool inb = k < B && ((s_blmb[b >> 6] >> (b & 63)) & 1ull);
+                    uint64_t wj[G];
+#pragma unroll
+                    for (int j = 0; j < G; j++) wj[j] = sb[j][b >> 6];
+#pragma unroll
+                    for (int j = 0; j < G; j++) {
+                        const bool mem = inb && ((wj[j] >> (b & 63)) & 1ull);
+                        const unsigned long long m = __ballot(mem);
+                        if (mem && found[j] < KR && j < ng) {
+                            const int rk = found[j] + (int)__popcll(m & lt);
+                            if (rk < KR) rec16[j][2 + rk] = (uint16_t)b;
+                        }
+                        found[j] += (int)__popcll(m);
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < G; j++) {
+                    if (j >= ng) break;
+                    for (int rk = found[j] + lane; rk < KR; rk += 64) rec16[j][2 + rk] = NONE16;
+                    // (|set ∩ bl_move|, rec16[0], is unchanged: a plain replace keeps bl_move)
+                    if (lane == 0) rec16[j][1] = (uint16_t)(found[j] < KR ? found[j] : KR);
+                }
+            }
+        }
+        if (tid < dnT) s_fl[s_T[tid]] &= ~BF_TOUCHED;
+        __syncthreads();
+    };
+    // the deferred prep's tables to memory (after the wait: the scan read the old ones)
+    auto flush_deferred = [&]() {
+        for (int i = tid; i < B; i += STEP_THREADS) {
+            const int b = s_ord[i];
+            a.order[i] = b;
+            a.posu[b] = i;
+            const int p = s_pm[i];
+            st32(a.posm + i, (uint32_t)p);
+            if (p >= 0) st32(a.blm + p, (uint32_t)i);
+        }
+        const int U = a.units, n = s_dn * U;
+        for (int q = tid; q < n; q += STEP_THREADS) {
+            const int j = q / U, u = q - j * U;
+            const int set = s_dlist[j];
+            stobj(a.setrec + (size_t)set * U + u, s_rec[(size_t)set * U + u]);
+        }
+    };
+    if (tid == 0) s_dp = 0;
     unsigned long long ts_b, ts_e, ts_pe;
     if constexpr (FUSED) {
         // k_pair's step workgroup (a resident workgroup of the scan's grid): the broker tables
@@ -1623,6 +1846,19 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
                 if (q + 1 < nq) *(uint4*)(s_sb + q) = *(const uint4*)(a.setbits + q);
                 else s_sb[q] = a.setbits[q];
             }
+        }
+        if (a.fp_lds) {
+            // this state's bl positions and set records (the fast prep's inputs); a deferred
+            // prep of the last move runs now, beside the scan (its control words do not change
+            // while the scan runs; with eager refolds the touched brokers' loads do: after the
+            // wait then)
+            stage_fp();
+            KB_STAMP(ctl, 7);
+            if (a.fuse_pre && !a.eager && ctl->fp && ctl->halted == H_RUN && !ctl->full_prep) {
+                deferred_prep(ctl->fp_t[0], ctl->fp_t[1]);
+                if (tid == 0) s_dp = 1;
+            }
+            KB_STAMP(ctl, 15);
         }
         __shared__ int s_prehalt;
         int egb = -1;
@@ -1705,6 +1941,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
         if (tid < CTL_WORDS) ((uint32_t*)&C)[tid] = ((const uint32_t*)ctl)[tid];
         if (s_prehalt == H_NEED_EXACT || !a.fuse_pre) stage_tables();
         else if (egb >= 0 && egb < B) { s_ld[egb] = a.load[egb]; s_e[egb] = a.eb[egb]; s_fl[egb] = a.bfl[egb]; }
+        if (s_dp) flush_deferred();
     } else {
     ts_b = ctl->ts_beg; ts_e = ctl->ts_end;         // (kernel timing, tk_on)
     ts_pe = ctl->ts_prev_end;
@@ -1755,6 +1992,28 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
     }
     if (tid < 2) { s_nd[tid] = 0; s_li[tid] = -1; s_kfail[tid] = 0; }
     __syncthreads();                               // the control block copy
+    if (a.fp_lds && !s_dp && C.fp && C.halted == H_RUN && !C.full_prep) {
+        // (a deferred prep still pending: k_step's two-launch path, or eager refolds that changed
+        // the touched brokers' loads while the scan ran)
+        if (!FUSED) stage_fp();
+        deferred_prep(C.fp_t[0], C.fp_t[1]);
+        flush_deferred();
+        if (tid == 0) s_dp = 1;
+        __syncthreads();
+    }
+    if (tid == 0 && (s_dp || C.fp)) {
+        // (a pending deferred prep skipped here was for a state a full prep rebuilds)
+        C.fp = 0;
+        if (s_dp) { C.light = s_dlight; C.heavy = s_dheavy; }
+    }
+    if (s_dp && s_dpunc) {
+        // the order after the last move is not certified by the load bounds: refold first
+        // (as the prep's own certification does)
+        __syncthreads();
+        if (tid == 0) { C.halted = H_NEED_EXACT; C.prepped = 0; C.total_exact_halts++; }
+        write_back();
+        return;
+    }
     {
         // this pair's first scan refolded the loads of a step halted for exact loads
         // (refresh_in_scan): resume as the host's refresh would, with a full prep
@@ -1808,6 +2067,8 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
     __shared__ int s_lrep[MAXR + 1];
     __shared__ unsigned long long s_lsb[MB / 64];
     if (tid == 0) { s_nT = 0; s_done = 0; s_exact_need = 0; s_retry = 0; s_moved = -1; s_lkind = 0; s_memb = 0; }
+    // (the fast prep's counters: the deferred prep and its flush are done with them)
+    if (tid == 0) { s_cntT[0] = 0; s_cntT[1] = 0; s_dn = 0; s_fpfail = 0; s_fpnsub = 0; s_fpub[0] = NONE64; s_fpub[1] = NONE64; }
     if (tid < NF) s_first[tid] = NONE32;
     if (tid < 2) { s_kc[tid] = 0; s_sok[tid] = -1; }   // (s_sok: -1 = no record offered its best key)
     if (halted != H_RUN) return;
@@ -1918,6 +2179,9 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
                 // is meaningful only then)
                 if (kc0 && hb0.s >= 0) { s_single[0] = hb0; s_sok[0] = cont_delta_ld(s_ld, hb0, inv_avg) <= g0 + 4.0 * eps; }
                 if (kc1 && hb1.s >= 0) { s_single[1] = hb1; s_sok[1] = cont_delta_ld(s_ld, hb1, inv_avg) <= g1 + 4.0 * eps; }
+                // (the fast prep's upper bound re-scores them after the apply: an LDS stash now,
+                // no second load from memory then)
+                if (a.fp_lds && a.fp_bk) { s_bk[2 * tid] = hb0; s_bk[2 * tid + 1] = hb1; }
             }
             kc0 = wave_sum(kc0); kc1 = wave_sum(kc1);
             if (lane == 0) {
@@ -2761,6 +3025,214 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
 #endif
     const int nT = s_nT;
     bool marked = false;                              // (unused: the fused path returns itself)
+    // ---- fast prep (round 6; DevCtl.fp): a plain move() replace -- frozen average, bl_move's
+    // membership unchanged, two touched brokers -- writes only what the next scan cannot derive
+    // and leaves the broker order, the positions and the full set records to the next launch's
+    // step workgroup (deferred_prep, before its wait, beside the scan):
+    //   FP1  the touched brokers' new bl positions (the bl_move brokers below each), the sets
+    //        holding one, r[] of the touched and the frozen totals (as the frozen prep below),
+    //        the upper bound from the records' best keys;
+    //   FP2  each marked set's record merged from its current one (LDS, s_rec): its untouched
+    //        members keep their order, the touched ones go in at their new positions; entries
+    //        up to the last untouched member are certain (a member past the record's end
+    //        could precede a touched broker inserted after it).  With <= 2 touched among KR = 6
+    //        listed, >= 4 = RC + 1 remain, so the scan's first target is right; walk_targets
+    //        continues in memory past a short record.  A set left with fewer certain members
+    //        sends the step to the full prep below instead.
+    if (FUSED && a.fp_ok && a.fp_lds && a.fp_bk && !full && do_res && D.status == 1 && D.kind == 1 &&
+        (D.step == 7 || D.step == 8) && !s_memb && nT >= 1 && nT <= 2 && C.frz_n > 0 && C.frz_n < FRZ_MAX &&
+        !a.eager && a.use_spill && !a.rebalance && !a.incr && !(KB_ABL & 32)) {
+        const int t0 = s_T[0], t1 = nT > 1 ? s_T[1] : -1;
+        const double iav = C.inv_avg;
+        // FP1 (the records' best keys first: their latency overlaps the counts)
+        const bool bkeys = tid < a.R.n;
+        Contender bk0, bk1;
+        bk0.s = bk1.s = -1;
+        if (bkeys) { bk0 = s_bk[2 * tid]; bk1 = s_bk[2 * tid + 1]; }   // (stashed with the headers)
+        const double L0 = s_ld[t0], L1 = t1 >= 0 ? s_ld[t1] : 0.0;
+        int c0 = 0, c1 = 0;
+        for (int b = tid; b < B; b += STEP_THREADS) {
+            const bool in = (s_fl[b] & (BF_PRESENT | BF_INCFG)) && b != t0 && b != t1;
+            const double Lb = s_ld[b];
+            c0 += in && (Lb < L0 || (Lb == L0 && b < t0)) ? 1 : 0;
+            c1 += in && t1 >= 0 && (Lb < L1 || (Lb == L1 && b < t1)) ? 1 : 0;
+        }
+        c0 = wave_sum(c0); c1 = wave_sum(c1);
+        if (lane == 0) { if (c0) atomicAdd(&s_cntT[0], c0); if (c1) atomicAdd(&s_cntT[1], c1); }
+        KB_STAMP(ctl, 9);
+        for (int set = tid; set < a.nsets; set += STEP_THREADS) {
+            const uint64_t* sb = s_sb + (size_t)set * a.W64;
+            bool hit = (sb[t0 >> 6] >> (t0 & 63)) & 1ull;
+            if (t1 >= 0) hit |= (sb[t1 >> 6] >> (t1 & 63)) & 1ull;
+            if (hit) s_dlist[atomicAdd(&s_dn, 1)] = set;
+        }
+        KB_STAMP(ctl, 16);
+        if (wid == 0) {
+            if (lane < nT) stdbl(a.r + s_T[lane], rel_ld(s_ld, s_T[lane], iav));
+            if (lane == 0) {
+                double dU = 0.0, aU = 0.0, dV = 0.0, dE = 0.0, rl = HUGE_VAL, rh = -HUGE_VAL;
+                for (int k = 0; k < nT; k++) {
+                    const int b = s_T[k];
+                    const double rn = rel_ld(s_ld, b, iav);
+                    const double ro = __fma_rn(s_Lold[k], iav, -1.0);   // the r[] the base wrote
+                    const double fn = fsq(rn), fo = fsq(ro);
+                    dU += fn - fo;
+                    aU += fn + fo;
+                    dV += fabs(rn) * (1.0 + fabs(rn)) - fabs(ro) * (1.0 + fabs(ro));
+                    dE += s_e[b] - s_ebold[k];
+                    rl = rn < rl ? rn : rl;
+                    rh = rn > rh ? rn : rh;
+                }
+                s_fpz[0] = dU; s_fpz[1] = aU; s_fpz[2] = dV; s_fpz[3] = dE; s_fpz[4] = rl; s_fpz[5] = rh;
+            }
+        }
+        KB_STAMP(ctl, 19);
+        if (bkeys || wid * 64 < a.R.n) {
+            // the best keys of every record but the moved partition's stay legal moves after a
+            // plain replace (keep_touched_keys), re-scored on the new loads
+            double ub0 = HUGE_VAL, ub1 = HUGE_VAL;
+            if (bkeys) {
+                const long long pm = s_moved;
+#pragma unroll
+                for (int k = 0; k < 2; k++) {
+                    const Contender& c = k ? bk1 : bk0;
+                    const bool keep = c.s >= 0 && (long long)(c.iter >> 21) != pm;
+                    if (a.ubdesc) {
+                        BlockDesc d;
+                        d.wmax = keep ? HUGE_VAL : -1.0;
+                        d.blk = keep ? (long long)(c.iter >> 21) / BLK : 0;
+                        stobj(a.ubdesc + 2 * tid + k, d);
+                        if (keep) atomicAdd(&s_fpnsub, 1);
+                    }
+                    if (!keep) continue;
+                    const double d2 = cont_delta_ld(s_ld, c, iav);
+                    if (k == 0) ub0 = d2 < ub0 ? d2 : ub0;
+                    else ub1 = d2 < ub1 ? d2 : ub1;
+                }
+            }
+            ub0 = wave_min(ub0); ub1 = wave_min(ub1);
+            if (lane == 0) { atomicMin(&s_fpub[0], enc(ub0)); atomicMin(&s_fpub[1], enc(ub1)); }
+        }
+        KB_STAMP(ctl, 20);
+        __syncthreads();                                // FP #1
+        KB_STAMP(ctl, 6);
+        // FP2: the touched brokers' bl positions before (s_pm: this state's) and after the move;
+        // u = the untouched bl_move brokers before each (the scan's patch, below)
+        const int o0 = s_pm[t0], o1 = t1 >= 0 ? s_pm[t1] : 0x7FFFFFFF;
+        const bool t1lt = t1 >= 0 && (L1 < L0 || (L1 == L0 && t1 < t0));
+        const int u0 = s_cntT[0], u1 = t1 >= 0 ? s_cntT[1] : 0x7FFFFFFF;
+        const int n0 = u0 + (t1lt ? 1 : 0), n1 = t1 >= 0 ? u1 + (t1lt ? 0 : 1) : 0x7FFFFFFF;
+        // (one record per thread: its 16-B unit and its members' positions in one LDS round trip
+        // each, the merge by counting -- every output index from comparisons, no serial walk)
+        const int nmk = s_dn, KR = a.KR;
+        for (int i = tid; i < nmk; i += STEP_THREADS) {
+            const int set = s_dlist[i];
+            const uint4 r4 = s_rec[set];                // (fp_lds: one 16-B unit per record)
+            const uint32_t wv[4] = {r4.x, r4.y, r4.z, r4.w};
+            const int nelig = (int)(wv[0] & 0xFFFFu), nl = (int)(wv[0] >> 16);
+            const uint64_t* sb = s_sb + (size_t)set * a.W64;
+            const bool in0 = (sb[t0 >> 6] >> (t0 & 63)) & 1ull;
+            const bool in1 = t1 >= 0 && ((sb[t1 >> 6] >> (t1 & 63)) & 1ull);
+            int e[6], pe[6];
+            bool v[6];
+#pragma unroll
+            for (int j = 0; j < 6; j++) {
+                e[j] = (int)((wv[1 + j / 2] >> (16 * (j & 1))) & 0xFFFFu);
+                v[j] = j < nl && e[j] != t0 && e[j] != t1;
+                pe[j] = s_pm[v[j] ? e[j] : 0];
+            }
+            int lastpe = -1, nv = 0;
+#pragma unroll
+            for (int j = 0; j < 6; j++) {
+                const int p = pe[j];
+                const int pc = p - (o0 < p ? 1 : 0) - (o1 < p ? 1 : 0);
+                pe[j] = pc + (u0 <= pc ? 1 : 0) + (u1 <= pc ? 1 : 0);
+                if (v[j]) { lastpe = pe[j]; nv++; }
+            }
+            // a touched member is certain when a listed untouched member follows it, or when
+            // the record listed the whole set
+            const bool all = nl >= nelig;
+            const bool c0 = in0 && (all || n0 < lastpe), c1 = in1 && (all || n1 < lastpe);
+            uint16_t out[6];
+#pragma unroll
+            for (int j = 0; j < 6; j++) out[j] = NONE16;
+            int kv = 0;
+#pragma unroll
+            for (int j = 0; j < 6; j++) {
+                const int idx = kv + (c0 && n0 < pe[j] ? 1 : 0) + (c1 && n1 < pe[j] ? 1 : 0);
+#pragma unroll
+                for (int q = 0; q < 6; q++) if (v[j] && idx == q) out[q] = (uint16_t)e[j];
+                kv += v[j] ? 1 : 0;
+            }
+            int i0 = 0, i1 = 0;
+#pragma unroll
+            for (int j = 0; j < 6; j++) { i0 += v[j] && pe[j] < n0 ? 1 : 0; i1 += v[j] && pe[j] < n1 ? 1 : 0; }
+            i0 += c1 && n1 < n0 ? 1 : 0;
+            i1 += c0 && n0 < n1 ? 1 : 0;
+#pragma unroll
+            for (int q = 0; q < 6; q++) {
+                if (c0 && i0 == q) out[q] = (uint16_t)t0;
+                if (c1 && i1 == q) out[q] = (uint16_t)t1;
+            }
+            const int no = nv + (c0 ? 1 : 0) + (c1 ? 1 : 0);
+            const int nn = no < KR ? no : KR;
+            const int kt = a.RC + 1 < nelig ? a.RC + 1 : nelig;
+            if (nn < kt) { s_fpfail = 1; continue; }
+            uint4 rec;
+            rec.x = (uint32_t)nelig | ((uint32_t)nn << 16);
+            rec.y = (uint32_t)out[0] | ((uint32_t)out[1] << 16);
+            rec.z = (uint32_t)out[2] | ((uint32_t)out[3] << 16);
+            rec.w = (uint32_t)out[4] | ((uint32_t)out[5] << 16);
+            stobj(a.setrec + set, rec);
+        }
+        KB_STAMP(ctl, 0);
+        __syncthreads();                                // FP #2
+        KB_STAMP(ctl, 8);
+        if (!s_fpfail) {
+            if (tid == 0) {
+                const double uu = DBL_EPSILON / 2;
+                const double S = C.S, avg = C.avg, U0 = C.U0 + s_fpz[0];
+                const int nblm = C.nblm;
+                const double uerr = C.uerr + 8.0 * uu * (fabs(C.U0) + fabs(U0) + s_fpz[1]);
+                const double V = (C.V + s_fpz[2]) * (1.0 + 8.0 * uu);
+                const double E = (C.E + s_fpz[3]) * (1.0 + 8.0 * uu);
+                const double Rm = fmax(C.rm_bound, fmax(fabs(s_fpz[4]), fabs(s_fpz[5])));
+                const double u = DBL_EPSILON / 2;
+                const double n = (double)nblm;
+                const double R = Rm + a.wmax * iav;
+                const double Ea = E * iav;
+                const double epsf = 64.0 * u * ((n + 8.0) * (U0 + 2.0 * V) + 4.0 * (1.0 + R) * (1.0 + R));
+                const double epsl = 16.0 * Ea * (V / (n > 0 ? n : 1.0) + R + 1.0) + 4.0 * Ea * Ea;
+                double ep = 2.0 * (epsf + epsl) + uerr;
+                if (!(ep > 1e-300)) ep = 1e-300;
+                C.rlo = fmin(C.rlo, s_fpz[4]); C.rhi = fmax(C.rhi, s_fpz[5]);
+                C.incr_ok = 0; C.wskip = 0.0;
+                C.ub_sub = a.ubdesc && a.R.n <= STEP_THREADS && (s_fpnsub > 0 || a.ub_heavy) ? 1 : 0;
+                C.S = S; C.avg = avg; C.U0 = U0; C.V = V; C.eps = ep; C.E = E;
+                C.uerr = uerr; C.rm_bound = Rm;
+                C.frz_n = C.frz_n + 1;
+                C.ub[0] = s_fpub[0] == NONE64 ? HUGE_VAL : dec(s_fpub[0]);
+                C.ub[1] = s_fpub[1] == NONE64 ? HUGE_VAL : dec(s_fpub[1]);
+                C.want_refresh = (epsl > epsf || C.ndirty >= 256) ? 1 : 0;
+                C.ncont = 0;
+                C.cont_overflow = 0;
+                C.fp = 1;
+                C.fp_t[0] = t0; C.fp_t[1] = t1;
+                C.fp_o[0] = o0; C.fp_o[1] = o1;
+                C.fp_n[0] = n0; C.fp_n[1] = n1;
+                C.fp_u[0] = u0; C.fp_u[1] = u1;
+                C.prepped = 1; C.full_prep = 0;
+                C.total_fp++;
+            }
+            KB_STAMP(ctl, 10);
+            write_back();
+            return;
+        }
+        // (a set left with too short a certain prefix: the full prep below; the records FP2
+        // wrote are rewritten there, the r[] it wrote are the same values)
+        if (tid == 0) { s_cntT[0] = 0; s_cntT[1] = 0; }
+        __syncthreads();
+    }
     if (!GB && !full && a.sb_lds) {
         // ---- fused incremental prep, wave-specialised.  A wave reduction of a double
         // costs ~340 clocks when all 16 waves run one (four per SIMD, issue-bound) and
@@ -2780,7 +3252,6 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
         // broker and their reductions are skipped).  eps doubles (the frozen fold's rounding
         // next to a fresh fold's) plus uerr, the rounding of the incremental U0 updates.  A
         // full recompute every FRZ_MAX steps, after a membership change and after a full prep.
-        constexpr int FRZ_MAX = 1024;
         // (replace / swap keep the real load sum: the weight changes brokers; a remove or an
         // add changes it, and then the sums are folded again)
         const bool frz = do_res && D.status == 1 && (D.kind == 1 || D.kind == 4) && !s_memb && C.frz_n > 0 &&

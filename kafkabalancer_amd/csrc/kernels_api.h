@@ -124,6 +124,11 @@ struct StepArgs {
     int wait_n;               //    grid's other workgroups), then resets it
     int fuse_pre;             // k_pair: stage the broker tables before the wait (diagnostic 0: after)
     unsigned long long wait_ticks;   // k_pair: the wait's bound (100 MHz ticks; 2 s, tests: 0)
+    // deferred prep (DevCtl.fp): fp_lds > 0 = the byte offset of its LDS region in the dynamic
+    // LDS (bl positions int32[B], then the set records uint4[nsets * units]); fp_ok = a step may
+    // leave its prep deferred (engine.cpp decides; a pending one is finished whenever fp_lds > 0)
+    int fp_lds, fp_ok;
+    int fp_bk;                // 1: the fp region also holds the records' best keys (2 per record)
 };
 
 

@@ -67,7 +67,7 @@ class kb_stats(C.Structure):
                 ("scan_workgroups", C.c_int64), ("retries", C.c_int64), ("spill_grows", C.c_int64),
                 ("blocks_scanned", C.c_int64), ("relists", C.c_int64),
                 ("fused_pairs", C.c_int64), ("fused_summaries", C.c_int64),
-                ("eager", C.c_int64), ("eager_switches", C.c_int64)]
+                ("eager", C.c_int64), ("eager_switches", C.c_int64), ("fast_preps", C.c_int64)]
 
 
 _lib = None
@@ -149,7 +149,7 @@ def lib():
         if hasattr(L, "kb_engine_set_incremental"):
             L.kb_engine_set_incremental.argtypes = [vp, C.c_int32]
             L.kb_engine_set_incremental.restype = C.c_int
-        if L.kb_abi_version() != 10 and not any_abi:
+        if L.kb_abi_version() != 11 and not any_abi:
             raise ImportError("libkbengine.so ABI mismatch")
         # the library's A/B and diagnostic switches (KB_FUSE, KB_EAGER, ...) are read from the
         # environment only after this opt-in (include/kbengine.h); the tests and the bench

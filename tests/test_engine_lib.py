@@ -25,7 +25,7 @@ def test_library_exports_header():
 
 
 def test_abi_version():
-    assert E.lib().kb_abi_version() == 10
+    assert E.lib().kb_abi_version() == 11
 
 
 def test_library_is_gfx950_code_object():

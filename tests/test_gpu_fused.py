@@ -262,3 +262,30 @@ print(json.dumps({"n": len(got), "equal": [key(c) for c in got[:30]] == [key(c) 
     assert r.returncode == 0, (r.returncode, r.stderr[-3000:])
     res = json.loads(r.stdout.strip().splitlines()[-1])
     assert res["err"] is None and res["n"] >= 30 and res["equal"], res
+
+
+def _run_env(cl, cfg, steps, env):
+    eng = _with_env(*env, lambda: E.Engine(cl, cfg))
+    changes, err = eng.plan(steps)
+    st = eng.stats()
+    loads = eng.loads()
+    eng.close()
+    return changes, err, st, loads
+
+
+# (full size: the pair is fused at full tiles; c3 -- the headline's leader 2-cycle -- and c3nl
+# -- a different partition almost every step)
+@pytest.mark.parametrize("name,allow_leader,steps", [("c3", True, 300), ("c3", False, 300)])
+def test_fast_prep_matches_full_prep(name, allow_leader, steps):
+    """The deferred prep (DevCtl.fp: the order, the positions and the set records of a plain
+    move left to the next launch's step workgroup, the scan patching the positions) gives the
+    plans and the device state of the full prep every step (KB_FP=0): every change with its
+    su / cu bits, every broker load; and it is the path the plan took."""
+    cl, cfg, _ = synth.config(name, scale=1.0)
+    cfg = dict(cfg, allow_leader=allow_leader)
+    a = _run_env(cl, cfg, steps, ("KB_FP", "1"))
+    b = _run_env(cl, cfg, steps, ("KB_FP", "0"))
+    assert a[1] is None and b[1] is None
+    assert keyed(a[0]) == keyed(b[0])
+    assert a[3] == b[3]
+    assert a[2]["fast_preps"] > steps // 2 and b[2]["fast_preps"] == 0, (a[2]["fast_preps"], b[2]["fast_preps"])
