@@ -293,6 +293,26 @@ def drop_in(args):
                           " " + " ".join(cmd[1:2] + ["-input", "<%.0f MB JSON>" % (ph["input_bytes"] / 1e6)] + cmd[4:]),
                           json_generation_s=gen_s,
                           plan_ms_per_change=1e3 * ph["plan_s"] / max(ph["changes"], 1))
+        # the reference's default -complete-partition=true (balancer.go:30): past -max-reassign
+        # the loop goes on while the change stays on the last partition, and the first change
+        # elsewhere (the probe) ends it -- kb_engine_plan_until batches; with -allow-leader
+        # the leader 2-cycle of SURVEY 3.4 never ends it (the reference loops forever, the
+        # CLI exits 5 after max-reassign + 1e6 steps), so that case is not timed
+        if cfg.get("allow_leader"):
+            out["cli_default_flags"] = {"skipped": "-allow-leader: the leader 2-cycle never completes the "
+                                                   "partition (the reference loops forever)"}
+        else:
+            cmd_d = [c for c in cmd if c != "-complete-partition=false"]
+            t0 = time.perf_counter()
+            r = subprocess.run(cmd_d, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=600)
+            wall_d = time.perf_counter() - t0
+            assert r.returncode == 0, r.stderr[-2000:]
+            with open(tpath) as f:
+                ph_d = json.loads(f.read().splitlines()[-1])
+            out["cli_default_flags"] = dict(ph_d, wall_s=wall_d,
+                                            plan_ms_per_change=1e3 * ph_d["plan_s"] / max(ph_d["changes"], 1),
+                                            vs_plan_per_step=(ph_d["plan_s"] / max(ph_d["changes"], 1)) /
+                                            max(plan_step, 1e-12))
     finally:
         for q in (jpath, tpath):
             if os.path.exists(q):

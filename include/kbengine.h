@@ -198,6 +198,13 @@ int kb_engine_step(kb_engine *e, uint32_t step_mask, kb_change *out);
  * Writes the changes to out[0..*n_out).  Returns the last status. */
 int kb_engine_plan(kb_engine *e, int64_t max_steps, kb_change *out, int64_t *n_out);
 
+/* kb_engine_plan that also stops after the first applied change whose partition is not
+ * stop_part (that change is applied and returned last): run()'s -complete-partition loop
+ * (kafkabalancer.go:193-221) -- past -max-reassign the reference keeps calling Balance() while
+ * the change is on the completing partition, and the first change that does not compare ends
+ * the loop (applied: the probe).  stop_part < 0: kb_engine_plan.  (ABI 11) */
+int kb_engine_plan_until(kb_engine *e, int64_t max_steps, int64_t stop_part, kb_change *out, int64_t *n_out);
+
 /* Current replicas of partition i (after applied changes); returns the count. */
 int64_t kb_engine_replicas(kb_engine *e, int64_t i, int64_t *buf, int64_t cap);
 

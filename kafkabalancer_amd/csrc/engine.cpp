@@ -113,6 +113,7 @@ struct kb_engine {
     bool eager_auto = false;          // lazy loads now; eager refolds once exact halts are frequent
     int64_t eager_switches = 0;
     int fp_lds = 0;                 // deferred prep: byte offset of its region in k_step's LDS (0: none)
+    int64_t stop_part = -1;         // kb_engine_plan_until's partition for the plan running now
     int fp_bk = 0;                  // ... which also holds the records' best keys
     // the halt rate's window: the steps and exact halts at the checkpoint before last (w0)
     // and at the last one (w1), checkpoints at least 64 steps apart
@@ -843,6 +844,7 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
     memset(&z, 0, sizeof z);
     z.logcap = e->logcap;
     z.full_prep = 1;
+    z.stop_part = -1;
     z.tk_on = e->time_kernels;
     z.step_mask = SM_ALL;
     z.ts_beg = NONE64;
@@ -1141,6 +1143,7 @@ static int reset_ctl(kb_engine* e, int64_t budget_steps) {
     c.halted = H_RUN;
     c.logpos = 0;
     c.logcap = e->logcap;
+    c.stop_part = e->stop_part;
     c.step_mask = e->step_mask;
     if (!e->reuse_now) { c.ncont = 0; c.cont_overflow = 0; }   // (a scan runs first: an empty spill)
     e->recs_fresh = false;
@@ -1404,6 +1407,7 @@ static int run_steps(kb_engine* e, int64_t max_steps) {
         else if (c.steps - st0 >= pairs - 1)
             e->batch = std::min(kStepBatch, 2 * e->batch);
         if (c.halted == H_DONE) break;
+        if (c.steps >= c.budget) break;              // (kb_engine_plan_until's stop, whatever the halt)
         if (c.halted == H_NEED_SPILL) {
             // more near-tied candidates than the spill buffer holds: grow it, run the step again
             const int rc = grow_spill(e);
@@ -1513,14 +1517,31 @@ extern "C" int kb_engine_plan(kb_engine* e, int64_t max_steps, kb_change* out, i
         const double t_c0 = now_us();
         for (int64_t i = 0; i < nlog; i++) {         // (run_steps copied the log entries)
             kb_change tmp;
-            rc = convert(e, e->h_log[i], out ? &out[k] : &tmp);
+            kb_change* o = out ? &out[k] : &tmp;
+            rc = convert(e, e->h_log[i], o);
             k++;
             if (rc != KB_CHANGE) { *n_out = k; e->host_us[3] += now_us() - t_c0; return rc; }
+            if (e->stop_part >= 0 && o->partition != e->stop_part) {   // (kb_engine_plan_until)
+                *n_out = k; e->host_us[3] += now_us() - t_c0; return rc;
+            }
         }
         e->host_us[3] += now_us() - t_c0;
         if (nlog < m) break;
     }
     *n_out = k;
+    return rc;
+}
+
+// run()'s -complete-partition loop device-resident (kafkabalancer.go:193-221): once
+// -max-reassign changes are out, the reference keeps calling Balance() while the change is on
+// the completing partition and stops after the first one that is not (it is applied: the
+// probe).  The same as kb_engine_plan with that stop on the device: 64 steps per host round
+// trip instead of one Balance() call per change.
+extern "C" int kb_engine_plan_until(kb_engine* e, int64_t max_steps, int64_t stop_part, kb_change* out, int64_t* n_out) {
+    if (!e || !n_out || max_steps < 0) return KB_ERR_INVALID;
+    e->stop_part = stop_part < 0 ? -1 : stop_part;
+    const int rc = kb_engine_plan(e, max_steps, out, n_out);
+    e->stop_part = -1;
     return rc;
 }
 

@@ -259,6 +259,10 @@ struct DevCtl {
     int32_t fp, fp_pad;
     int32_t fp_t[2], fp_o[2], fp_n[2], fp_u[2];
     unsigned long long total_fp;    // steps that took the fast prep
+    // kb_engine_plan_until: the plan ends after the first applied change whose partition is
+    // not stop_part (-1: no such stop) -- run()'s -complete-partition loop (kafkabalancer.go:
+    // 193-221: the probe change that does not compare is applied, then the loop ends)
+    long long stop_part;
     // diagnostic phase stamps (builds with -DKB_STAMPS): accumulated
     // shader-clock ticks (clock64) per phase of k_step; [24]/[25] the wall-clock
     // (100 MHz) and shader-clock length of k_step; [26] one stamp's own cost

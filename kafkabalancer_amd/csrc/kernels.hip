@@ -1532,6 +1532,9 @@ __device__ double incr_wskip(double rlo, double rhi, double thr, double avg, dou
     return ws * iav <= best ? ws : 0.0;
 }
 
+#ifndef KB_FPABL
+#define KB_FPABL 0   // diagnostic timing builds of the fast prep (1: no merge, 2: no counts / marks)
+#endif
 // the frozen average is folded again from scratch every FRZ_MAX steps (k_step's prep)
 constexpr int FRZ_MAX = 1024;
 
@@ -1619,7 +1622,8 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
     __shared__ int s_nd[2], s_li[2], s_kfail[2];
     __shared__ int s_fpfail, s_fpnsub;
     __shared__ unsigned long long s_fpub[2];
-    __shared__ double s_fpz[6];
+    __shared__ double s_fpz[9];
+    __shared__ __align__(16) uint16_t s_mrow[NW][8];   // the fast prep's merged records, one row per wave
     Dedup T{s_key, s_wb, s_it, DEDUP_STEP, s_nd, s_li};
     const int B = a.B;
 
@@ -2976,6 +2980,10 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
             if (C.logpos < C.logcap) a.log[C.logpos] = ch;
             C.logpos++;
             C.steps++;
+            // (kb_engine_plan_until: a change on another partition ends the plan after it; the
+            // budget goes too, so no later launch of the batch -- a refresh's resumed prep
+            // included -- takes another step)
+            if (D.status == 1 && C.stop_part >= 0 && D.part != C.stop_part) { C.budget = C.steps; C.halted = H_DONE; }
             // reference candidate count of the steps that actually ran this iteration
             unsigned long long add = 0;
             if (D.step < 0 || D.step >= 7) {
@@ -3044,32 +3052,32 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
         !a.eager && a.use_spill && !a.rebalance && !a.incr && !(KB_ABL & 32)) {
         const int t0 = s_T[0], t1 = nT > 1 ? s_T[1] : -1;
         const double iav = C.inv_avg;
-        // FP1 (the records' best keys first: their latency overlaps the counts)
-        const bool bkeys = tid < a.R.n;
-        Contender bk0, bk1;
-        bk0.s = bk1.s = -1;
-        if (bkeys) { bk0 = s_bk[2 * tid]; bk1 = s_bk[2 * tid + 1]; }   // (stashed with the headers)
+        // FP1, one job per group of waves so that no wave runs two of them in series (the barrier
+        // waits for the slowest): waves 0-3 the upper bound (records 0..255, then every 256th),
+        // wave 4 the frozen totals and eps (lane 0), waves 8-15 the counts and the marks
         const double L0 = s_ld[t0], L1 = t1 >= 0 ? s_ld[t1] : 0.0;
-        int c0 = 0, c1 = 0;
-        for (int b = tid; b < B; b += STEP_THREADS) {
-            const bool in = (s_fl[b] & (BF_PRESENT | BF_INCFG)) && b != t0 && b != t1;
-            const double Lb = s_ld[b];
-            c0 += in && (Lb < L0 || (Lb == L0 && b < t0)) ? 1 : 0;
-            c1 += in && t1 >= 0 && (Lb < L1 || (Lb == L1 && b < t1)) ? 1 : 0;
-        }
-        c0 = wave_sum(c0); c1 = wave_sum(c1);
-        if (lane == 0) { if (c0) atomicAdd(&s_cntT[0], c0); if (c1) atomicAdd(&s_cntT[1], c1); }
-        KB_STAMP(ctl, 9);
-        for (int set = tid; set < a.nsets; set += STEP_THREADS) {
-            const uint64_t* sb = s_sb + (size_t)set * a.W64;
-            bool hit = (sb[t0 >> 6] >> (t0 & 63)) & 1ull;
-            if (t1 >= 0) hit |= (sb[t1 >> 6] >> (t1 & 63)) & 1ull;
-            if (hit) s_dlist[atomicAdd(&s_dn, 1)] = set;
-        }
-        KB_STAMP(ctl, 16);
-        if (wid == 0) {
+        if (wid >= 8) {
+            const int t8 = tid - 8 * 64;
+            int c0 = 0, c1 = 0;
+            for (int b = t8; b < ((KB_FPABL & 2) ? 0 : B); b += STEP_THREADS - 8 * 64) {   // (KB_FPABL: timing only)
+                const bool in = (s_fl[b] & (BF_PRESENT | BF_INCFG)) && b != t0 && b != t1;
+                const double Lb = s_ld[b];
+                c0 += in && (Lb < L0 || (Lb == L0 && b < t0)) ? 1 : 0;
+                c1 += in && t1 >= 0 && (Lb < L1 || (Lb == L1 && b < t1)) ? 1 : 0;
+            }
+            for (int set = t8; set < ((KB_FPABL & 2) ? 0 : a.nsets); set += STEP_THREADS - 8 * 64) {
+                const uint64_t* sb = s_sb + (size_t)set * a.W64;
+                bool hit = (sb[t0 >> 6] >> (t0 & 63)) & 1ull;
+                if (t1 >= 0) hit |= (sb[t1 >> 6] >> (t1 & 63)) & 1ull;
+                if (hit) s_dlist[atomicAdd(&s_dn, 1)] = set;
+            }
+            c0 = wave_sum(c0); c1 = wave_sum(c1);
+            if (lane == 0) { if (c0) atomicAdd(&s_cntT[0], c0); if (c1) atomicAdd(&s_cntT[1], c1); }
+        } else if (wid == 4) {
             if (lane < nT) stdbl(a.r + s_T[lane], rel_ld(s_ld, s_T[lane], iav));
             if (lane == 0) {
+                // the frozen totals after the move (as the frozen prep below: the base's sum and
+                // average, the touched brokers' increments, each bound grown by a few ulps) and eps
                 double dU = 0.0, aU = 0.0, dV = 0.0, dE = 0.0, rl = HUGE_VAL, rh = -HUGE_VAL;
                 for (int k = 0; k < nT; k++) {
                     const int b = s_T[k];
@@ -3083,35 +3091,54 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
                     rl = rn < rl ? rn : rl;
                     rh = rn > rh ? rn : rh;
                 }
-                s_fpz[0] = dU; s_fpz[1] = aU; s_fpz[2] = dV; s_fpz[3] = dE; s_fpz[4] = rl; s_fpz[5] = rh;
+                const double uu = DBL_EPSILON / 2;
+                const double U0 = C.U0 + dU;
+                const double uerr = C.uerr + 8.0 * uu * (fabs(C.U0) + fabs(U0) + aU);
+                const double V = (C.V + dV) * (1.0 + 8.0 * uu);
+                const double E = (C.E + dE) * (1.0 + 8.0 * uu);
+                const double Rm = fmax(C.rm_bound, fmax(fabs(rl), fabs(rh)));
+                const double n = (double)C.nblm;
+                const double R = Rm + a.wmax * iav;
+                const double Ea = E * iav;
+                const double epsf = 64.0 * uu * ((n + 8.0) * (U0 + 2.0 * V) + 4.0 * (1.0 + R) * (1.0 + R));
+                const double epsl = 16.0 * Ea * (V / (n > 0 ? n : 1.0) + R + 1.0) + 4.0 * Ea * Ea;
+                double ep = 2.0 * (epsf + epsl) + uerr;
+                if (!(ep > 1e-300)) ep = 1e-300;
+                s_fpz[0] = U0; s_fpz[1] = uerr; s_fpz[2] = V; s_fpz[3] = E; s_fpz[4] = rl; s_fpz[5] = rh;
+                s_fpz[6] = Rm; s_fpz[7] = ep; s_fpz[8] = epsl > epsf ? 1.0 : 0.0;
             }
-        }
-        KB_STAMP(ctl, 19);
-        if (bkeys || wid * 64 < a.R.n) {
+        } else if (wid < 4) {
             // the best keys of every record but the moved partition's stay legal moves after a
             // plain replace (keep_touched_keys), re-scored on the new loads
             double ub0 = HUGE_VAL, ub1 = HUGE_VAL;
-            if (bkeys) {
-                const long long pm = s_moved;
+            int nkeep = 0;
+            const long long pm = s_moved;
+            for (int i = tid; i < a.R.n; i += 4 * 64) {
+                const Contender bk[2] = {s_bk[2 * i], s_bk[2 * i + 1]};   // (stashed with the headers)
 #pragma unroll
                 for (int k = 0; k < 2; k++) {
-                    const Contender& c = k ? bk1 : bk0;
+                    const Contender& c = bk[k];
                     const bool keep = c.s >= 0 && (long long)(c.iter >> 21) != pm;
                     if (a.ubdesc) {
                         BlockDesc d;
                         d.wmax = keep ? HUGE_VAL : -1.0;
                         d.blk = keep ? (long long)(c.iter >> 21) / BLK : 0;
-                        stobj(a.ubdesc + 2 * tid + k, d);
-                        if (keep) atomicAdd(&s_fpnsub, 1);
+                        stobj(a.ubdesc + 2 * i + k, d);
                     }
+                    nkeep += keep ? 1 : 0;
                     if (!keep) continue;
                     const double d2 = cont_delta_ld(s_ld, c, iav);
                     if (k == 0) ub0 = d2 < ub0 ? d2 : ub0;
                     else ub1 = d2 < ub1 ? d2 : ub1;
                 }
             }
+            // (one LDS atomic per wave: same-address atomics of a whole wave serialise)
             ub0 = wave_min(ub0); ub1 = wave_min(ub1);
-            if (lane == 0) { atomicMin(&s_fpub[0], enc(ub0)); atomicMin(&s_fpub[1], enc(ub1)); }
+            nkeep = wave_sum(nkeep);
+            if (lane == 0) {
+                atomicMin(&s_fpub[0], enc(ub0)); atomicMin(&s_fpub[1], enc(ub1));
+                if (a.ubdesc && nkeep) atomicAdd(&s_fpnsub, nkeep);
+            }
         }
         KB_STAMP(ctl, 20);
         __syncthreads();                                // FP #1
@@ -3122,98 +3149,70 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
         const bool t1lt = t1 >= 0 && (L1 < L0 || (L1 == L0 && t1 < t0));
         const int u0 = s_cntT[0], u1 = t1 >= 0 ? s_cntT[1] : 0x7FFFFFFF;
         const int n0 = u0 + (t1lt ? 1 : 0), n1 = t1 >= 0 ? u1 + (t1lt ? 0 : 1) : 0x7FFFFFFF;
-        // (one record per thread: its 16-B unit and its members' positions in one LDS round trip
-        // each, the merge by counting -- every output index from comparisons, no serial walk)
-        const int nmk = s_dn, KR = a.KR;
-        for (int i = tid; i < nmk; i += STEP_THREADS) {
-            const int set = s_dlist[i];
+        // (one wave per marked set, one lane per listed member: its position and its output index
+        // by ballots -- no serial merge in one lane)
+        const int nmk = (KB_FPABL & 1) ? 0 : s_dn, KR = a.KR;
+        const unsigned long long ltm = (1ull << lane) - 1ull;
+        for (int g = wid; g < nmk; g += NW) {
+            const int set = s_dlist[g];
             const uint4 r4 = s_rec[set];                // (fp_lds: one 16-B unit per record)
-            const uint32_t wv[4] = {r4.x, r4.y, r4.z, r4.w};
-            const int nelig = (int)(wv[0] & 0xFFFFu), nl = (int)(wv[0] >> 16);
+            const int nelig = (int)(r4.x & 0xFFFFu), nl = (int)(r4.x >> 16);
             const uint64_t* sb = s_sb + (size_t)set * a.W64;
             const bool in0 = (sb[t0 >> 6] >> (t0 & 63)) & 1ull;
             const bool in1 = t1 >= 0 && ((sb[t1 >> 6] >> (t1 & 63)) & 1ull);
-            int e[6], pe[6];
-            bool v[6];
-#pragma unroll
-            for (int j = 0; j < 6; j++) {
-                e[j] = (int)((wv[1 + j / 2] >> (16 * (j & 1))) & 0xFFFFu);
-                v[j] = j < nl && e[j] != t0 && e[j] != t1;
-                pe[j] = s_pm[v[j] ? e[j] : 0];
-            }
-            int lastpe = -1, nv = 0;
-#pragma unroll
-            for (int j = 0; j < 6; j++) {
-                const int p = pe[j];
-                const int pc = p - (o0 < p ? 1 : 0) - (o1 < p ? 1 : 0);
-                pe[j] = pc + (u0 <= pc ? 1 : 0) + (u1 <= pc ? 1 : 0);
-                if (v[j]) { lastpe = pe[j]; nv++; }
-            }
-            // a touched member is certain when a listed untouched member follows it, or when
-            // the record listed the whole set
+            const int j = lane < 6 ? lane : 5;
+            const uint32_t wj = j < 2 ? r4.y : (j < 4 ? r4.z : r4.w);
+            const int e = (int)((wj >> (16 * (j & 1))) & 0xFFFFu);
+            const bool v = lane < 6 && lane < nl && e != t0 && e != t1;
+            const int p = s_pm[v ? e : 0];
+            const int pc = p - (o0 < p ? 1 : 0) - (o1 < p ? 1 : 0);
+            const int pe = pc + (u0 <= pc ? 1 : 0) + (u1 <= pc ? 1 : 0);
+            const unsigned long long vm = __ballot(v);
+            const int nv = (int)__popcll(vm);
+            const int lastpe = vm ? __shfl(pe, 63 - __clzll(vm)) : -1;
+            // a touched member is certain when a listed untouched member follows it, or when the
+            // record listed the whole set
             const bool all = nl >= nelig;
             const bool c0 = in0 && (all || n0 < lastpe), c1 = in1 && (all || n1 < lastpe);
-            uint16_t out[6];
-#pragma unroll
-            for (int j = 0; j < 6; j++) out[j] = NONE16;
-            int kv = 0;
-#pragma unroll
-            for (int j = 0; j < 6; j++) {
-                const int idx = kv + (c0 && n0 < pe[j] ? 1 : 0) + (c1 && n1 < pe[j] ? 1 : 0);
-#pragma unroll
-                for (int q = 0; q < 6; q++) if (v[j] && idx == q) out[q] = (uint16_t)e[j];
-                kv += v[j] ? 1 : 0;
-            }
-            int i0 = 0, i1 = 0;
-#pragma unroll
-            for (int j = 0; j < 6; j++) { i0 += v[j] && pe[j] < n0 ? 1 : 0; i1 += v[j] && pe[j] < n1 ? 1 : 0; }
-            i0 += c1 && n1 < n0 ? 1 : 0;
-            i1 += c0 && n0 < n1 ? 1 : 0;
-#pragma unroll
-            for (int q = 0; q < 6; q++) {
-                if (c0 && i0 == q) out[q] = (uint16_t)t0;
-                if (c1 && i1 == q) out[q] = (uint16_t)t1;
-            }
             const int no = nv + (c0 ? 1 : 0) + (c1 ? 1 : 0);
             const int nn = no < KR ? no : KR;
             const int kt = a.RC + 1 < nelig ? a.RC + 1 : nelig;
-            if (nn < kt) { s_fpfail = 1; continue; }
-            uint4 rec;
-            rec.x = (uint32_t)nelig | ((uint32_t)nn << 16);
-            rec.y = (uint32_t)out[0] | ((uint32_t)out[1] << 16);
-            rec.z = (uint32_t)out[2] | ((uint32_t)out[3] << 16);
-            rec.w = (uint32_t)out[4] | ((uint32_t)out[5] << 16);
-            stobj(a.setrec + set, rec);
+            if (nn < kt) { if (lane == 0) s_fpfail = 1; continue; }
+            uint16_t* row = &s_mrow[wid][0];
+            if (lane < 8) row[lane] = NONE16;
+            __builtin_amdgcn_wave_barrier();
+            const int idx = (int)__popcll(vm & ltm) + (c0 && n0 < pe ? 1 : 0) + (c1 && n1 < pe ? 1 : 0);
+            if (v && idx < 6) row[2 + idx] = (uint16_t)e;
+            const int i0 = (int)__popcll(__ballot(v && pe < n0)) + (c1 && n1 < n0 ? 1 : 0);
+            const int i1 = (int)__popcll(__ballot(v && pe < n1)) + (c0 && n0 < n1 ? 1 : 0);
+            if (lane == 0) {
+                if (c0 && i0 < 6) row[2 + i0] = (uint16_t)t0;
+                if (c1 && i1 < 6) row[2 + i1] = (uint16_t)t1;
+                row[0] = (uint16_t)nelig;
+                row[1] = (uint16_t)nn;
+            }
+            __builtin_amdgcn_wave_barrier();
+            if (lane == 0) {
+                uint4 rec = *(const uint4*)row;
+                // (entries past nn: NONE16 -- the row held NONE16 before the writes, and nn <= KR)
+                stobj(a.setrec + set, rec);
+            }
+            __builtin_amdgcn_wave_barrier();
         }
         KB_STAMP(ctl, 0);
         __syncthreads();                                // FP #2
         KB_STAMP(ctl, 8);
         if (!s_fpfail) {
             if (tid == 0) {
-                const double uu = DBL_EPSILON / 2;
-                const double S = C.S, avg = C.avg, U0 = C.U0 + s_fpz[0];
-                const int nblm = C.nblm;
-                const double uerr = C.uerr + 8.0 * uu * (fabs(C.U0) + fabs(U0) + s_fpz[1]);
-                const double V = (C.V + s_fpz[2]) * (1.0 + 8.0 * uu);
-                const double E = (C.E + s_fpz[3]) * (1.0 + 8.0 * uu);
-                const double Rm = fmax(C.rm_bound, fmax(fabs(s_fpz[4]), fabs(s_fpz[5])));
-                const double u = DBL_EPSILON / 2;
-                const double n = (double)nblm;
-                const double R = Rm + a.wmax * iav;
-                const double Ea = E * iav;
-                const double epsf = 64.0 * u * ((n + 8.0) * (U0 + 2.0 * V) + 4.0 * (1.0 + R) * (1.0 + R));
-                const double epsl = 16.0 * Ea * (V / (n > 0 ? n : 1.0) + R + 1.0) + 4.0 * Ea * Ea;
-                double ep = 2.0 * (epsf + epsl) + uerr;
-                if (!(ep > 1e-300)) ep = 1e-300;
+                C.U0 = s_fpz[0]; C.uerr = s_fpz[1]; C.V = s_fpz[2]; C.E = s_fpz[3];
+                C.rm_bound = s_fpz[6]; C.eps = s_fpz[7];
                 C.rlo = fmin(C.rlo, s_fpz[4]); C.rhi = fmax(C.rhi, s_fpz[5]);
                 C.incr_ok = 0; C.wskip = 0.0;
                 C.ub_sub = a.ubdesc && a.R.n <= STEP_THREADS && (s_fpnsub > 0 || a.ub_heavy) ? 1 : 0;
-                C.S = S; C.avg = avg; C.U0 = U0; C.V = V; C.eps = ep; C.E = E;
-                C.uerr = uerr; C.rm_bound = Rm;
                 C.frz_n = C.frz_n + 1;
                 C.ub[0] = s_fpub[0] == NONE64 ? HUGE_VAL : dec(s_fpub[0]);
                 C.ub[1] = s_fpub[1] == NONE64 ? HUGE_VAL : dec(s_fpub[1]);
-                C.want_refresh = (epsl > epsf || C.ndirty >= 256) ? 1 : 0;
+                C.want_refresh = (s_fpz[8] != 0.0 || C.ndirty >= 256) ? 1 : 0;
                 C.ncont = 0;
                 C.cont_overflow = 0;
                 C.fp = 1;
@@ -3392,6 +3391,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
             // just resolved whose partition and brokers the applied move did not touch
             // are still candidates; re-scored on the new loads they bound the new minimum
             double ub0 = HUGE_VAL, ub1 = HUGE_VAL;
+            int nkeep = 0;
             if (bkeys) {
                 const long long pm = s_moved;
                 const bool keep_t = keep_touched_keys();
@@ -3407,10 +3407,8 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
                     BlockDesc d;
                     d.wmax = keep ? HUGE_VAL : -1.0;
                     d.blk = keep ? (long long)(c.iter >> 21) / BLK : 0;
-                    if (a.ubdesc) {
-                        stobj(a.ubdesc + 2 * tid + k, d);
-                        if (keep) atomicAdd(&s_nsub, 1);
-                    }
+                    if (a.ubdesc) stobj(a.ubdesc + 2 * tid + k, d);
+                    nkeep += keep ? 1 : 0;
                     if (!keep) continue;
                     if (!keep_t && ((s_fl[c.s] | s_fl[c.t]) & BF_TOUCHED)) continue;
                     const double d2 = cont_delta_ld(s_ld, c, iav);
@@ -3428,6 +3426,11 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
                 }
             }
             ub0 = wave_min(ub0); ub1 = wave_min(ub1);
+            // (the kept keys counted per wave: same-address LDS atomics of a whole wave serialise)
+            if (a.ubdesc) {
+                nkeep = wave_sum(nkeep);
+                if (lane == 0 && nkeep) atomicAdd(&s_nsub, nkeep);
+            }
             if (!frz && wid < NRW) {
                 su = wave_sum(su); v = wave_sum(v); rm = wave_max(rm);
                 rlo = wave_min(rlo); rhi = wave_max(rhi);

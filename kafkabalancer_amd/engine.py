@@ -30,7 +30,7 @@ EXPORTS = ["kb_abi_version", "kb_engine_create", "kb_engine_balance", "kb_engine
            "kb_engine_sharded_reset", "kb_engine_sharded_scan", "kb_engine_sharded_resolve",
            "kb_engine_sharded_collect", "kb_engine_set_incremental", "kb_engine_step",
            "kb_engine_host_timings", "kb_comm_unique_id", "kb_engine_comm_init", "kb_engine_sharded_plan",
-           "kb_set_diagnostics", "kb_diagnostics_enabled"]
+           "kb_set_diagnostics", "kb_diagnostics_enabled", "kb_engine_plan_until"]
 
 P64 = C.POINTER(C.c_int64)
 PD = C.POINTER(C.c_double)

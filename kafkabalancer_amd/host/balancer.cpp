@@ -168,7 +168,9 @@ StepResult Planner::Step() {
     return apply(ch, rc);
 }
 
-std::vector<StepResult> Planner::Plan(int64_t n) {
+std::vector<StepResult> Planner::Plan(int64_t n) { return PlanUntil(n, -1); }
+
+std::vector<StepResult> Planner::PlanUntil(int64_t n, int64_t pidx) {
     // in chunks: the change buffer stays bounded whatever -max-reassign asks for
     // (the reference loops until no change, kafkabalancer.go:177-233)
     constexpr int64_t kChunk = 4096;
@@ -177,12 +179,13 @@ std::vector<StepResult> Planner::Plan(int64_t n) {
     while (n > 0) {
         const int64_t m = std::min<int64_t>(n, kChunk);
         int64_t got = 0;
-        int rc = kb_engine_plan(eng_, m, chs.data(), &got);
+        int rc = kb_engine_plan_until(eng_, m, pidx, chs.data(), &got);
         for (int64_t i = 0; i < got; i++) {
             int s = chs[(size_t)i].status;
             int r = s == KB_CHANGE ? KB_CHANGE : (s == KB_NOCHANGE ? KB_NOCHANGE : rc);
             out.push_back(apply(chs[(size_t)i], r));
             if (r != KB_CHANGE) return out;
+            if (pidx >= 0 && chs[(size_t)i].partition != pidx) return out;
         }
         if (got == 0) {
             if (rc < 0) {

@@ -30,6 +30,9 @@ public:
     StepResult Step();
     // up to n Balance() calls device-resident; stops after a no-change or error
     std::vector<StepResult> Plan(int64_t n);
+    // ... and after the first change on a partition other than pidx (kb_engine_plan_until:
+    // the -complete-partition loop, kafkabalancer.go:193-221)
+    std::vector<StepResult> PlanUntil(int64_t n, int64_t pidx);
 
 private:
     StepResult apply(const kb_change& ch, int rc);

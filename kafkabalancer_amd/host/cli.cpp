@@ -326,9 +326,17 @@ int Run(const std::vector<std::string>& args, const std::function<std::string(bo
     int64_t iters = 0;
     const int64_t guard = max_reassign + 1000000;
     std::vector<StepResult> pending;
-    if (r > 0 && !cfg.complete_partition) pending = planner.Plan(r);   // device-resident fast path
+    // device-resident: the first -max-reassign changes in one plan (every mode: the completing
+    // logic starts only after them), then the -complete-partition loop in batches that stop
+    // after the first change on another partition (kb_engine_plan_until)
+    if (r > 0) pending = planner.Plan(r);
     size_t pi = 0;
+    int64_t cidx = -1;                                      // the completing partition's index
     while (r > 0) {                                         // MainLoop (kafkabalancer.go:181-221)
+        if (pi >= pending.size() && completing) {
+            pending = planner.PlanUntil(64, cidx);
+            pi = 0;
+        }
         StepResult sr = pi < pending.size() ? pending[pi++] : planner.Step();
         if (++iters > guard) {
             log.print("plan does not terminate: the reference loops forever on this input (-complete-partition)");
@@ -363,6 +371,7 @@ int Run(const std::vector<std::string>& args, const std::function<std::string(bo
             r = 1;
             if (!completing) {
                 cpart = opl.partitions.back();
+                cidx = sr.change.partition;
                 completing = true;
                 log.print("Forcing complete of Partition: " + cpart.str());
             }

@@ -13,7 +13,7 @@ for spec in "$@"; do
   [ "$lib" = "-" ] && lib=libkbengine.so
   ( export KB_ENGINE_LIB=$PWD/kafkabalancer_amd/lib/$lib
     IFS=','; for kv in $envs; do export "$kv"; done; unset IFS
-    timeout -k 10 200 python3 -u bench.py --workload $WL --steps $STEPS --warmup 20 --no-cpu-baseline > $O/$name.out 2>&1 ) || { echo "$name failed"; tail -5 $O/$name.out; exit 1; }
+    timeout -k 10 200 python3 -u bench.py --workload $WL --steps $STEPS --warmup 20 --no-cpu-baseline --no-secondary > $O/$name.out 2>&1 ) || { echo "$name failed"; tail -5 $O/$name.out; exit 1; }
   python3 -c "
 import json
 d=[json.loads(l) for l in open('$O/$name.out') if l.startswith('{')][0]
