@@ -1563,23 +1563,6 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
     KB_STAMP_BEGIN();
     __shared__ unsigned long long s_span_from;      // (kernel timing: the scan's end, or 0)
     __shared__ unsigned long long s_pair_from;      // (k_pair: its first workgroup's start, or 0)
-    auto write_back = [&]() {
-        KB_STAMP_FLUSH(ctl);
-        __syncthreads();
-        unsigned long long t_out = 0;
-        if (tid == 0 && C.tk_on) {
-            // kernel timing: this launch (the scan's interval was folded in at the start:
-            // a load here would wait for every store this thread issued)
-            t_out = wall_clock64();
-            C.tk_sum[1] += t_out - t_in;
-            C.tk_n[1]++;
-            if (s_span_from) { C.tk_span[1] += t_out - s_span_from; C.tk_span_n[1]++; }
-            if (s_pair_from && t_out > s_pair_from) { C.tk_pair += t_out - s_pair_from; C.tk_pair_n++; }
-        }
-        __syncthreads();
-        if (tid < CTL_WORDS) ((uint32_t*)ctl)[tid] = ((const uint32_t*)&C)[tid];
-        if (tid == 0 && t_out) ctl->ts_prev_end = t_out;
-    };
     // diagnostic phase stops: a -DKB_STOP_AT=k build returns after phase k (the code
     // after it is dead there); kb_engine_bench_step times such builds on a fixed input
 #ifdef KB_STOP_AT
@@ -1818,9 +1801,12 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
         if (tid < dnT) s_fl[s_T[tid]] &= ~BF_TOUCHED;
         __syncthreads();
     };
-    // the deferred prep's tables to memory (after the wait: the scan read the old ones)
-    auto flush_deferred = [&]() {
-        for (int i = tid; i < B; i += STEP_THREADS) {
+    // the deferred prep's tables to memory (after the wait: the scan read the old ones), by
+    // threads t0, t0 + nt, ... -- on the fast path by the waves the apply leaves idle, else
+    // before the first phase that reads them from memory (the general resolve) or at the end
+    __shared__ int s_flushed;
+    auto flush_deferred = [&](int t0, int nt) {
+        for (int i = t0; i < B; i += nt) {
             const int b = s_ord[i];
             a.order[i] = b;
             a.posu[b] = i;
@@ -1829,13 +1815,32 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
             if (p >= 0) st32(a.blm + p, (uint32_t)i);
         }
         const int U = a.units, n = s_dn * U;
-        for (int q = tid; q < n; q += STEP_THREADS) {
+        for (int q = t0; q < n; q += nt) {
             const int j = q / U, u = q - j * U;
             const int set = s_dlist[j];
             stobj(a.setrec + (size_t)set * U + u, s_rec[(size_t)set * U + u]);
         }
     };
-    if (tid == 0) s_dp = 0;
+    auto write_back = [&]() {
+        KB_STAMP_FLUSH(ctl);
+        __syncthreads();
+        // (a deferred prep whose tables no earlier phase of this launch flushed)
+        if (s_dp && !s_flushed) flush_deferred(tid, STEP_THREADS);
+        unsigned long long t_out = 0;
+        if (tid == 0 && C.tk_on) {
+            // kernel timing: this launch (the scan's interval was folded in at the start:
+            // a load here would wait for every store this thread issued)
+            t_out = wall_clock64();
+            C.tk_sum[1] += t_out - t_in;
+            C.tk_n[1]++;
+            if (s_span_from) { C.tk_span[1] += t_out - s_span_from; C.tk_span_n[1]++; }
+            if (s_pair_from && t_out > s_pair_from) { C.tk_pair += t_out - s_pair_from; C.tk_pair_n++; }
+        }
+        __syncthreads();
+        if (tid < CTL_WORDS) ((uint32_t*)ctl)[tid] = ((const uint32_t*)&C)[tid];
+        if (tid == 0 && t_out) ctl->ts_prev_end = t_out;
+    };
+    if (tid == 0) { s_dp = 0; s_flushed = 0; }
     unsigned long long ts_b, ts_e, ts_pe;
     if constexpr (FUSED) {
         // k_pair's step workgroup (a resident workgroup of the scan's grid): the broker tables
@@ -1945,7 +1950,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
         if (tid < CTL_WORDS) ((uint32_t*)&C)[tid] = ((const uint32_t*)ctl)[tid];
         if (s_prehalt == H_NEED_EXACT || !a.fuse_pre) stage_tables();
         else if (egb >= 0 && egb < B) { s_ld[egb] = a.load[egb]; s_e[egb] = a.eb[egb]; s_fl[egb] = a.bfl[egb]; }
-        if (s_dp) flush_deferred();
+
     } else {
     ts_b = ctl->ts_beg; ts_e = ctl->ts_end;         // (kernel timing, tk_on)
     ts_pe = ctl->ts_prev_end;
@@ -2001,8 +2006,8 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
         // the touched brokers' loads while the scan ran)
         if (!FUSED) stage_fp();
         deferred_prep(C.fp_t[0], C.fp_t[1]);
-        flush_deferred();
-        if (tid == 0) s_dp = 1;
+        flush_deferred(tid, STEP_THREADS);
+        if (tid == 0) { s_dp = 1; s_flushed = 1; }
         __syncthreads();
     }
     if (tid == 0 && (s_dp || C.fp)) {
@@ -2355,6 +2360,13 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
         }
         __syncthreads();
         if (!s_fast) {
+            // (the general path reads the bl positions / order from memory: a deferred prep's
+            // tables go out first)
+            if (s_dp && !s_flushed) {
+                flush_deferred(tid, STEP_THREADS);
+                __syncthreads();
+                if (tid == 0) s_flushed = 1;
+            }
             // ---- Validate(dup) / RemoveExtra / AddMissing / MoveDisallowed / ReassignLeaders
             if (tid == 0) {
                 const double su = U0h;
@@ -2996,6 +3008,11 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
             // next masked step resolves the same scan records, kb_engine_step)
             if (D.status != 1) { C.halted = H_DONE; if (!(D.status == 0 && sm != SM_ALL)) C.prepped = 0; }
             }
+        } else if (s_dp && !s_flushed) {
+            // (the fast path's flush: the waves the apply leaves idle; before the prep below,
+            // whose merged set records must land after the rebuilt ones)
+            flush_deferred(tid - 64, STEP_THREADS - 64);
+            if (tid == 64) s_flushed = 1;
         }
         __syncthreads();
         if (D.status != 1) { write_back(); return; }
