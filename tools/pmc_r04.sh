@@ -12,7 +12,7 @@ for wl in $WLS; do
   steps=200; [ "$wl" = "c5" ] && steps=100
   for grp in FETCH_SIZE WRITE_SIZE; do
     timeout -k 5 -s KILL 240 rocprofv3 --kernel-trace --pmc $grp --output-format csv -d gpurun_out/pmc_${wl}_$grp -o run \
-        -- python3 bench.py --workload $wl --steps $steps --warmup 5 --no-cpu-baseline \
+        -- python3 bench.py --workload $wl --steps $steps --warmup 5 --no-cpu-baseline --no-secondary \
         > gpurun_out/pmc_${wl}_$grp.log 2>&1 || exit $?
   done
   python3 tools/pmc_summarise.py pmc_$wl gpurun_out/pmc_traffic.json $wl $HEAD || exit $?

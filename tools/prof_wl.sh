@@ -7,7 +7,7 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 for w in ${WLS:-c3 c2}; do
   v=STEPS_$w; st=${!v:-$([ $w = c2 ] && echo 80 || echo 200)}
   O=gpurun_out/prof/$w; mkdir -p $O
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O -o run -- python3 -u bench.py --workload $w --steps $st --warmup 20 --no-cpu-baseline $EXTRA > $O/bench.out 2>&1 || { echo "$w failed"; tail -5 $O/bench.out; exit 1; }
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O -o run -- python3 -u bench.py --workload $w --steps $st --warmup 20 --no-cpu-baseline --no-secondary $EXTRA > $O/bench.out 2>&1 || { echo "$w failed"; tail -5 $O/bench.out; exit 1; }
   f=$(find $O -name 'run_kernel_stats.csv' | head -1)
   echo "== $w ($st steps): $f"
   python3 - "$f" <<'EOF'
