@@ -1981,6 +1981,9 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
         hflg &= 1u;
         const uint32_t nkk = ld32(&h->nkk[0]);
         hnk0 = nkk & 0xFFFFu; hnk1 = nkk >> 16;
+        // the best keys in the same round trip, straight to their LDS stash (the key count below
+        // and the fast prep's upper bound read them there), not in a second round trip
+        if (a.fp_lds && a.fp_bk) { s_bk[2 * tid] = ldobj(&h->best[0]); s_bk[2 * tid + 1] = ldobj(&h->best[1]); }
     }
     KB_STAMP(ctl, 28);
     dedup_clear(T);
@@ -2085,7 +2088,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
     // round trip so they are not held in registers through it
     Contender hb0, hb1;
     hb0.s = hb1.s = -1;
-    if (do_res && tid < a.R.n) { hb0 = ldobj(&a.R.h(tid)->best[0]); hb1 = ldobj(&a.R.h(tid)->best[1]); }
+    if (do_res && tid < a.R.n && !(a.fp_lds && a.fp_bk)) { hb0 = ldobj(&a.R.h(tid)->best[0]); hb1 = ldobj(&a.R.h(tid)->best[1]); }
     KB_STAMP(ctl, 12);
     KB_STOP(1);
     // ---- the scan records (or the gathered rank summaries): one per thread, reduced
@@ -2184,13 +2187,11 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
                 const bool q0 = hd0 <= g0 + 8.0 * eps, q1 = hd1 <= g1 + 8.0 * eps;
                 kc0 = q0 ? (int)hnk0 : 0;
                 kc1 = q1 ? (int)hnk1 : 0;
+                if (a.fp_lds && a.fp_bk) { hb0 = s_bk[2 * tid]; hb1 = s_bk[2 * tid + 1]; }   // (stashed with the headers)
                 // (a kind with one key overall: this record's best key is it; the write
                 // is meaningful only then)
                 if (kc0 && hb0.s >= 0) { s_single[0] = hb0; s_sok[0] = cont_delta_ld(s_ld, hb0, inv_avg) <= g0 + 4.0 * eps; }
                 if (kc1 && hb1.s >= 0) { s_single[1] = hb1; s_sok[1] = cont_delta_ld(s_ld, hb1, inv_avg) <= g1 + 4.0 * eps; }
-                // (the fast prep's upper bound re-scores them after the apply: an LDS stash now,
-                // no second load from memory then)
-                if (a.fp_lds && a.fp_bk) { s_bk[2 * tid] = hb0; s_bk[2 * tid + 1] = hb1; }
             }
             kc0 = wave_sum(kc0); kc1 = wave_sum(kc1);
             if (lane == 0) {
