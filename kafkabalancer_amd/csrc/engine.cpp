@@ -687,8 +687,13 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
         // (small shards -- scan tiles of fewer than 16 scoring waves, c2's 10k partitions --
         // keep two launches: there the hand-off measured slower than the launch boundary,
         // 0.0427 vs 0.0389 ms/step at c2, profiles/r04_c)
+        // (small shards too -- scan tiles of fewer than 16 scoring waves, c2's 10k partitions --
+        // since the fast / deferred prep runs in the fused step only: c2 0.0410 -> 0.0388 ms/step
+        // on one box, round 6; round 4 had measured the hand-off slower there without it)
+        bool small_fuse = true;
+        if (const char* v = diag_getenv("KB_FUSE_SMALL")) small_fuse = *v != '0';                  // A/B
         e->fuse = !e->gb && pair_supported(e->rc_dev) && e->nsets <= (int64_t)MAX_SETS &&
-                  full_shard && e->nscan > 1 && e->twaves == SCAN_THREADS / 64;
+                  full_shard && e->nscan > 1 && (e->twaves == SCAN_THREADS / 64 || small_fuse);
         if (const char* v = diag_getenv("KB_FUSE")) e->fuse = e->fuse && *v != '0';                      // A/B
         if (const char* v = diag_getenv("KB_FUSE_PRE")) e->fuse_pre = *v != '0';                          // diagnostic
         if (const char* v = diag_getenv("KB_PAIR_WAIT_TICKS")) e->pair_wait_ticks = strtoull(v, nullptr, 10);   // tests

@@ -2237,15 +2237,25 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
             }
             __syncthreads();
             const int tot = a.R.n * cap;
-            for (int x = tid; x < tot; x += STEP_THREADS) {
-                const int i = x / cap, k = x - i * cap;
-                const uint32_t rq = s_rq[i];
-                if (k >= (int)(rq >> 2)) continue;
-                const Contender c = ldobj(a.R.k(i) + k);
-                if (!((rq >> (c.kind ? 1 : 0)) & 1u)) continue;
+            // (two slots per thread and pass, both loads issued before either is used: one round
+            // trip for up to 2 * STEP_THREADS slots -- c2's 79 records of 16 slots took two)
+            auto take = [&](const Contender& c, uint32_t rq) {
+                if (!((rq >> (c.kind ? 1 : 0)) & 1u)) return;
                 if (cont_delta_ld(s_ld, c, inv_avg) <= (c.kind ? g1 : g0) + 4.0 * eps &&
                     dedup_insert(T, c.kind, c.s, c.t, c.w, c.iter) < 0)
                     s_kfail[c.kind] = 1;
+            };
+            for (int x0 = tid; x0 < tot; x0 += 2 * STEP_THREADS) {
+                const int x1 = x0 + STEP_THREADS;
+                const int i0 = x0 / cap, k0 = x0 - i0 * cap;
+                const int i1 = x1 < tot ? x1 / cap : i0, k1 = x1 - i1 * cap;
+                const uint32_t rq0 = s_rq[i0], rq1 = x1 < tot ? s_rq[i1] : 0u;
+                const bool v0 = k0 < (int)(rq0 >> 2), v1 = x1 < tot && k1 < (int)(rq1 >> 2);
+                Contender c0, c1;
+                if (v0) c0 = ldobj(a.R.k(i0) + k0);
+                if (v1) c1 = ldobj(a.R.k(i1) + k1);
+                if (v0) take(c0, rq0);
+                if (v1) take(c1, rq1);
             }
         } else {
             for (int i = tid; (need0 || need1) && i < a.R.n; i += STEP_THREADS) {
@@ -2476,10 +2486,24 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
                 __syncthreads();
             }
             // exact su (sequential folds in bl order); s_e doubles as the bl-ordered loads
-            // (every load is exact here, so every error bound is zero)
+            // (every load is exact here, so every error bound is zero).  k_pair with the deferred
+            // prep's region holds this state's bl positions in LDS (s_pm: staged before the wait,
+            // moved by a deferred prep): the bl-ordered loads are scattered from them and the
+            // contenders' positions read there, no round trip to memory
             double* s_Lm = s_e;
+            const bool pm_lds = FUSED && a.fp_lds;
+            auto bpos = [&](int b) -> int { return pm_lds ? (int)s_pm[b] : (int)ld32(a.posm + b); };
             auto stage_exact = [&]() {
-                for (int k = tid; k < nblm0; k += STEP_THREADS) s_Lm[k] = s_ld[(int)ld32(a.blm + k)];
+                if (pm_lds) {
+                    // (every error bound is zero: the positions' loads are read before any is
+                    // overwritten -- s_Lm aliases s_e, not s_ld)
+                    for (int b = tid; b < B; b += STEP_THREADS) {
+                        const int p = s_pm[b];
+                        if (p >= 0) s_Lm[p] = s_ld[b];
+                    }
+                } else {
+                    for (int k = tid; k < nblm0; k += STEP_THREADS) s_Lm[k] = s_ld[(int)ld32(a.blm + k)];
+                }
                 __syncthreads();
             };
             auto su_wave = [&]() {               // (wave 0, after stage_exact)
@@ -2625,8 +2649,8 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
                             auto put = [&](int pos, int h) {
                                 s_cl[pos] = (uint16_t)h;
                                 const uint32_t k = s_key[h];
-                                s_cps[pos] = (int16_t)(int32_t)ld32(a.posm + ((k >> 15) & 0x7FFF));
-                                s_cpt[pos] = (int16_t)(int32_t)ld32(a.posm + (k & 0x7FFF));
+                                s_cps[pos] = (int16_t)bpos((int)((k >> 15) & 0x7FFF));
+                                s_cpt[pos] = (int16_t)bpos((int)(k & 0x7FFF));
                             };
                             if (v0) put(woff + (int)__popcll(m0 & lt), h0);
                             if (v1) put(woff + (int)__popcll(m0) + (int)__popcll(m1 & lt), h1);
@@ -2637,7 +2661,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
                     if (wid == 0) su_wave();
                     if (!fail && ndist == 1) {
                         if (wid == 1) {
-                            const double u = exact_unb_w<GB>(s_Lm, nblm0, (int)ld32(a.posm + cw.s), (int)ld32(a.posm + cw.t),
+                            const double u = exact_unb_w<GB>(s_Lm, nblm0, bpos(cw.s), bpos(cw.t),
                                                                   s_ld[cw.s] - cw.w, s_ld[cw.t] + cw.w, s_fold + 64);
                             if (lane == 0) { s_dv[0] = u; atomicAdd(&C.total_folds, 1ull); }
                         }
@@ -2672,7 +2696,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
                                 for (int h = wid - 1; h < DEDUP_STEP; h += NW - 1) {
                                     if (!(s_key[h] != NONE32 && (int)(s_key[h] >> 30) == kind)) continue;
                                     const Contender c = dedup_entry(T, h);
-                                    const double u = exact_unb_w<GB>(s_Lm, nblm0, (int)ld32(a.posm + c.s), (int)ld32(a.posm + c.t),
+                                    const double u = exact_unb_w<GB>(s_Lm, nblm0, bpos(c.s), bpos(c.t),
                                                                           s_ld[c.s] - c.w, s_ld[c.t] + c.w, s_fold + 64 * wid);
                                     if (lane == 0) nf++;
                                     better(u, c);
@@ -2681,7 +2705,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
                             // (the spill path: per-thread folds over the records and the buffer)
                             __syncthreads();
                             for_each_contender(a, s_ld, C.ncont, kind, g, eps, inv_avg, [&](const Contender& c) {
-                                const double u = exact_unbalance_lds(s_Lm, nblm0, (int)ld32(a.posm + c.s), (int)ld32(a.posm + c.t),
+                                const double u = exact_unbalance_lds(s_Lm, nblm0, bpos(c.s), bpos(c.t),
                                                                      s_ld[c.s] - c.w, s_ld[c.t] + c.w);
                                 nf++;
                                 better(u, c);

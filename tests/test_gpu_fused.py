@@ -59,13 +59,6 @@ def test_fused_eager_checkpoints_match_two_launches():
     assert a[3] == b[3]
 
 
-def test_small_shard_keeps_two_launches():
-    cl, cfg, _ = synth.config("c2")
-    eng = E.Engine(cl, cfg)
-    assert eng.stats()["fused_pairs"] == 0
-    eng.close()
-
-
 def _with_env(name, value, fn):
     old = os.environ.get(name)
     os.environ[name] = value
@@ -76,6 +69,25 @@ def _with_env(name, value, fn):
             del os.environ[name]
         else:
             os.environ[name] = old
+
+
+def test_small_shard_fused_matches_two_launches():
+    """c2's 10k partitions (79 scan workgroups of one scoring wave) run as fused pairs since
+    round 6 (the fast / deferred prep exists only in the fused step); the plan, every
+    unbalance figure and the final state equal the two-launch path's (KB_FUSE_SMALL=0)."""
+    cl, cfg, _ = synth.config("c2")
+    out = []
+    for v in ("1", "0"):
+        eng = _with_env("KB_FUSE_SMALL", v, lambda: E.Engine(cl, cfg))
+        ch, err = eng.plan(100)
+        assert err is None, err
+        out.append((eng.stats()["fused_pairs"], ch, eng.state()))
+        eng.close()
+    (f1, c1, s1), (f0, c0, s0) = out
+    assert f1 == 1 and f0 == 0, (f1, f0)
+    assert len(c1) == 100
+    assert c1 == c0
+    assert s1 == s0
 
 
 def test_pair_timeout_poisons_engine():
