@@ -665,9 +665,9 @@ extern "C" int kb_engine_create(const kb_cluster* c, const kb_config* cfg, kb_en
         // the step's mark words)
         e->fp_lds = 0;
         e->fp_bk = 0;
-        const int fpb = (((int)e->B * 4 + 15) & ~15) + (int)e->nsets * 16;
+        const int fpb = (((int)e->B * 4 + 15) & ~15) + (int)e->nsets * 16 * e->units;
         const int fpk = (int)std::min<int64_t>(e->nscan, STEP_THREADS) * 2 * (int)sizeof(Contender);
-        bool fp = !e->gb && e->sb_lds && e->units == 1 && e->nsets <= 1024 &&
+        bool fp = !e->gb && e->sb_lds && e->units <= FP_MAXU && e->nsets <= 1024 &&
                   st_lds + e->step_lds_bytes + fpb <= lim;
         if (const char* v = diag_getenv("KB_FP")) fp = fp && *v != '0';                           // A/B
         if (fp) {

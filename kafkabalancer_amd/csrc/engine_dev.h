@@ -92,8 +92,16 @@ constexpr uint32_t MAX_SETS = 1u << 15;
 // Per-set target record, maintained by k_step (16-byte units, u16 fields):
 //   [0] nelig = |set ∩ bl_move|, [1] nl = valid ids, [2 .. 2+KR) the first KR
 //   brokers of set ∩ bl_move in bl order (dense ids, NONE16 past nl).
-// KR >= RC + 1 so the first eligible non-replica target is always inside.
-__host__ __device__ constexpr int sr_units(int rc) { return (rc + 1 + 2 + 7) / 8; }
+// KR >= RC + 1 so the first eligible non-replica target is always inside.  At least two
+// units (KR = 14): a census walk that passes the record's last entry goes on through the set's
+// membership words in memory, a round trip per four bl positions, and with KR = 6 the three c3
+// census workgroups walked ~1000 positions per step there (~2.5 us behind every other scan
+// workgroup); the scan's first-target pick reads only the first unit (RC + 1 <= 6).
+__host__ __device__ constexpr int sr_units(int rc) { return (rc + 1 + 2 + 7) / 8 > 2 ? (rc + 1 + 2 + 7) / 8 : 2; }
+// set-record units the fast prep's merge handles (engine.cpp: the deferred prep needs units <= this)
+constexpr int FP_MAXU = 2;
+// the units holding a record's first RC + 1 entries (the scan's first-target pick)
+__host__ __device__ constexpr int sr_units_first(int rc) { return (rc + 1 + 2 + 7) / 8; }
 __host__ __device__ constexpr int sr_kr(int rc) { return sr_units(rc) * 8 - 2; }
 
 struct Contender {                  // a near-tie candidate move (32 B)

@@ -718,10 +718,11 @@ __device__ void walk_targets(const ScanArgs& a, const Dedup& T, RF s_rf, PS s_po
 template <int RC, bool LSETS>
 __device__ __forceinline__ int first_target(const ScanArgs& a, const uint4* s_set, uint32_t set,
                                             const uint32_t (&reps)[RC], int nrep, int* nelig) {
-    constexpr int U = sr_units(RC);
+    constexpr int U = sr_units(RC), UF = sr_units_first(RC);
     constexpr int KT = RC + 1;
-    uint4 R[U];
-    set_record<RC, LSETS>(a, s_set, set, R);
+    uint4 R[UF];
+#pragma unroll
+    for (int u = 0; u < UF; u++) R[u] = LSETS ? s_set[set * U + u] : ldobj(a.setrec + (size_t)set * U + u);
     *nelig = (int)rec_u16(R, 0);
     // slots past nrep compare against an id no record holds (ids < MAXB_G, NONE16 = padding);
     // padding is never a replica, so it is picked only when no valid target precedes it
@@ -1606,7 +1607,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
     __shared__ int s_fpfail, s_fpnsub;
     __shared__ unsigned long long s_fpub[2];
     __shared__ double s_fpz[9];
-    __shared__ __align__(16) uint16_t s_mrow[NW][8];   // the fast prep's merged records, one row per wave
+    __shared__ __align__(16) uint16_t s_mrow[NW][8 * FP_MAXU];   // the fast prep's merged records, one row per wave
     Dedup T{s_key, s_wb, s_it, DEDUP_STEP, s_nd, s_li};
     const int B = a.B;
 
@@ -1632,7 +1633,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
     // scan reads posm / setrec while it runs).  The same phases as the prep below (P1-P5).
     int32_t* s_pm = (int32_t*)(dsm + (a.fp_lds ? a.fp_lds : 0));          // bl position per broker
     uint4* s_rec = (uint4*)(dsm + (a.fp_lds ? a.fp_lds + ((B * 4 + 15) & ~15) : 0));   // set records
-    Contender* s_bk = (Contender*)(s_rec + (a.fp_lds ? a.nsets : 0));   // the records' best keys (fp_bk)
+    Contender* s_bk = (Contender*)(s_rec + (a.fp_lds ? a.nsets * a.units : 0));   // the records' best keys (fp_bk)
     int* s_dlist = (int*)s_smark;                    // sets rebuilt (free until the resolve's exact folds)
     __shared__ int s_dp, s_dn, s_dpunc, s_dlight, s_dheavy, s_dwc[NW];
     auto stage_fp = [&]() {                          // (fp_lds: the positions and the set records)
@@ -3197,15 +3198,13 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
         const unsigned long long ltm = (1ull << lane) - 1ull;
         for (int g = wid; g < nmk; g += NW) {
             const int set = s_dlist[g];
-            const uint4 r4 = s_rec[set];                // (fp_lds: one 16-B unit per record)
-            const int nelig = (int)(r4.x & 0xFFFFu), nl = (int)(r4.x >> 16);
+            const uint16_t* r16 = (const uint16_t*)(s_rec + (size_t)set * a.units);   // (fp_lds: a.units 16-B units)
+            const int nelig = (int)r16[0], nl = (int)r16[1];
             const uint64_t* sb = s_sb + (size_t)set * a.W64;
             const bool in0 = (sb[t0 >> 6] >> (t0 & 63)) & 1ull;
             const bool in1 = t1 >= 0 && ((sb[t1 >> 6] >> (t1 & 63)) & 1ull);
-            const int j = lane < 6 ? lane : 5;
-            const uint32_t wj = j < 2 ? r4.y : (j < 4 ? r4.z : r4.w);
-            const int e = (int)((wj >> (16 * (j & 1))) & 0xFFFFu);
-            const bool v = lane < 6 && lane < nl && e != t0 && e != t1;
+            const int e = (int)r16[2 + (lane < KR ? lane : KR - 1)];
+            const bool v = lane < KR && lane < nl && e != t0 && e != t1;
             const int p = s_pm[v ? e : 0];
             const int pc = p - (o0 < p ? 1 : 0) - (o1 < p ? 1 : 0);
             const int pe = pc + (u0 <= pc ? 1 : 0) + (u1 <= pc ? 1 : 0);
@@ -3221,23 +3220,22 @@ __device__ __forceinline__ void step_body(const StepArgs& a, DevCtl& C) {
             const int kt = a.RC + 1 < nelig ? a.RC + 1 : nelig;
             if (nn < kt) { if (lane == 0) s_fpfail = 1; continue; }
             uint16_t* row = &s_mrow[wid][0];
-            if (lane < 8) row[lane] = NONE16;
+            if (lane < 8 * a.units) row[lane] = NONE16;
             __builtin_amdgcn_wave_barrier();
             const int idx = (int)__popcll(vm & ltm) + (c0 && n0 < pe ? 1 : 0) + (c1 && n1 < pe ? 1 : 0);
-            if (v && idx < 6) row[2 + idx] = (uint16_t)e;
+            if (v && idx < KR) row[2 + idx] = (uint16_t)e;
             const int i0 = (int)__popcll(__ballot(v && pe < n0)) + (c1 && n1 < n0 ? 1 : 0);
             const int i1 = (int)__popcll(__ballot(v && pe < n1)) + (c0 && n0 < n1 ? 1 : 0);
             if (lane == 0) {
-                if (c0 && i0 < 6) row[2 + i0] = (uint16_t)t0;
-                if (c1 && i1 < 6) row[2 + i1] = (uint16_t)t1;
+                if (c0 && i0 < KR) row[2 + i0] = (uint16_t)t0;
+                if (c1 && i1 < KR) row[2 + i1] = (uint16_t)t1;
                 row[0] = (uint16_t)nelig;
                 row[1] = (uint16_t)nn;
             }
             __builtin_amdgcn_wave_barrier();
-            if (lane == 0) {
-                uint4 rec = *(const uint4*)row;
+            if (lane < a.units) {
                 // (entries past nn: NONE16 -- the row held NONE16 before the writes, and nn <= KR)
-                stobj(a.setrec + set, rec);
+                stobj(a.setrec + (size_t)set * a.units + lane, *(const uint4*)(row + 8 * lane));
             }
             __builtin_amdgcn_wave_barrier();
         }
