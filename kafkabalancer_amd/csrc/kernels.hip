@@ -114,9 +114,14 @@ __device__ __forceinline__ T wave_max(T v) { return wave_red_max(v); }
 template <typename T>
 __device__ __forceinline__ T wave_sum(T v) { return wave_red_sum(v); }
 
-// u16 field idx of a set record held in registers / memory as 16-B units
-__device__ __forceinline__ uint32_t rec_u16(const uint4* v, int idx) {
-    const uint4 q = v[idx >> 3];
+// u16 field idx of a set record held in registers as U 16-B units (the unit picked by selects:
+// a runtime index into the register array would put it in scratch)
+template <int U>
+__device__ __forceinline__ uint32_t rec_u16(const uint4 (&v)[U], int idx) {
+    uint4 q = v[0];
+#pragma unroll
+    for (int u = 1; u < U; u++)
+        if ((idx >> 3) == u) q = v[u];
     const int c = (idx >> 1) & 3;
     const uint32_t word = c == 0 ? q.x : (c == 1 ? q.y : (c == 2 ? q.z : q.w));
     return (idx & 1) ? (word >> 16) : (word & 0xFFFFu);
@@ -654,18 +659,20 @@ __device__ __forceinline__ void set_record(const ScanArgs& a, const uint4* s_set
 // walk every allowed, non-replica target in bl order for one (partition, slot)
 // and emit the ones within 4*eps of the tile minimum g; stop once 8*eps is
 // exceeded (the approximate delta is monotone in the target load up to 2*eps).
-template <int RC, typename RF, typename PS, typename BL>
+// (ENT: the record's u16 field by index -- from LDS where the set records are staged, else
+// from registers)
+template <int RC, typename RF, typename PS, typename BL, typename ENT>
 __device__ void walk_targets(const ScanArgs& a, const Dedup& T, RF s_rf, PS s_pos,
-                             BL s_blm, const uint4 (&R)[sr_units(RC)], int kind, long long p,
+                             BL s_blm, ENT ent, int kind, long long p,
                              int slot, int src, const uint32_t (&reps)[RC], int nrep, int set, double w, double ds,
                              double g, double eps, double inv_avg, int nblm) {
     const unsigned long long ib = ((unsigned long long)p << 21) | ((unsigned long long)slot << 16);
     const double delta = w * inv_avg;
-    const int nl = (int)rec_u16(R, 1);
+    const int nl = (int)ent(1);
     int last = -1;
     KB_COUNT_WALK(a.ctl, 29, 1);
     for (int i = 0; i < nl; i++) {                // the set's first KR eligible brokers
-        const int b = (int)rec_u16(R, 2 + i);
+        const int b = (int)ent(2 + i);
         KB_COUNT_WALK(a.ctl, 28, 1);
         last = b;
         bool isrep = false;
@@ -678,7 +685,7 @@ __device__ void walk_targets(const ScanArgs& a, const Dedup& T, RF s_rf, PS s_po
     }
     // (the record lists the whole set, or the walk continues past its last member: a record
     // the fast prep merged may list fewer than KR members of a larger set)
-    if (nl >= (int)rec_u16(R, 0) || last < 0) return;
+    if (nl >= (int)ent(0) || last < 0) return;
     // rare: more than KR near-tied targets -- the walk goes on in bl order through the set's
     // membership words in memory, LA positions per round trip (their broker ids, then their
     // words, all in flight together): a set of 64 in 1000 brokers has a member every ~16
@@ -837,6 +844,7 @@ __device__ __forceinline__ void scan_round(const ScanArgs& a, const ScanParams& 
     __shared__ uint32_t s_nk;
     __shared__ unsigned long long s_benc[2];
     __shared__ uint32_t s_bslot[2], s_nkk[2];
+    __shared__ uint32_t s_fw[NW][NF];                // per wave: its first-index predicate minima
     __shared__ unsigned long long s_bke[2][NW];      // per wave and kind: its best non-census key
     __shared__ Contender s_bkc[2][NW];
 
@@ -883,6 +891,7 @@ __device__ __forceinline__ void scan_round(const ScanArgs& a, const ScanParams& 
     if (tid == 0) s_nk = 0;
     if (tid < 2) { s_benc[tid] = NONE64; s_bslot[tid] = NONE32; s_nkk[tid] = 0; }
     if (tid < 2 * NW) (&s_bke[0][0])[tid] = NONE64;
+    if (tid < NW * NF) (&s_fw[0][0])[tid] = NONE32;
     __shared__ unsigned long long s_cz[3];           // diagnostic (a.wgt): census clocks, waves, walk clocks
     if (tid < 3) s_cz[tid] = 0;
     const bool run = q.run != 0;
@@ -916,9 +925,12 @@ __device__ __forceinline__ void scan_round(const ScanArgs& a, const ScanParams& 
     const double prune_t = (a.dbg & 16) ? HUGE_VAL : ubP + 16.0 * eps;    // dbg 16: no pruning
 
     double wgL = HUGE_VAL, wgN = HUGE_VAL;
+    // the first-index predicates (rare once the plan is in shape): a wave's minima in LDS,
+    // not eight registers held through the scoring loop (they pushed its loop-invariant
+    // census thresholds to scratch, reloaded inside the loop behind a vmcnt(0) that also
+    // waited for the prefetched tile)
     uint32_t fst[NF];
-#pragma unroll
-    for (int f = 0; f < NF; f++) fst[f] = NONE32;
+    auto fmin_ = [&](int f, uint32_t v) { if (v != NONE32) atomicMin(&s_fw[wid][f], v); };
     unsigned long long cL = 0, cN = 0;
 
     // score one tile held in P (partitions base, base + 1 of this lane)
@@ -927,7 +939,7 @@ __device__ __forceinline__ void scan_round(const ScanArgs& a, const ScanParams& 
             uint32_t x = P.m.x ^ P.m.y ^ (uint32_t)__double2hiint(P.w.x) ^ (uint32_t)__double2hiint(P.w.y);
 #pragma unroll
             for (int k = 0; k < RC; k++) x ^= P.r[k];
-            fst[F_DUP] = min(fst[F_DUP], x | 0x80000000u);
+            fmin_(F_DUP, x | 0x80000000u);
             return;
         }
         double lL = HUGE_VAL, lN = HUGE_VAL;
@@ -998,16 +1010,16 @@ __device__ __forceinline__ void scan_round(const ScanArgs& a, const ScanParams& 
                     for (int x = 0; x < RC; x++)
 #pragma unroll
                         for (int y = x + 1; y < RC; y++) dup |= (y < nrep) && P.rp(x, j) == P.rp(y, j);
-                    if (dup) fst[F_DUP] = min(fst[F_DUP], pi);
+                    if (dup) fmin_(F_DUP, pi);
                 }
-                if (want < nrep) fst[F_REMOVE] = min(fst[F_REMOVE], pi);
-                if (want > nrep) fst[F_ADD] = min(fst[F_ADD], pi);
+                if (want < nrep) fmin_(F_REMOVE, pi);
+                if (want > nrep) fmin_(F_ADD, pi);
                 if (nrep == 0) {
-                    fst[F_EMPTY] = min(fst[F_EMPTY], pi);
-                    if (elig) fst[F_EMPTY_ELIG] = min(fst[F_EMPTY_ELIG], pi);
+                    fmin_(F_EMPTY, pi);
+                    if (elig) fmin_(F_EMPTY_ELIG, pi);
                 }
-                if (meta_dis(m)) fst[F_DIS] = min(fst[F_DIS], pi);
-                if (a.rebalance && elig && nrep > 0 && (int)P.rp(0, j) == heavy) fst[F_LEAD] = min(fst[F_LEAD], pi);
+                if (meta_dis(m)) fmin_(F_DIS, pi);
+                if (a.rebalance && elig && nrep > 0 && (int)P.rp(0, j) == heavy) fmin_(F_LEAD, pi);
             }
         }
         // branch-free: every lane scores both partitions; invalid ones are masked
@@ -1146,10 +1158,17 @@ __device__ __forceinline__ void scan_round(const ScanArgs& a, const ScanParams& 
 #pragma unroll
                 for (int q2 = 1; q2 < RC; q2++) src = k == q2 ? reps[q2] : src;
                 const int nrep = (int)meta_nrep(m), set = (int)set_of<RC, LSETS>(P, j);
-                uint4 R[U];
-                set_record<RC, LSETS>(a, s_set, (uint32_t)set, R);
+                // (the record's fields: LDS reads where it is staged -- a runtime index into
+                // a register copy of its units went through scratch)
+                uint4 R[LSETS ? 1 : U];
+                if (!LSETS) set_record<RC, LSETS>(a, s_set, (uint32_t)set, *(uint4(*)[U])R);
+                const uint16_t* rs = (const uint16_t*)(s_set + (size_t)set * U);
+                auto ent = [&](int idx) -> uint32_t {
+                    if constexpr (LSETS) return rs[idx];
+                    else return rec_u16(*(const uint4(*)[U])R, idx);
+                };
                 const double ds = dsrc_f(s_rf[src], w * inv_avg);
-                walk_targets<RC>(a, T, s_rf, s_pos, s_blm, R, k ? 1 : 0, base + j, k, (int)src, reps, nrep,
+                walk_targets<RC>(a, T, s_rf, s_pos, s_blm, ent, k ? 1 : 0, base + j, k, (int)src, reps, nrep,
                                       set, w, ds, k ? tN : tL, eps, inv_avg, nblm);
             }
             if (a.wgt && lane == __ffsll((long long)__ballot(1)) - 1) {   // (the census lanes' first)
@@ -1215,7 +1234,7 @@ __device__ __forceinline__ void scan_round(const ScanArgs& a, const ScanParams& 
     }
     bool anyf = false;
 #pragma unroll
-    for (int f = 0; f < NF; f++) anyf |= fst[f] != NONE32;
+    for (int f = 0; f < NF; f++) { fst[f] = s_fw[wid][f]; anyf |= fst[f] != NONE32; }
     if (__ballot(anyf)) {                          // first-index predicates are rare
 #pragma unroll
         for (int f = 0; f < NF; f++) fst[f] = wave_min(fst[f]);
