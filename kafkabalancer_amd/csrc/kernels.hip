@@ -4411,7 +4411,11 @@ __device__ __attribute__((noinline)) void refresh_in_scan(const RefreshArgs* rfp
 __device__ bool eager_edit_refold(const RefreshArgs& rf, int b, int op, uint32_t q, ListExt& x, double* buf, int cap) {
     const uint32_t st = x.st, n = x.n, nt = blockDim.x;
     const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
-    if (n + 1 > LIST_K * nt || (int)n + 1 + 32 > cap) return false;   // (+32: the chain's read-ahead)
+    // LDS: two chunks of contributions (a ring, +32 for the chain's read-ahead), then the new
+    // list's partition ids from position base on
+    constexpr int ECH = 1024;
+    uint32_t* ids = (uint32_t*)(buf + 2 * ECH + 32);
+    if (n + 1 > LIST_K * nt || 2 * ECH + 32 + ((int)n + 2) / 2 > cap) return false;
     if (op == 2 && n >= rf.L.lcap[b]) return false;          // (the general path reports it)
     __shared__ int s_at;
     __shared__ double s_acc0;
@@ -4441,7 +4445,7 @@ __device__ bool eager_edit_refold(const RefreshArgs& rf, int b, int op, uint32_t
     const uint32_t nn = op == 1 ? n - 1 : (op == 2 ? n + 1 : n);
     const uint32_t dp = (uint32_t)at < x.dp ? (uint32_t)at : x.dp;
     const uint32_t base = (dp < nn ? dp : nn) & ~63u;
-    // the edit's stores, and the contributions of the new positions >= base
+    // the edit's stores, and the new list's partition ids from position base on (LDS)
 #pragma unroll
     for (int k = 0; k < LIST_K; k++) {
         const uint32_t i = k * nt + tid;
@@ -4449,32 +4453,50 @@ __device__ bool eager_edit_refold(const RefreshArgs& rf, int b, int op, uint32_t
         uint32_t np = i;
         if (op == 1) { if (i == (uint32_t)at) continue; if (i > (uint32_t)at) { np = i - 1; rf.L.lent[st + np] = v[k]; } }
         if (op == 2 && i >= (uint32_t)at) { np = i + 1; rf.L.lent[st + np] = v[k]; }
-        if (np >= base) {
-            const uint32_t pp = v[k];
-            const double w = rf.w[pp];
-            const uint32_t m = rf.meta[pp];
-            const int32_t ncp = rf.nc[pp];
-            const uint16_t r0 = rf.rep[pp];
-            buf[np - base] = r0 == (uint16_t)b ? w * (double)((int)meta_nrep(m) + ncp) : w;
-        }
+        if (np >= base) ids[np - base] = v[k];
     }
     if (tid == 0) {
         if (op == 2) {
             rf.L.lent[st + at] = q;
-            if ((uint32_t)at >= base) {
-                const double w = rf.w[q];
-                const uint32_t m = rf.meta[q];
-                const int32_t ncp = rf.nc[q];
-                const uint16_t r0 = rf.rep[q];
-                buf[at - base] = r0 == (uint16_t)b ? w * (double)((int)meta_nrep(m) + ncp) : w;
-            }
+            if ((uint32_t)at >= base) ids[at - base] = q;
         }
         rf.L.llen[b] = nn;
         s_acc0 = base ? rf.L.ck[st + base - 1] : 0.0;
     }
+    // The contributions (getBrokerLoad's terms, utils.go:92-105: slot 0 carries the leader
+    // weight W * (len(R) + NumConsumers)) are gathered a chunk ahead of the chain: waves 1..
+    // gather chunk c + 1 from the partition words into the ring's other half while wave 0 folds
+    // chunk c in order -- the random partition-word loads (~half the refold's time at c5,
+    // 7300-entry lists) overlap the add-latency-bound chain instead of preceding it
+    const int mtot = (int)(nn - base);
+    auto gather = [&](int c1, int c2, int t, int ntt) {
+        double* dst = buf + ((c1 / ECH) & 1) * ECH - c1;
+        for (int i = c1 + t; i < c2; i += ntt) {
+            const uint32_t pp = ids[i];
+            const double w = rf.w[pp];
+            const uint32_t m = rf.meta[pp];
+            const int32_t ncp = rf.nc[pp];
+            const uint16_t r0 = rf.rep[pp];
+            dst[i] = r0 == (uint16_t)b ? w * (double)((int)meta_nrep(m) + ncp) : w;
+        }
+    };
     __syncthreads();
+    gather(0, mtot < ECH ? mtot : ECH, tid, (int)nt);
+    __syncthreads();
+    double acc = s_acc0;
+    for (int c0 = 0; c0 < mtot; c0 += ECH) {
+        const int c1 = c0 + ECH < mtot ? c0 + ECH : mtot;
+        if (wid > 0) {
+            gather(c1, c1 + ECH < mtot ? c1 + ECH : mtot, tid - 64, (int)nt - 64);
+        } else {
+            // (in-order chain over the chunk's ring slot; checkpoints relative to its start, a
+            // multiple of 64; the read-ahead past its end reads the other slot, unused)
+            acc = chain_lds_ck(acc, (const lds_f64*)(buf + ((c0 / ECH) & 1) * ECH), c1 - c0,
+                               rf.L.ck + st + base + c0, lane);
+        }
+        __syncthreads();
+    }
     if (wid == 0) {
-        const double acc = chain_lds_ck(s_acc0, (const lds_f64*)buf, (int)(nn - base), rf.L.ck + st + base, lane);
         if (lane == 0) {
             rf.load[b] = acc;
             rf.lerr[b] = gamma_n((int)nn) * acc;
