@@ -989,7 +989,7 @@ static void enqueue_scan(kb_engine* e, bool rf = false) {
 
 // the first step after a full prep has no best keys to bound its minimum: a
 // census-free scan (no list op) plus k_ubinit sets ub to the step's own minima
-static void enqueue_ubinit(kb_engine* e, bool rf = false) {
+static void enqueue_ubinit(kb_engine* e, bool rf = false, bool tighten = false) {
     if (e->nscan == 0) return;
     mark(e, TK_BOUND);
     ScanArgs s;
@@ -998,14 +998,14 @@ static void enqueue_ubinit(kb_engine* e, bool rf = false) {
     s.listwg = 0;
     s.eager = 0;                      // (the main scan launch refolds)
     s.dbg |= 1;
-    s.ubpass = 1;
+    s.ubpass = tighten ? 2 : 1;
     // (set records in LDS: the block-list kernel, which scans only the blocks of the last
     // records' best keys when k_step left them, DevCtl.ub_sub)
     s.incr = e->lds_sets ? 1 : 0;
     s.bdesc = e->ubdesc;
     s.nblk = (int)e->nubdesc;
     launch_scan(s, e->rc_dev, e->lds_sets, e->scan_lds, e->st);
-    launch_ubinit(e->ctl, scan_recs(e->recs, (int)e->nscan), e->allow_leader, e->st);
+    launch_ubinit(e->ctl, scan_recs(e->recs, (int)e->nscan), e->allow_leader, tighten ? 1 : 0, e->st);
 }
 
 static void enqueue_step(kb_engine* e, bool rf = false) {
@@ -1932,6 +1932,9 @@ static int grow_summary(kb_engine* e) {
                       " near-tied candidates in one rank summary";
         return KB_ERR_CAPACITY;
     }
+    // (an open census bound spilled on some rank -- the gathered flags, alike on every rank:
+    // bound passes from now on; a pass only ever tightens this rank's own census)
+    if (c.cont_overflow || any_growable) e->ub_mode = true;
     if (c.cont_overflow && e->cont_cap < kContMax) {
         const int rc = grow_spill(e);
         if (rc != KB_OK) return rc;
@@ -1959,6 +1962,15 @@ extern "C" int kb_engine_set_stream(kb_engine* e, void* s) {
 // this rank's scan and its summary into summary_dev: one k_scansum launch (the summary
 // workgroup waits in the scan's grid), or k_scan then k_summary
 static int enqueue_scan_summary(kb_engine* e, void* summary_dev) {
+    // the tightening bound pass (a census-free scan, then ub = min(ub, this shard's minima)):
+    // a rank's prep bounds the next minimum with its one gathered summary's few keys, which
+    // at thousands of brokers either share a broker with the applied move (an open bound)
+    // or sit far above the minimum -- either way most waves then pass the census gate and
+    // spill (c5 at world size 1: 64M spilled keys through the summary workgroup, ~0.2-0.5 s
+    // per step, before this pass).  The rank's own minima are a valid census bound for its
+    // own scan (its summary holds the keys within 4 eps of its own minima); the resolve
+    // reads ub only for its -inf state, which the pass leaves alone.
+    if (e->ub_mode || e->B >= 2048) enqueue_ubinit(e, false, true);
     SumArgs s;
     s.ctl = e->ctl; s.R = scan_recs(e->recs, (int)e->nscan); s.cont = e->cont; s.cont_cap = e->cont_cap;
     s.r = e->r; s.B = (int)e->B; s.out = summary_recs((unsigned char*)summary_dev, 1, e->sum_keys);

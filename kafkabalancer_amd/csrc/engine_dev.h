@@ -294,9 +294,15 @@ struct DevCtl {
     if (threadIdx.x < 29) _kb_st[threadIdx.x] = 0;                              \
     if (threadIdx.x == 0) { _kb_st[29] = clock64(); _kb_st[30] = wall_clock64(); } \
     KB_STAMP(ctl, 26)
+// (the shader clock by inline asm: clock64() made the compiler wait vmcnt(0) before the
+// stamp's LDS write, charging outstanding stores to the phase that issued them)
 #define KB_STAMP(ctl, i)                                                        \
     do {                                                                        \
-        if (threadIdx.x == 0) _kb_st[i] = clock64();                            \
+        if (threadIdx.x == 0) {                                                 \
+            unsigned long long _t;                                              \
+            asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t));    \
+            _kb_st[i] = _t;                                                     \
+        }                                                                       \
     } while (0)
 #define KB_STAMP_FLUSH(ctl)                                                     \
     do {                                                                        \

@@ -901,7 +901,7 @@ __device__ __forceinline__ void scan_round(const ScanArgs& a, const ScanParams& 
     const bool tk_on = q.tk_on != 0;
     __syncthreads();
     const bool ub_open = ubN == HUGE_VAL || (a.allow_leader && ubL == HUGE_VAL);
-    if (!run || (a.dbg & 4) || (a.ubpass && !ub_open)) return;
+    if (!run || (a.dbg & 4) || (a.ubpass == 1 && !ub_open)) return;
     const bool census_off = (a.dbg & 1) || q.ubpass;
     // (bound keys are for the next step's census bound: none when this step's bound is
     // -inf -- the step after a first-index stage, whose successor is almost always one too
@@ -1394,7 +1394,7 @@ __device__ __forceinline__ void scan_kernel_body(const ScanArgs& a) {
     const CtlK cc = (CtlK)ctl;
     // a conditional bound pass returns at once unless a bound is open: decided before
     // any partition word is loaded (it runs before every scan once a plan retried)
-    if (a.ubpass) {
+    if (a.ubpass == 1) {                 // (2: the sharded engines' tightening pass, every scan)
         const double ubL = cc->ub[0], ubN = cc->ub[1];
         const int h = cc->halted;
         if (!(ubN == HUGE_VAL || (a.allow_leader && ubL == HUGE_VAL))) {
@@ -4886,7 +4886,9 @@ __global__ __launch_bounds__(1024) void k_touch(double* r, int B, int32_t* blm, 
 // valid for the census gate (tL <= ub + 12 eps) and the prune (LB > ub + 16 eps).
 // Only a bound that is +inf is set (the records are this pass's only when a bound
 // was open: otherwise the bound pass returned at once and they are stale).
-__global__ __launch_bounds__(256) void k_ubinit(DevCtl* ctl, Recs R, int allow_leader) {
+// (tighten: the sharded engines' pass runs on every scan and lowers a finite bound too -- a
+// rank's bound from its one gathered summary's few keys can sit far above its minimum)
+__global__ __launch_bounds__(256) void k_ubinit(DevCtl* ctl, Recs R, int allow_leader, int tighten) {
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const bool run = ctl->halted == H_RUN && ctl->prepped && ctl->steps < ctl->budget;
     if (!run) return;                            // uniform over the workgroup
@@ -4908,16 +4910,22 @@ __global__ __launch_bounds__(256) void k_ubinit(DevCtl* ctl, Recs R, int allow_l
         }
         m0 = s_m[0][0] < m0 ? s_m[0][0] : m0;
         m1 = s_m[1][0] < m1 ? s_m[1][0] : m1;
-        const bool open1 = ctl->ub[1] == HUGE_VAL, open0 = allow_leader && ctl->ub[0] == HUGE_VAL;
-        if (open0 || open1) {                    // the bound pass ran on this state
-            if (open0) ctl->ub[0] = m0;
-            if (open1) ctl->ub[1] = m1;
+        const double u0 = ctl->ub[0], u1 = ctl->ub[1];
+        if (tighten) {                           // (-inf: census off, left alone)
+            if (u1 != -HUGE_VAL && m1 < u1) ctl->ub[1] = m1;
+            if (allow_leader && u0 != -HUGE_VAL && m0 < u0) ctl->ub[0] = m0;
+        } else {
+            const bool open1 = u1 == HUGE_VAL, open0 = allow_leader && u0 == HUGE_VAL;
+            if (open0 || open1) {                // the bound pass ran on this state
+                if (open0) ctl->ub[0] = m0;
+                if (open1) ctl->ub[1] = m1;
+            }
         }
     }
 }
 
-void launch_ubinit(DevCtl* ctl, const Recs& R, int allow_leader, hipStream_t st) {
-    hipLaunchKernelGGL(k_ubinit, dim3(1), dim3(256), 0, st, ctl, R, allow_leader);
+void launch_ubinit(DevCtl* ctl, const Recs& R, int allow_leader, int tighten, hipStream_t st) {
+    hipLaunchKernelGGL(k_ubinit, dim3(1), dim3(256), 0, st, ctl, R, allow_leader, tighten);
 }
 
 void launch_touch(double* r, int B, int32_t* blm, int32_t* posm, uint4* setrec, int nrec, hipStream_t st) {

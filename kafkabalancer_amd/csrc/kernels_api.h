@@ -157,7 +157,7 @@ int pair_blocks_per_cu(int rc, bool lds_sets, size_t lds_bytes, int* static_lds)
 void launch_pair(const ScanArgs& a, const StepArgs& sa, int rc, bool lds_sets, size_t lds_bytes, hipStream_t st);
 int step_static_lds(bool gb);
 // diagnostic: one workgroup rewrites the given tables in place (n = 0: nothing)
-void launch_ubinit(DevCtl* ctl, const Recs& R, int allow_leader, hipStream_t st);
+void launch_ubinit(DevCtl* ctl, const Recs& R, int allow_leader, int tighten, hipStream_t st);
 void launch_touch(double* r, int B, int32_t* blm, int32_t* posm, uint4* setrec, int nrec, hipStream_t st);
 void launch_listop(DevCtl* ctl, const Lists& L, hipStream_t st);
 void launch_refresh(const RefreshArgs& a, hipStream_t st);

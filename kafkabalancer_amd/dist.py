@@ -313,6 +313,7 @@ def bench_world1(args, cpu_baseline=None):
     (buf, n, rc), wall_s = _timed(eng.sharded_plan_raw, args.steps)
     sh_changes, err = eng.changes(buf, n, rc)
     assert err is None, err
+    sh_stats = eng.stats()
     eng.close()
     ref = E.Engine(cl, cfg, device=0)
     _plan_or_raise(ref.plan, args.warmup)
@@ -327,6 +328,8 @@ def bench_world1(args, cpu_baseline=None):
            "ms_per_step_sharded": 1e3 * wall_s / steps, "ms_per_step_plain": 1e3 * wall_p / max(1, len(pl_changes)),
            "ratio": (wall_s / steps) / (wall_p / max(1, len(pl_changes))), "steps": steps, "warmup": args.warmup,
            "plans_equal": key(sh_changes) == key(pl_changes), "plain_fused_pairs": fused,
+           "sharded_stats": {k: sh_stats.get(k) for k in ("refreshes", "exact_halts", "exact_folds", "retries",
+                                                         "spill_grows", "eager", "fast_preps", "relists")},
            "def": "kb_engine_sharded_plan (scan + k_summary, ncclAllGather on a 1-rank communicator, k_step "
                   "resolve; 64 rounds per host round trip) vs kb_engine_plan, same warm-up and steps"}
     print(json.dumps(out), flush=True)
