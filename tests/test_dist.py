@@ -559,6 +559,54 @@ def test_rccl_sharded_plan_from_c_matches_oracle():
     assert st == opl.state()
 
 
+def _rccl_wide_worker(steps, q):
+    """A world-1 sharded plan at 2500 brokers (the tightening bound pass on every scan)
+    next to the plain plan of the same cluster, in one child process."""
+    try:
+        torch.cuda.set_device(0)
+        from kafkabalancer_amd import engine as E
+        from kafkabalancer_amd import synth
+        cl = synth.make_cluster(20000, 2500, 3, "zipf", seed=0x5EED00B5)
+        cfg = {"allow_leader": False, "rebalance_leaders": False, "min_replicas": 2, "min_unbalance": 0.0,
+               "brokers": None}
+        uid = E.comm_unique_id()
+        eng = E.Engine(cl, cfg, shard=shard_bounds(cl.n, 1, 0))
+        eng.comm_init(1, 0, uid)
+        a, err = eng.sharded_plan(steps)
+        assert err is None, err
+        sh = ([(c["step"], c["pidx"], c["kind"], c["from_"], c["to"], c["slot"]) for c in a], eng.state(),
+              eng.stats()["spill_grows"])
+        eng.close()
+        ref = E.Engine(cl, cfg)
+        b, err = ref.plan(steps)
+        assert err is None, err
+        pl = ([(c["step"], c["pidx"], c["kind"], c["from_"], c["to"], c["slot"]) for c in b], ref.state())
+        ref.close()
+        q.put((sh, pl, None))
+    except Exception as ex:                        # reported to the parent, not swallowed
+        q.put((None, None, repr(ex)))
+
+
+@pytest.mark.gpu
+def test_rccl_sharded_plan_wide_brokers_matches_plain():
+    """Sharded engines at B >= 2048 run the tightening bound pass before every scan (a rank's
+    bound from its one gathered summary is open or loose there, and the census spilled
+    every wave: c5 0.2 s per step): same plan and state as the plain engine, no spill
+    growth."""
+    steps = 24
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_wide_worker, args=(steps, q))
+    p.start()
+    sh, pl, err = q.get(timeout=300)
+    p.join(timeout=60)
+    assert err is None, err
+    assert len(sh[0]) == steps
+    assert sh[0] == pl[0]
+    assert sh[1] == pl[1]
+    assert sh[2] == 0
+
+
 @pytest.mark.gpu
 def test_bench_sharded_world1_line():
     """`bench.py --sharded`: the world-1 sharded protocol line, with the sharded plan equal
