@@ -244,6 +244,65 @@ def test_two_engines_one_gpu_batched_protocol():
 
 
 
+def _protocol_plan(cl, cfg, world, steps):
+    """The batched protocol with host-staged summaries over `world` shards of one process:
+    (the plan of rank 0, every rank's plan, every engine's final state)."""
+    from kafkabalancer_amd import engine as E
+    engs = [E.Engine(cl, cfg, shard=shard_bounds(cl.n, world, r)) for r in range(world)]
+    got = [[] for _ in range(world)]
+    done = False
+    while not done and len(got[0]) < steps:
+        nb = engs[0].summary_bytes()
+        summ = [torch.zeros(nb, dtype=torch.uint8, device="cuda") for _ in range(world)]
+        gathered = torch.zeros(world * nb, dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()
+        batch = min(8, steps - len(got[0]))
+        for e in engs:
+            e.sharded_reset(batch)
+        for _ in range(batch):
+            for e, b in zip(engs, summ):
+                e.sharded_scan(b.data_ptr())
+            torch.cuda.synchronize()
+            for r in range(world):
+                gathered[r * nb:(r + 1) * nb].copy_(summ[r])
+            torch.cuda.synchronize()
+            for e in engs:
+                e.sharded_resolve(gathered.data_ptr(), world)
+            torch.cuda.synchronize()
+        res = [e.sharded_collect(batch + 1) for e in engs]
+        assert len({st for st, _ in res}) == 1, [st for st, _ in res]
+        for r in range(world):
+            got[r].extend(res[r][1])
+        done = res[0][0] == "done"
+    states = [e.state() for e in engs]
+    grows = [e.stats()["spill_grows"] for e in engs]
+    for e in engs:
+        e.close()
+    return got, states, grows
+
+
+@pytest.mark.gpu
+def test_sharded_protocol_wide_brokers_two_shards_matches_plain():
+    """Two shards at 2500 brokers: each rank's tightening bound pass sets its own census
+    bound from its own shard (the ranks' bounds differ), yet both ranks apply the same plan
+    -- the plain engine's -- and end in its state, with no spill growth."""
+    from kafkabalancer_amd import engine as E
+    from kafkabalancer_amd import synth
+    cl = synth.make_cluster(20000, 2500, 3, "zipf", seed=0x5EED00B6)
+    cfg = default_cfg(allow_leader=False, min_unbalance=0.0)
+    steps = 24
+    got, states, grows = _protocol_plan(cl, cfg, 2, steps)
+    ref = E.Engine(cl, cfg)
+    want, err = ref.plan(steps)
+    assert err is None, err
+    key = lambda c: (c["step"], c["pidx"], c["kind"], c["from_"], c["to"], c["slot"])
+    assert [key(c) for c in got[1]] == [key(c) for c in got[0]]
+    assert [key(c) for c in got[0]] == [key(c) for c in want]
+    assert states[0] == states[1] == ref.state()
+    assert grows == [0, 0]
+    ref.close()
+
+
 def _gpu_cluster():
     from kafkabalancer_amd import synth
     cl = synth.make_cluster(2500, 40, 3, "zipf", nsets=8, set_size=24, seed=5, with_names=True)
