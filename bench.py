@@ -327,11 +327,25 @@ def spawn_ranks(args):
     """`bench.py --gpus N` without a launcher: run N ranks under torch.distributed.run as a
     child process (one process per GPU, rendezvous on 127.0.0.1) and exit with its status.
     Nothing here touches the GPU: the ranks initialise their own devices."""
+    import random
     import socket
     import subprocess
-    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
-        so.bind(("127.0.0.1", 0))
-        port = so.getsockname()[1]
+    # (a port below the ephemeral range: one the kernel hands out for bind(0) can be taken
+    # by an outgoing connection before the launcher binds it -- EADDRINUSE, seen once)
+    port = None
+    for _ in range(64):
+        cand = random.randrange(20000, 30000)
+        with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+            try:
+                so.bind(("127.0.0.1", cand))
+            except OSError:
+                continue
+        port = cand
+        break
+    if port is None:
+        with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+            so.bind(("127.0.0.1", 0))
+            port = so.getsockname()[1]
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(args.gpus),
            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
     env = dict(os.environ)
