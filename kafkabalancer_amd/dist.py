@@ -13,6 +13,7 @@ step_begin, step_finish) so the exchange logic is testable with a CPU engine
 over gloo (tests/test_dist.py).
 """
 import json
+import os
 import time
 
 TILE = 1024
@@ -249,6 +250,7 @@ def bench_main(args, world, rank, local, cpu_baseline=None):
         st1["n_sets"] * ((st1["n_brokers"] + 63) // 64) * 8
     round_us = 1e3 * (dev_ms if dev_ms else wall * 1e3) / steps
     achieved = b8d / (round_us * 1e-6) / 1e9
+    tr1, tr_src = _round_traffic(args.workload)
     if rank == 0:
         out = {
             "metric": "candidate moves scored/sec (+ ms per reassignment step)",
@@ -270,9 +272,11 @@ def bench_main(args, world, rank, local, cpu_baseline=None):
                                                                               if rccl else "gloo, host-staged")),
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": 8000.0 * world, "unit": "GB/s",
                          "frac": achieved / (8000.0 * world),
-                         # (PMC passes are 1-GPU runs: profiles/pmc_traffic.json carries the world-1
-                         # sharded protocol's per-launch traffic where one was taken)
-                         "traffic": None,
+                         # (PMC passes are 1-GPU runs: the world-1 sharded round's k_scansum + k_step,
+                         # tools/pmc_sharded.sh; at N > 1 a rank scans 1/N of it, so only the world-1
+                         # line carries it as its traffic, the others beside it)
+                         "traffic": tr1 if world == 1 else None,
+                         "traffic_world1_round": tr1, "traffic_source": tr_src,
                          "kernel": "one sharded round: k_scansum (scan + rank summary) + ncclAllGather + k_step "
                                    "(resolve), whole cluster on %d GPUs" % world,
                          "bytes_per_launch": b8d,
@@ -294,6 +298,20 @@ def bench_main(args, world, rank, local, cpu_baseline=None):
         print(json.dumps(out), flush=True)
     dist.barrier()
     dist.destroy_process_group()
+
+
+def _round_traffic(workload):
+    """HBM-side bytes of one world-1 sharded round (k_scansum + k_step) from the committed
+    PMC passes (profiles/pmc_traffic.json["<workload>_sharded"]): (bytes, source) or (None, None)."""
+    try:
+        root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+        with open(os.path.join(root, "profiles", "pmc_traffic.json")) as f:
+            d = json.load(f)[workload + "_sharded"]
+        b = d["k_scansum"]["traffic_bytes_per_launch"] + d["k_step"]["traffic_bytes_per_launch"]
+        return b, "profiles/pmc_traffic.json[%s_sharded] (k_scansum + k_step per round, git %s)" % (
+            workload, d.get("git_head"))
+    except (OSError, KeyError, ValueError, TypeError):
+        return None, None
 
 
 def bench_world1(args, cpu_baseline=None):

@@ -17,6 +17,8 @@ def kernel_key(name):
     """k_scan = the full-scan instantiations (k_scan<RC, LSETS, false, GT>); k_scan_bound = the
     block-list instantiation (k_scan<RC, LSETS, true, GT>: the conditional bound passes and the
     incremental mode); k_pair (the fused scan + step launch); k_step; k_ubinit."""
+    if "k_scansum" in name:                 # (the sharded scan + rank summary launch)
+        return "k_scansum"
     if "k_scan" in name:
         params = name.replace(" ", "").split("<", 1)[-1].split(">")[0].split(",")
         return "k_scan_bound" if len(params) > 2 and params[2] == "true" else "k_scan"
