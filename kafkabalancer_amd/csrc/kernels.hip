@@ -4414,7 +4414,8 @@ __device__ bool eager_edit_refold(const RefreshArgs& rf, int b, int op, uint32_t
     // LDS: two chunks of contributions (a ring, +32 for the chain's read-ahead), then the new
     // list's partition ids from position base on.  (Chunks of 512: the gather before the first
     // fold and the last chunk's fold after the last gather are what the overlap leaves
-    // exposed -- c5 eager workgroup 42.4 us at 1024, 38.0 at 512, 39.7 at 256, 45.0 at 2048)
+    // exposed -- c5 eager workgroup 42.4 us at 1024, 38.0-38.7 at 512, 39.1 at 384, 39.7 at
+    // 256, 41.5 at 768, 45.0 at 2048)
     constexpr int ECH = 512;
     uint32_t* ids = (uint32_t*)(buf + 2 * ECH + 32);
     if (n + 1 > LIST_K * nt || 2 * ECH + 32 + ((int)n + 2) / 2 > cap) return false;
